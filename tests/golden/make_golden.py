@@ -1,0 +1,420 @@
+"""Generate the golden fixtures in tests/golden/ by running the REAL reference.
+
+Runs only in the development container (it reads /root/reference, which never
+travels to the GPU box).  The reference imports dgl, wandb and torchvision,
+none of which are installed; they are replaced by the stubs below.  The DGL
+stub keeps exactly the graph API the hot path touches
+(``pinsage_model.py:41,44,93``; ``spotify_graph.py:48-63``): successors in
+edge-insertion order (stable COO->CSR), ``number_of_nodes``, ``edges``.
+
+Outputs are plain ``.npz`` files (no pickle): inputs and expected outputs only.
+
+    python tests/golden/make_golden.py            # all fixtures
+    python tests/golden/make_golden.py walk topk  # a subset
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import shutil
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+
+def _load_synthetic():
+    spec = importlib.util.spec_from_file_location(
+        "_pinsage_synthetic", os.path.join(REPO, "gcn-song-embeddings_amd", "synthetic.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["_pinsage_synthetic"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+syn = _load_synthetic()
+
+
+# ----------------------------------------------------------------------------- stubs
+class _StubDGLGraph:
+    """Minimal DGLGraph: the subset the reference's PinSage path calls."""
+
+    def __init__(self):
+        self._n = 0
+        self._src = np.zeros(0, np.int64)
+        self._dst = np.zeros(0, np.int64)
+        self._csr = None
+
+    def add_nodes(self, n):
+        self._n += int(n)
+
+    def add_edges(self, u, v):
+        self._src = np.concatenate([self._src, np.asarray(u, np.int64)])
+        self._dst = np.concatenate([self._dst, np.asarray(v, np.int64)])
+        self._csr = None
+
+    def number_of_nodes(self):
+        return self._n
+
+    def _build(self):
+        if self._csr is None:
+            order = np.argsort(self._src, kind="stable")
+            indptr = np.zeros(self._n + 1, np.int64)
+            np.cumsum(np.bincount(self._src, minlength=self._n), out=indptr[1:])
+            self._csr = (indptr, self._dst[order].copy())
+        return self._csr
+
+    def successors(self, v):
+        indptr, indices = self._build()
+        v = int(v)
+        return torch.from_numpy(indices[indptr[v]:indptr[v + 1]])
+
+    def edges(self):
+        return torch.from_numpy(self._src.copy()), torch.from_numpy(self._dst.copy())
+
+
+def _install_stubs():
+    dgl = types.ModuleType("dgl")
+    dgl.DGLGraph = _StubDGLGraph
+    sys.modules["dgl"] = dgl
+    wandb = types.ModuleType("wandb")
+    wandb.init = lambda *a, **k: None
+    wandb.watch = lambda *a, **k: None
+    wandb.log = lambda *a, **k: None
+    sys.modules["wandb"] = wandb
+    tv = types.ModuleType("torchvision")
+    tv_io = types.ModuleType("torchvision.io")
+    tv_img = types.ModuleType("torchvision.io.image")
+    tv_img.ImageReadMode = object
+    tv.io = tv_io
+    tv_io.image = tv_img
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.io"] = tv_io
+    sys.modules["torchvision.io.image"] = tv_img
+
+
+def _import_reference():
+    _install_stubs()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import pinsage_model as ref_psm  # noqa: E402
+    import pinsage_training as ref_pt  # noqa: E402
+    import spotify_graph as ref_sg  # noqa: E402
+    return ref_psm, ref_pt, ref_sg
+
+
+def stub_graph(pg):
+    g = _StubDGLGraph()
+    g.add_nodes(pg.n_all)
+    src, dst = pg.edge_arrays()
+    g.add_edges(src, dst)
+    return g
+
+
+def next_draws(n=4):
+    """Raw 32-bit draws that follow, to pin how many draws a call consumed."""
+    return np.array([int(torch.randint(2 ** 31, ())) for _ in range(n)], np.int64)
+
+
+# ----------------------------------------------------------------------------- graphs
+# G_small: N_all = 360 -> topk partial_sort only for k*64 <= 360 (k=3), nth_element above.
+# G_mid:   N_all ~ 8.5k -> partial_sort for every k <= 132.
+GRAPHS = {
+    "small": dict(n_tracks=300, n_cols=60, n_memberships=1500, seed=11),
+    "mid": dict(n_tracks=7000, n_cols=1500, n_memberships=40000, seed=12),
+}
+
+
+def graph_arrays(name):
+    pg = syn.make_playlist_graph(**GRAPHS[name])
+    indptr, indices = pg.csr()
+    src, dst = pg.edge_arrays()
+    return pg, dict(n_tracks=pg.n_tracks, n_cols=pg.n_cols, indptr=indptr, indices=indices,
+                    src=src, dst=dst)
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    sz = os.path.getsize(path)
+    print(f"wrote {path} ({sz/1024:.1f} KiB)")
+
+
+# ----------------------------------------------------------------------------- fixtures
+def fx_walk(ref_psm, ref_pt, ref_sg):
+    for gname, n_src, seed in (("small", 40, 1234), ("mid", 24, 99)):
+        pg, ga = graph_arrays(gname)
+        g = stub_graph(pg)
+        rng = np.random.default_rng(seed)
+        nodeset = torch.from_numpy(rng.integers(0, pg.n_tracks, n_src).astype(np.int64))
+        torch.manual_seed(seed)
+        trace = ref_psm.do_random_walks(g, nodeset, 500, 0.85)
+        after = next_draws()
+        # alpha edge cases: always restart (1.0) / never restart (0.0)
+        torch.manual_seed(seed + 1)
+        trace_a1 = ref_psm.do_random_walks(g, nodeset[:8], 60, 1.0)
+        torch.manual_seed(seed + 2)
+        trace_a0 = ref_psm.do_random_walks(g, nodeset[:8], 60, 0.0)
+        save(f"walk_{gname}", **ga, nodeset=nodeset.numpy(), seed=seed, n_hops=500, alpha=0.85,
+             trace=trace.numpy(), after=after, trace_a1=trace_a1.numpy(), trace_a0=trace_a0.numpy())
+
+
+def fx_topk(ref_psm, ref_pt, ref_sg):
+    ks = [1, 3, 10, 25, 50, 100]
+    for gname, n_src, seed, n_hops in (("small", 16, 7, 500), ("mid", 48, 8, 500)):
+        pg, ga = graph_arrays(gname)
+        g = stub_graph(pg)
+        rng = np.random.default_rng(seed)
+        nodeset = torch.from_numpy(rng.integers(0, pg.n_tracks, n_src).astype(np.int64))
+        torch.manual_seed(seed)
+        vp = ref_psm.sample_neighborhood(g, pg.n_tracks, nodeset, n_hops, 0.85)
+        after = next_draws()
+        out = dict(ga, nodeset=nodeset.numpy(), seed=seed, n_hops=n_hops, alpha=0.85, after=after,
+                   ks=np.array(ks))
+        # store the dense visit_prob sparsely: (row, col, value)
+        r, c = torch.nonzero(vp, as_tuple=True)
+        out.update(vp_row=r.numpy(), vp_col=c.numpy(), vp_val=vp[r, c].numpy(), vp_shape=np.array(vp.shape))
+        for k in ks:
+            v, i = vp.topk(k, 1)
+            out[f"val_{k}"] = v.numpy()
+            out[f"idx_{k}"] = i.numpy()
+        # the composite API call, reseeded: (values, indices) namedtuple
+        torch.manual_seed(seed)
+        tk = ref_psm.sample_neighborhood_topt(g, pg.n_tracks, nodeset, n_hops, 0.85, 10)
+        out["topt_val"] = tk.values.numpy()
+        out["topt_idx"] = tk.indices.numpy()
+        save(f"topk_{gname}", **out)
+
+
+def fx_precompute(ref_psm, ref_pt, ref_sg):
+    for gname, seed, n_hops in (("small", 21, 500), ("mid", 22, 100)):
+        pg, ga = graph_arrays(gname)
+        g = stub_graph(pg)
+        tmp = tempfile.mkdtemp()
+        try:
+            torch.manual_seed(seed)
+            w, nb = ref_psm.precompute_neighborhoods_topt(g, pg.n_tracks, n_hops, 0.85, 100,
+                                                          os.path.join(tmp, "nb.pt"))
+            after = next_draws()
+        finally:
+            shutil.rmtree(tmp)
+        save(f"precompute_{gname}", **ga, seed=seed, n_hops=n_hops, alpha=0.85, T=100,
+             weights=w.numpy(), nodes=nb.numpy(), after=after)
+
+
+def fx_frontier(ref_psm, ref_pt, ref_sg):
+    d = np.load(os.path.join(HERE, "precompute_mid.npz"))
+    nbhds = (torch.from_numpy(d["weights"]), torch.from_numpy(d["nodes"]))
+    rng = np.random.default_rng(31)
+    out = {}
+    for case, (B, L, T) in enumerate([(20, 1, 3), (20, 2, 3), (20, 3, 3), (64, 2, 10), (7, 3, 25),
+                                      (1, 2, 3)]):
+        nodeset = torch.from_numpy(rng.integers(0, 7000, B).astype(np.int64))
+        if B > 4:
+            nodeset[1] = nodeset[0]  # duplicates are kept at the top layer
+        S = ref_psm.relevant_nodes_per_layer_precomp(nodeset, L, T, nbhds)
+        out[f"c{case}_nodeset"] = nodeset.numpy()
+        out[f"c{case}_LT"] = np.array([L, T])
+        for l, (ns, w, nb) in enumerate(S):
+            out[f"c{case}_l{l}_nodes"] = ns.numpy()
+            out[f"c{case}_l{l}_w"] = w.numpy()
+            out[f"c{case}_l{l}_nb"] = nb.numpy()
+    # on-the-fly sampling version (commented out in the reference forward, a6)
+    pg, ga = graph_arrays("small")
+    g = stub_graph(pg)
+    nodeset = torch.from_numpy(rng.integers(0, pg.n_tracks, 6).astype(np.int64))
+    torch.manual_seed(41)
+    S = ref_psm.relevant_nodes_per_layer(g, pg.n_tracks, nodeset, 2, 100, 0.85, 3)
+    out["fly_nodeset"] = nodeset.numpy()
+    out["fly_after"] = next_draws()
+    for l, (ns, w, nb) in enumerate(S):
+        out[f"fly_l{l}_nodes"] = ns.numpy()
+        out[f"fly_l{l}_w"] = w.numpy()
+        out[f"fly_l{l}_nb"] = nb.numpy()
+    save("frontier", **out)
+
+
+def _model_state(model):
+    return {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def fx_model(ref_psm, ref_pt, ref_sg):
+    d = np.load(os.path.join(HERE, "precompute_mid.npz"))
+    nbhds = (torch.from_numpy(d["weights"]), torch.from_numpy(d["nodes"]))
+    n = 7000
+    feats = torch.from_numpy(syn.make_features(n, 24, seed=5))
+    out = {"features_sum": np.float64(feats.double().sum())}  # regenerated by the tests
+    rng = np.random.default_rng(51)
+    for L in (1, 2, 3):
+        torch.manual_seed(100 + L)
+        model = ref_psm.PinSageModel(None, n, L, (24, 32, 16), 500, 0.85, 5, nbhds)
+        nodeset = torch.from_numpy(rng.integers(0, n, 20).astype(np.int64))
+        nodeset[3] = nodeset[7]
+        y = model(feats, nodeset)
+        # gradients of a fixed linear functional of the output
+        cvec = torch.from_numpy(rng.standard_normal(y.shape).astype(np.float32))
+        (y * cvec).sum().backward()
+        out[f"L{L}_nodeset"] = nodeset.numpy()
+        out[f"L{L}_out"] = y.detach().numpy()
+        out[f"L{L}_cvec"] = cvec.numpy()
+        for k, v in _model_state(model).items():
+            out[f"L{L}_p_{k}"] = v
+        for k, p in model.named_parameters():
+            out[f"L{L}_g_{k}"] = p.grad.numpy().copy()
+    # a single ConvLayer call with raw inputs
+    torch.manual_seed(7)
+    conv = ref_psm.ConvLayer(24, 16, 32)
+    ns = torch.from_numpy(rng.integers(0, n, 11).astype(np.int64))
+    w, nb = nbhds[0][ns, :4], nbhds[1][ns, :4]
+    yc = conv(feats, ns, nb, w)
+    out.update(conv_nodeset=ns.numpy(), conv_out=yc.detach().numpy(),
+               **{f"conv_p_{k}": v.detach().numpy() for k, v in conv.state_dict().items()})
+    save("model", **out)
+
+
+def fx_train(ref_psm, ref_pt, ref_sg):
+    """Two reference train_batch steps of the real PinSage trainer (default dims)."""
+    d = np.load(os.path.join(HERE, "precompute_mid.npz"))
+    pg, ga = graph_arrays("mid")
+    g = stub_graph(pg)
+    tmp = tempfile.mkdtemp()
+    cwd = os.getcwd()
+    try:
+        os.chdir(tmp)
+        os.mkdir("runs")
+        g.nbhds_path = os.path.join(tmp, "nb.pt")
+        g.base_dir = tmp
+        torch.save((torch.from_numpy(d["weights"]), torch.from_numpy(d["nodes"])), g.nbhds_path)
+        # d_in must be >= out_dim (128) or put_embeddings fails (pinsage_model.py:27-29)
+        feats = torch.from_numpy(syn.make_features(pg.n_tracks, 128, seed=6))
+        positives = torch.from_numpy(syn.make_positives(pg, 5 * pg.n_tracks, seed=7))
+        torch.manual_seed(2024)
+        tr = ref_pt.PinSage(g, pg.n_tracks, feats, positives, log=False, load_save=False)
+        out = dict(features_sum=np.float64(feats.double().sum()),
+                   positives_sum=np.int64(positives.sum()), init_seed=2024)
+        for k, v in _model_state(tr.model).items():
+            out[f"init_{k}"] = v
+        torch.manual_seed(77)
+        for step in range(2):
+            batch, nodeset = ref_pt.sample_batch(tr.all_ids, tr.positives, tr.batch_size, tr.nbhds,
+                                                 hard_negatives=tr.hard_negatives)
+            loss, nfl, var = tr.train_batch(batch)
+            out[f"s{step}_batch"] = batch.numpy()
+            out[f"s{step}_loss"] = np.float64(loss.item())
+            out[f"s{step}_nfl"] = np.float64(nfl.item())
+            out[f"s{step}_var"] = np.float64(var.item())
+            if step == 0:
+                for k, p in tr.model.named_parameters():
+                    out[f"s0_g_{k}"] = p.grad.numpy().copy()
+        for k, v in _model_state(tr.model).items():
+            out[f"s1_p_{k}"] = v
+        out["after"] = next_draws()
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+    save("train", **out)
+
+
+def fx_batch(ref_psm, ref_pt, ref_sg):
+    pg, _ = graph_arrays("mid")
+    positives = torch.from_numpy(syn.make_positives(pg, 5 * pg.n_tracks, seed=7))
+    all_ids = torch.arange(0, pg.n_tracks, dtype=torch.int64)
+    out = dict(positives=positives.numpy(), n_items=pg.n_tracks)
+    torch.manual_seed(5)
+    for i, bs in enumerate((128, 512, 1)):
+        batch, nodeset = ref_pt.sample_batch(all_ids, positives, bs, None, hard_negatives=False)
+        out[f"b{i}_bs"] = bs
+        out[f"b{i}_batch"] = batch.numpy()
+        out[f"b{i}_nodeset"] = nodeset.numpy()
+    out["after"] = next_draws()
+    # raw randperm and randint semantics pinned directly
+    torch.manual_seed(9)
+    out["randperm_37"] = torch.randperm(37).numpy()
+    out["randperm_5000"] = torch.randperm(5000).numpy()
+    out["randperm_after"] = next_draws()
+    torch.manual_seed(10)
+    out["rand_f32"] = np.array([torch.rand(()).item() for _ in range(16)], np.float32)
+    torch.manual_seed(10)
+    out["raw_u32"] = np.array([int(torch.randint(2 ** 32, ())) for _ in range(16)], np.int64)
+    save("batch", **out)
+
+
+def fx_loss(ref_psm, ref_pt, ref_sg):
+    rng = np.random.default_rng(61)
+    out = {}
+    for i, (B, d) in enumerate([(8, 16), (128, 128), (2, 4)]):
+        hq, hp, hn = (torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).requires_grad_()
+                      for _ in range(3))
+        margin = 1e-5 if i != 1 else 0.3
+        loss = ref_pt.max_margin_loss(hq, hp, hn, margin)
+        loss.backward()
+        out.update({f"c{i}_hq": hq.detach().numpy(), f"c{i}_hp": hp.detach().numpy(),
+                    f"c{i}_hn": hn.detach().numpy(), f"c{i}_margin": np.float64(margin),
+                    f"c{i}_loss": np.float64(loss.item()), f"c{i}_gq": hq.grad.numpy(),
+                    f"c{i}_gp": hp.grad.numpy(), f"c{i}_gn": hn.grad.numpy()})
+    save("loss", **out)
+
+
+def fx_dataset(ref_psm, ref_pt, ref_sg):
+    """SpotifyGraph.to_dgl_graph / load_positives on a synthetic JSON triple that
+    reuses the real track ids of dataset_micro/positives.json."""
+    import json
+    with open(os.path.join(REF, "dataset_micro", "positives.json"), encoding="utf-8") as f:
+        pos = json.load(f)
+    ids = []
+    seen = set()
+    for p in pos:
+        for t in (p["a"], p["b"]):
+            if t not in seen:
+                seen.add(t)
+                ids.append(t)
+    n = len(ids)
+    pg = syn.make_playlist_graph(n, 500, 9000, seed=13)
+    tmp = tempfile.mkdtemp()
+    try:
+        ds_dir = os.path.join(tmp, "ds")
+        syn.write_spotify_dataset(ds_dir, pg, track_ids=ids, seed=14)
+        # features: one .pt per track (generate_node_features.py:120-128 format)
+        fdir = os.path.join(ds_dir, "features_test")
+        os.makedirs(fdir)
+        raw = np.random.default_rng(15).standard_normal((n, 8)).astype(np.float32) * 3 + 1
+        for i, tid in enumerate(ids):
+            torch.save(torch.from_numpy(raw[i].copy()), os.path.join(fdir, tid + ".pt"))
+        shutil.copy(os.path.join(REF, "dataset_micro", "positives.json"), os.path.join(ds_dir, "positives.json"))
+        ds = ref_sg.SpotifyGraph(ds_dir, fdir)
+        g, track_ids, col_ids, features = ds.to_dgl_graph()
+        torch.manual_seed(3)
+        positives = ds.load_positives(os.path.join(ds_dir, "positives.json"))
+        after = next_draws()
+        tr, te = ds.load_positives_split(os.path.join(ds_dir, "positives.json"))
+        src, dst = g.edges()
+        succ69 = g.successors(69).numpy()
+    finally:
+        shutil.rmtree(tmp)
+    save("dataset", track_ids=np.array(ids), n_cols=500, graph_seed=13, json_seed=14, feat_seed=15,
+         src=src.numpy().astype(np.int32), dst=dst.numpy().astype(np.int32), features=features.numpy(),
+         positives=positives.numpy(), after=after, split_train=tr.numpy(), split_test=te.numpy(),
+         succ69=succ69, n_track_ids=len(track_ids), col_ids=np.array(col_ids))
+
+
+FIXTURES = {"walk": fx_walk, "topk": fx_topk, "precompute": fx_precompute, "frontier": fx_frontier,
+            "model": fx_model, "train": fx_train, "batch": fx_batch, "loss": fx_loss,
+            "dataset": fx_dataset}
+
+
+def main(argv):
+    refs = _import_reference()
+    names = argv or list(FIXTURES)
+    for name in names:
+        print(f"== {name}")
+        FIXTURES[name](*refs)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
