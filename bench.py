@@ -1,0 +1,275 @@
+"""PinSAGE train-step throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--no-cpu-baseline]
+
+A step = sample_batch (reference RNG semantics, host) + PinSage.train_batch
+(fused HIP forward of the query/positive/negative ids, loss, backward, Adam)
+on a synthetic playlist graph resident in HBM.  N > 1: one process per GPU
+(torch.distributed over RCCL), each rank trains batch_size triples per step
+(weak scaling), gradients all-reduced.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gcn-song-embeddings_amd"))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # BASELINE.json configs[1]: dataset_final_intersect-like, 2-layer, fanout 10, batch 512
+    "c2": dict(workload="synthetic dataset_final_intersect-scale playlist graph, 2-layer PinSAGE, "
+                        "fanout 10, batch 512", n_tracks=100_000, n_cols=25_000,
+               memberships=1_000_000, d_in=512, n_layers=2, T=10, batch=512),
+    "c3": dict(workload="synthetic dataset_large-scale playlist graph, 2-layer PinSAGE, fanout 25, "
+                        "batch 2048", n_tracks=1_000_000, n_cols=250_000, memberships=10_000_000,
+               d_in=512, n_layers=2, T=25, batch=2048),
+    "c4": dict(workload="synthetic 10M nodes / 100M edges, 128-d features, 2-layer, per-GPU batch 512",
+               n_tracks=8_000_000, n_cols=2_000_000, memberships=50_000_000, d_in=128, n_layers=2,
+               T=10, batch=512),
+}
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(n_gpus):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world
+
+
+def build_problem(cfg, seed=0):
+    import graph
+    import synthetic
+    t0 = time.time()
+    pg = synthetic.make_playlist_graph(cfg["n_tracks"], cfg["n_cols"], cfg["memberships"], seed=seed)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices)
+    rng = np.random.default_rng(seed + 1)
+    feats = torch.from_numpy(rng.standard_normal((cfg["n_tracks"], cfg["d_in"]), dtype=np.float32))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 5 * cfg["n_tracks"], seed=seed + 2))
+    log(f"[bench] graph n_all={pg.n_all} edges={pg.n_edges} built in {time.time()-t0:.1f}s")
+    return pg, g, feats, pos
+
+
+def precompute(g, cfg, mode):
+    import pinsage_model as pm
+    pm.set_rng_mode(mode)
+    torch.manual_seed(0)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):  # progress prints must not reach the JSON line
+        nb = pm.precompute_neighborhoods_topt(g, cfg["n_tracks"], pm.DEF_HOPS, pm.DEF_ALPHA,
+                                              pm.DEF_T_PRECOMP, None)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    pm.set_rng_mode("mt19937")
+    return nb, dt
+
+
+def kernel_table(engine):
+    import ctypes
+    import _native as nat
+    L = nat.lib()
+    L.pinsage_engine_timing_collect(engine.h)
+    out = {}
+    i = 0
+    name = ctypes.create_string_buffer(128)
+    ms = ctypes.c_double()
+    calls = ctypes.c_int64()
+    while L.pinsage_engine_timing_get(engine.h, i, name, 128, ctypes.byref(ms), ctypes.byref(calls)) == 0:
+        out[name.value.decode()] = (ms.value, calls.value)
+        i += 1
+    return out
+
+
+def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
+    """The oracle's restatement of the reference train step (dense clone
+    put_embeddings, f64 aggregation, torch CPU) on the same workload."""
+    from oracle import oracle as orc
+    import pinsage_model as pm
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1)
+    dims = (cfg["d_in"], 512, 128)
+    tmp = {}
+    in_dims = [dims[0]] + [dims[2]] * (cfg["n_layers"] - 1)
+    for i in range(cfg["n_layers"]):
+        c = pm.ConvLayer(in_dims[i], dims[2], dims[1])  # CPU params, reference init
+        for k, v in c.state_dict().items():
+            tmp[f"conv_layers.{i}.{k}"] = v.numpy()
+    G1 = torch.nn.Linear(128, 128)
+    G2 = torch.nn.Linear(128, 128, bias=False)
+    tmp.update({"G1.weight": G1.weight.detach().numpy(), "G1.bias": G1.bias.detach().numpy(),
+                "G2.weight": G2.weight.detach().numpy()})
+    tr = orc.RefTrainer(tmp, feats, nbhds[0].numpy(), nbhds[1].numpy(), n_layers=cfg["n_layers"],
+                        T=cfg["T"])
+    mt = orc.MT(2)
+    times = []
+    t_start = time.time()
+    while len(times) < max_steps and (time.time() - t_start) < seconds:
+        t0 = time.time()
+        b, _ = orc.sample_batch_easy(mt, pos.numpy(), cfg["n_tracks"], cfg["batch"])
+        tr.step(b)
+        times.append(time.time() - t0)
+    t_step = float(np.median(times[1:] if len(times) > 2 else times))
+    return dict(value=3 * cfg["batch"] / t_step, unit="target nodes/s", cores=threads, kind="port",
+                sample=f"{len(times)} train steps (median) of the oracle's reference restatement "
+                       f"(torch CPU, {threads} threads) on the same synthetic graph and config",
+                ms_per_step=t_step * 1e3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precompute-rng", default="philox", choices=["philox", "mt19937"])
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    rank, world = setup_dist(args.gpus)
+
+    import pinsage_training as pt
+    import _native as nat
+    nat.require_gpu()
+    pg, g, feats, pos = build_problem(cfg)
+    nbhds, t_pre = precompute(g, cfg, args.precompute_rng)
+    hops = cfg["n_tracks"] * 500
+    log(f"[bench] precompute ({args.precompute_rng}) {t_pre:.2f}s = {hops/t_pre/1e6:.1f} M hops/s")
+
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        g.nbhds_path = os.path.join(tmp, "nb.pt")
+        torch.save(nbhds, g.nbhds_path)
+        torch.manual_seed(0)
+        tr = pt.PinSage(g, cfg["n_tracks"], feats.cuda(), pos, log=False, load_save=False)
+        # BASELINE config: n_layers / fanout / batch (bound before the model, as the reference does)
+        if tr.T != cfg["T"] or tr.n_layers != cfg["n_layers"]:
+            import pinsage_model as pm
+            tr.T, tr.n_layers = cfg["T"], cfg["n_layers"]
+            torch.manual_seed(0)
+            tr.model = pm.PinSageModel(g, tr.n, tr.n_layers, tr.dimensions, tr.n_hops, tr.alpha, tr.T, tr.nbhds)
+            tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+            tr.scheduler = torch.optim.lr_scheduler.ExponentialLR(tr.optimizer, tr.decay)
+        tr.batch_size = cfg["batch"]
+        torch.manual_seed(1234)  # same global batches on every rank
+
+        def step():
+            batch, _ = tr.next_batch()
+            return tr.train_batch(batch)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step()[0]
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        elapsed = t1 - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            elapsed = float(t.item())
+        ms_per_step = elapsed / args.steps * 1e3
+        value = 3 * cfg["batch"] * world * args.steps / elapsed
+
+        # per-kernel timing pass (HIP events on the launch stream), separate from the timed loop
+        eng = tr.model.runner().engine
+        nat.lib().pinsage_engine_timing(eng.h, 1)
+        n_t = max(5, min(20, args.steps))
+        sizes = []
+        for _ in range(n_t):
+            step()
+            torch.cuda.synchronize()
+            off = eng.off
+            ws = tr._fused.ws
+            cN0 = int(eng.view(ws, int(off.count_N[0]), torch.int32, 1).item())
+            cS0 = int(eng.view(ws, int(off.count_S[0]), torch.int32, 1).item())
+            sizes.append((cN0, cS0))
+        kt = kernel_table(eng)
+        nat.lib().pinsage_engine_timing(eng.h, 0)
+        os.chdir(cwd)
+
+    U0 = float(np.mean([s[0] for s in sizes]))
+    F0 = float(np.mean([s[1] for s in sizes]))
+    d, hid, T = cfg["d_in"], 512, cfg["T"]
+    q_ms, q_calls = kt.get("fwd.q_gemm.l0", (0.0, 1))
+    q_avg = q_ms / max(q_calls, 1)
+    q_flops = 2.0 * U0 * d * hid
+    achieved_tf = q_flops / (q_avg * 1e-3) / 1e12 if q_avg > 0 else 0.0
+    a_ms, a_calls = kt.get("fwd.agg.l0", (0.0, 1))
+    a_avg = a_ms / max(a_calls, 1)
+    agg_bytes = F0 * T * hid * 4 + F0 * T * 8 + F0 * hid * 4
+    kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "calls": v[1]} for k, v in sorted(kt.items())}
+    result = {
+        "metric": "PinSAGE train-step nodes/sec (2-hop, batch 512) at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "target nodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded playlist graph, N(0,1) features, co-membership positives)",
+        "config": {"workload": cfg["workload"], "n_tracks": cfg["n_tracks"], "n_cols": cfg["n_cols"],
+                   "memberships": cfg["memberships"], "d_in": cfg["d_in"], "hidden": hid, "out": 128,
+                   "n_layers": cfg["n_layers"], "fanout": T, "batch_per_gpu": cfg["batch"],
+                   "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
+                   "batch_rng": "mt19937 (reference-exact)"},
+        "roofline": {"bound": "mfma", "kernel": "fwd.q_gemm.l0 (gather + fp32 MFMA Q projection)",
+                     "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+                     "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg},
+        "gather_kernel": {"kernel": "fwd.agg.l0", "bound": "hbm", "avg_launch_ms": a_avg,
+                          "achieved_GBs": agg_bytes / (a_avg * 1e-3) / 1e9 if a_avg > 0 else 0.0,
+                          "peak_GBs": PEAK_HBM_GBS, "algorithmic_bytes": agg_bytes},
+        "frontier": {"U0_mean": U0, "F0_mean": F0},
+        "precompute": {"seconds": t_pre, "rng": args.precompute_rng, "hops_per_s": hops / t_pre},
+        "kernels": kernels,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(cfg, pg, feats, pos, nbhds)
+        except Exception as ex:  # report, never fail the bench line
+            result["cpu_baseline"] = {"error": repr(ex)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,317 @@
+// C-ABI entry points (see include/pinsage_hip.h) other than the engine's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pinsage_hip.h"
+#include "common.h"
+#include "gemm.h"
+#include "mt19937.h"
+
+namespace ps {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* last_error() { return g_err.c_str(); }
+
+int launch_mt_expand(const MTChunk*, int64_t, int64_t, int64_t, uint32_t*, hipStream_t);
+int launch_walk(const int64_t*, const int32_t*, const int64_t*, int64_t, int64_t, float,
+                const uint32_t*, uint64_t, uint32_t, int64_t, int32_t*, int*, hipStream_t);
+int launch_visit_topk(const int32_t*, const int64_t*, int64_t, int64_t, int64_t, int64_t, void*,
+                      double*, int64_t*, float*, int32_t*, int64_t, hipStream_t);
+int launch_visit_dense(const int32_t*, const int64_t*, int64_t, int64_t, int64_t, double*,
+                       hipStream_t);
+int64_t bitset_words(int64_t universe);
+int64_t bitset_blocks(int64_t universe);
+int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
+int launch_mark_table_i64(unsigned long long*, const int64_t*, int64_t, const int32_t*, int64_t,
+                          int, int64_t, int*, hipStream_t);
+int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
+                        int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
+int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
+               hipStream_t);
+
+// Fisher-Yates prefix of torch.randperm(n): first k entries, all n-1 draws consumed.
+static void randperm_prefix(MTState& g, int64_t n, int64_t k, int64_t* out) {
+  k = std::min(k, n);
+  std::unordered_map<int64_t, int64_t> sw;
+  sw.reserve((size_t)(2 * k + 16));
+  auto get = [&](int64_t i) {
+    auto it = sw.find(i);
+    return it == sw.end() ? i : it->second;
+  };
+  const int64_t steps = std::min(k, n - 1);
+  for (int64_t i = 0; i < steps; ++i) {
+    const int64_t z = (int64_t)(g.draw() % (uint64_t)(n - i));
+    const int64_t a = get(i), b = get(i + z);
+    sw[i] = b;
+    sw[i + z] = a;
+  }
+  for (int64_t i = 0; i < k; ++i) out[i] = get(i);
+  if (n - 1 > steps) g.skip(n - 1 - steps);
+}
+
+}  // namespace ps
+
+using namespace ps;
+
+extern "C" {
+
+int pinsage_version(void) { return 100; }
+const char* pinsage_last_error(void) { return ps::last_error(); }
+int pinsage_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ------------------------------------------------------------------ RNG
+int pinsage_mt_state_bytes(void) { return (int)sizeof(MTState); }
+int pinsage_mt_from_torch(void* mt, const uint8_t* st, int64_t nbytes) {
+  if (!reinterpret_cast<MTState*>(mt)->from_torch(st, nbytes)) {
+    set_error("mt_from_torch: not a valid torch CPU generator state");
+    return kErrArg;
+  }
+  return kOk;
+}
+int pinsage_mt_to_torch(const void* mt, uint8_t* st, int64_t nbytes) {
+  if (nbytes < MTState::kTorchBytes) {
+    set_error("mt_to_torch: buffer smaller than torch.get_rng_state()");
+    return kErrArg;
+  }
+  reinterpret_cast<const MTState*>(mt)->to_torch(st);
+  return kOk;
+}
+int pinsage_mt_seed(void* mt, uint64_t seed) {
+  reinterpret_cast<MTState*>(mt)->seed_with(seed);
+  return kOk;
+}
+int pinsage_mt_skip(void* mt, int64_t n) {
+  reinterpret_cast<MTState*>(mt)->skip(n);
+  return kOk;
+}
+int pinsage_mt_draws(void* mt, uint32_t* out, int64_t n) {
+  MTState* g = reinterpret_cast<MTState*>(mt);
+  for (int64_t i = 0; i < n; ++i) out[i] = g->draw();
+  return kOk;
+}
+int pinsage_mt_randperm_prefix(void* mt, int64_t n, int64_t k, int64_t* out) {
+  if (n < 0 || k < 0) {
+    set_error("randperm_prefix: negative size");
+    return kErrArg;
+  }
+  randperm_prefix(*reinterpret_cast<MTState*>(mt), n, k, out);
+  return kOk;
+}
+
+int pinsage_sample_batch_easy(void* mt, const int64_t* positives, int64_t P, int64_t n_items,
+                              int64_t batch_size, int64_t* batch_out) {
+  MTState& g = *reinterpret_cast<MTState*>(mt);
+  const int64_t B = std::min(batch_size, P);
+  std::vector<int64_t> sel((size_t)B);
+  randperm_prefix(g, P, B, sel.data());
+  std::vector<int64_t> mem;
+  mem.reserve((size_t)(2 * B));
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t a = positives[2 * sel[(size_t)b]], p = positives[2 * sel[(size_t)b] + 1];
+    if (a < 0 || a >= n_items || p < 0 || p >= n_items) {
+      set_error("sample_batch: positive pair id out of range");
+      return kErrIndex;
+    }
+    batch_out[3 * b] = a;
+    batch_out[3 * b + 1] = p;
+    mem.push_back(a);
+    mem.push_back(p);
+  }
+  std::sort(mem.begin(), mem.end());
+  mem.erase(std::unique(mem.begin(), mem.end()), mem.end());
+  const int64_t m = n_items - (int64_t)mem.size();
+  std::vector<int64_t> r((size_t)B);
+  randperm_prefix(g, m, B, r.data());
+  const int64_t nneg = std::min(B, m);
+  for (int64_t b = 0; b < B; ++b) {
+    if (b >= nneg) {
+      // the reference's torch.cat fails when fewer negatives than pairs exist
+      set_error("sample_batch: fewer candidate negatives than pairs");
+      return kErrArg;
+    }
+    // r[b]-th smallest id not in mem
+    const int64_t want = r[(size_t)b];
+    int64_t v = want, c = 0;
+    for (;;) {
+      const int64_t c2 = std::upper_bound(mem.begin(), mem.end(), v) - mem.begin();
+      if (c2 == c) break;
+      c = c2;
+      v = want + c;
+    }
+    batch_out[3 * b + 2] = v;
+  }
+  return kOk;
+}
+
+// ------------------------------------------------------------------ walks
+int64_t pinsage_walk_mt_workspace(int64_t n_src, int64_t n_hops) {
+  const int64_t chunks = 1024;
+  return align_up(chunks * (int64_t)sizeof(MTChunk), 256) + 256 +
+         align_up(std::max<int64_t>(n_src, 1) * 3 * n_hops * 4, 256);
+}
+
+int pinsage_walk_mt(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                    const int64_t* sources, int64_t n_src, int64_t n_hops, float alpha, void* mt,
+                    void* ws, int64_t ws_bytes, int32_t* trace, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  PS_REQUIRE(n_src >= 0 && n_hops > 0 && n_all > 0, kErrArg, "walk_mt: bad sizes");
+  if (n_src == 0) return kOk;
+  MTState& g = *reinterpret_cast<MTState*>(mt);
+  const int64_t kChunks = 1024;
+  const int64_t desc_bytes = align_up(kChunks * (int64_t)sizeof(MTChunk), 256);
+  char* base = static_cast<char*>(ws);
+  MTChunk* desc_dev = reinterpret_cast<MTChunk*>(base);
+  int* err_dev = reinterpret_cast<int*>(base + desc_bytes);
+  uint32_t* raw = reinterpret_cast<uint32_t*>(base + desc_bytes + 256);
+  const int64_t per_src = 3 * n_hops;
+  const int64_t room = (ws_bytes - desc_bytes - 256) / (per_src * 4);
+  PS_REQUIRE(room >= 1, kErrWorkspace, "walk_mt: workspace too small for one source");
+  std::vector<MTChunk> desc((size_t)kChunks);
+  PS_CHECK_HIP(hipMemsetAsync(err_dev, 0x7f, 4, st));
+  for (int64_t r0 = 0; r0 < n_src; r0 += room) {
+    const int64_t nr = std::min(room, n_src - r0);
+    const int64_t spc = (nr + kChunks - 1) / kChunks;  // sources per chunk
+    const int64_t n_chunks = (nr + spc - 1) / spc;
+    const int64_t wpc = spc * per_src;
+    for (int64_t c = 0; c < n_chunks; ++c) {
+      MTChunk& d = desc[(size_t)c];
+      std::memcpy(d.s, g.s, sizeof(d.s));
+      d.next = g.next;
+      d.avail = (uint32_t)g.avail();
+      const int64_t words = std::min(wpc, (nr - c * spc) * per_src);
+      g.skip(words);
+    }
+    PS_CHECK_HIP(hipMemcpyAsync(desc_dev, desc.data(), (size_t)n_chunks * sizeof(MTChunk),
+                                hipMemcpyHostToDevice, st));
+    PS_TRY(launch_mt_expand(desc_dev, n_chunks, wpc, nr * per_src, raw, st));
+    PS_TRY(launch_walk(indptr, indices, sources + r0, nr, n_hops, alpha, raw, 0, 0, 0,
+                       trace + r0 * n_hops, err_dev, st));
+    PS_CHECK_HIP(hipStreamSynchronize(st));  // desc host buffer is reused next round
+  }
+  int err = 0;
+  PS_CHECK_HIP(hipMemcpy(&err, err_dev, 4, hipMemcpyDeviceToHost));
+  if (err != 0x7f7f7f7f) {
+    set_error("walk: zero-degree node met (the reference's torch.randint(0) raises here)");
+    return kErrGraph;
+  }
+  return kOk;
+}
+
+int pinsage_walk_philox(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                        const int64_t* sources, int64_t n_src, int64_t n_hops, float alpha,
+                        uint64_t seed, uint32_t offset, int64_t src_base, int32_t* trace,
+                        void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  PS_REQUIRE(n_src >= 0 && n_hops > 0 && n_all > 0, kErrArg, "walk_philox: bad sizes");
+  if (n_src == 0) return kOk;
+  int* err_dev = nullptr;
+  PS_CHECK_HIP(hipMallocAsync((void**)&err_dev, 4, st));
+  PS_CHECK_HIP(hipMemsetAsync(err_dev, 0x7f, 4, st));
+  int rc = launch_walk(indptr, indices, sources, n_src, n_hops, alpha, nullptr, seed, offset,
+                       src_base, trace, err_dev, st);
+  int err = 0x7f7f7f7f;
+  if (rc == kOk) {
+    PS_CHECK_HIP(hipMemcpyAsync(&err, err_dev, 4, hipMemcpyDeviceToHost, st));
+    PS_CHECK_HIP(hipStreamSynchronize(st));
+  }
+  PS_CHECK_HIP(hipFreeAsync(err_dev, st));
+  if (rc != kOk) return rc;
+  if (err != 0x7f7f7f7f) {
+    set_error("walk: zero-degree node met (the reference's torch.randint(0) raises here)");
+    return kErrGraph;
+  }
+  return kOk;
+}
+
+// ------------------------------------------------------------------ visits / top-k
+int64_t pinsage_visit_topk_scratch(int64_t n_src, int64_t n_all, int64_t k) {
+  return (k * 64 <= n_all) ? 0 : n_src * n_all * 8;
+}
+
+int pinsage_visit_topk(const int32_t* trace, const int64_t* sources, int64_t n_src,
+                       int64_t n_hops, int64_t n_all, int64_t k, void* dense_scratch,
+                       double* w_out, int64_t* nb_out, float* wn_out, int32_t* nb32_out,
+                       int64_t t_norm, void* stream) {
+  PS_REQUIRE(k >= 1 && k <= n_all, kErrArg, "visit_topk: k out of range (torch: selected index k out of range)");
+  PS_REQUIRE(!wn_out || (t_norm >= 1 && t_norm <= k), kErrArg, "visit_topk: t_norm must be in [1, k]");
+  PS_REQUIRE(k * 64 <= n_all || dense_scratch, kErrWorkspace,
+             "visit_topk: nth_element regime needs dense scratch");
+  PS_REQUIRE(n_all < (int64_t)0xFFFFFFFF, kErrArg, "visit_topk: n_all must fit 32 bits");
+  return launch_visit_topk(trace, sources, n_src, n_hops, n_all, k, dense_scratch, w_out, nb_out,
+                           wn_out, nb32_out, t_norm, (hipStream_t)stream);
+}
+
+int pinsage_visit_dense(const int32_t* trace, const int64_t* sources, int64_t n_src,
+                        int64_t n_hops, int64_t n_all, double* dense, void* stream) {
+  return launch_visit_dense(trace, sources, n_src, n_hops, n_all, dense, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------ frontier step
+int64_t pinsage_frontier_workspace(int64_t n_items) {
+  const int64_t nw = bitset_words(n_items);
+  return align_up(nw * 8, 256) + align_up(nw * 4, 256) +
+         align_up(std::max<int64_t>(bitset_blocks(n_items), 1) * 4, 256) + 256;
+}
+
+int pinsage_frontier_step(const int64_t* nodeset, int64_t n, const int32_t* nb_table, int64_t ld,
+                          int64_t T, int64_t n_items, void* ws, int32_t* nodes_out,
+                          int32_t* count_out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nw = bitset_words(n_items);
+  char* b = static_cast<char*>(ws);
+  auto* bits = reinterpret_cast<unsigned long long*>(b);
+  auto* prefix = reinterpret_cast<uint32_t*>(b + align_up(nw * 8, 256));
+  auto* bsum = reinterpret_cast<uint32_t*>(b + align_up(nw * 8, 256) + align_up(nw * 4, 256));
+  int* err = reinterpret_cast<int*>(b + align_up(nw * 8, 256) + align_up(nw * 4, 256) +
+                                    align_up(std::max<int64_t>(bitset_blocks(n_items), 1) * 4, 256));
+  PS_CHECK_HIP(hipMemsetAsync(bits, 0, (size_t)nw * 8, st));
+  PS_CHECK_HIP(hipMemsetAsync(err, 0, 4, st));
+  PS_TRY(launch_mark_i64(bits, nodeset, n, n_items, err, st));
+  PS_TRY(launch_mark_table_i64(bits, nodeset, n, nb_table, ld, (int)T, n_items, err, st));
+  PS_TRY(launch_set_finalize(bits, bits, nullptr, n_items, bsum, prefix, nodes_out, count_out, st));
+  int herr = 0;
+  PS_CHECK_HIP(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  PS_CHECK_HIP(hipStreamSynchronize(st));
+  if (herr) {
+    set_error("frontier: node id out of range of the feature table (reference: IndexError)");
+    return kErrIndex;
+  }
+  return kOk;
+}
+
+// ------------------------------------------------------------------ single kernels
+int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
+                   const float* W, const float* bias, int64_t N, int act, float* C, int64_t ldc,
+                   void* stream) {
+  GemmParams p;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.a = A;
+  p.lda = lda;
+  p.a_idx = a_idx;
+  p.b = W;
+  p.ldb = K;
+  p.c = C;
+  p.ldc = ldc;
+  p.bias = bias;
+  p.act = act != 0;
+  return launch_gemm(p, (hipStream_t)stream);
+}
+
+int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
+                         int64_t n_rows, int64_t T, float* agg, void* stream) {
+  return launch_agg(q, (int)hid, loc, w, (int)T, nullptr, n_rows, agg, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,807 @@
+// Convolution, loss and optimizer kernels for gfx950 (everything of the train
+// step that is not a GEMM).
+//
+//   layer_prep      per-layer index tables (self rows, neighbour slots, weights)
+//   agg             importance-weighted neighbour mean (pinsage_model.py:202)
+//   csr_*           transpose of the neighbour slots for the backward scatter
+//   dq_gather       d(agg) -> d(q) through the transpose, times lrelu'(q)
+//   norm_lrelu_bwd  backward of z/||z|| and leaky_relu (pinsage_model.py:209-210)
+//   loss_*          max_margin_loss (pinsage_training.py:31-41) fwd+bwd with the
+//                   reference's duplicate-gradient semantics, plus monitors
+//                   (pinsage_training.py:200-212)
+//   adam            torch.optim.Adam step (pinsage_training.py:147,191)
+#include "common.h"
+
+namespace ps {
+
+__device__ __forceinline__ int32_t rank_in(const unsigned long long* bits, const uint32_t* prefix,
+                                           int64_t v) {
+  const unsigned long long w = bits[v >> 6];
+  return (int32_t)(prefix[v >> 6] + __popcll(w & ((1ull << (v & 63)) - 1ull)));
+}
+
+// ---------------------------------------------------------------- layer prep
+// For f < *nS (rows of the layer's node set S_l, sorted ids):
+//   self_src[f]   = row of h_l holding node f (rank in S_{l-1}, or the id at l=0)
+//   loc[f*T+t]    = rank of nb[id][t] in N_l (row of the Q output)
+//   wloc[f*T+t]   = normalised importance weight
+// For u < *nN (rows of N_l):  q_src[u] = row of h_l holding that node.
+__global__ void layer_prep_kernel(const int32_t* __restrict__ S_mem, const int* __restrict__ nS,
+                                  const int32_t* __restrict__ N_mem, const int* __restrict__ nN,
+                                  const unsigned long long* __restrict__ N_bits,
+                                  const uint32_t* __restrict__ N_pref,
+                                  const unsigned long long* __restrict__ P_bits,
+                                  const uint32_t* __restrict__ P_pref,
+                                  const int32_t* __restrict__ nb, const float* __restrict__ wn,
+                                  int64_t ldT, int T, int32_t* __restrict__ self_src,
+                                  int32_t* __restrict__ q_src, int32_t* __restrict__ loc,
+                                  float* __restrict__ wloc) {
+  const int64_t FS = (int64_t)(*nS), FN = (int64_t)(*nN);
+  const int64_t total = FS * T + FS + FN;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < FS * T) {
+      const int64_t f = e / T, t = e - f * T;
+      const int64_t id = S_mem[f];
+      const int64_t u = nb[id * ldT + t];
+      loc[e] = rank_in(N_bits, N_pref, u);
+      wloc[e] = wn[id * ldT + t];
+    } else if (e < FS * T + FS) {
+      const int64_t f = e - FS * T;
+      const int64_t id = S_mem[f];
+      self_src[f] = P_bits ? rank_in(P_bits, P_pref, id) : (int32_t)id;
+    } else {
+      const int64_t u = e - FS * T - FS;
+      const int64_t id = N_mem[u];
+      q_src[u] = P_bits ? rank_in(P_bits, P_pref, id) : (int32_t)id;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- aggregation
+// agg[f][:] = sum_t wloc[f,t] * q[loc[f,t]][:]   (weights pre-normalised by the
+// row sum in f64, so this is the reference's sum(w*q)/sum(w)).  One wave per
+// row, float4 per lane; the T gathered q rows are L2-resident.
+template <int VEC>  // float4s per lane per row chunk
+__global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, int hid,
+                                                  const int32_t* __restrict__ loc,
+                                                  const float* __restrict__ wloc, int T,
+                                                  const int* __restrict__ nS, int64_t nS_host,
+                                                  float* __restrict__ agg) {
+  const int64_t F = nS ? (int64_t)(*nS) : nS_host;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int h4 = hid >> 2;
+  for (int64_t f = wid; f < F; f += nw) {
+    for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
+      float4 a[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) a[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int t = 0; t < T; ++t) {
+        const int64_t r = loc[f * T + t];
+        const float w = wloc[f * T + t];
+        const float4* qr = reinterpret_cast<const float4*>(q + r * hid);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const int c = c0 + v * 64 + lane;
+          if (c < h4) {
+            const float4 x = qr[c];
+            a[v].x = fmaf(w, x.x, a[v].x);
+            a[v].y = fmaf(w, x.y, a[v].y);
+            a[v].z = fmaf(w, x.z, a[v].z);
+            a[v].w = fmaf(w, x.w, a[v].w);
+          }
+        }
+      }
+      float4* out = reinterpret_cast<float4*>(agg + f * hid);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const int c = c0 + v * 64 + lane;
+        if (c < h4) out[c] = a[v];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- transpose (CSR by q row)
+// Lanes of a wave holding the same q row combine into one atomic (popular
+// tracks sit in many neighbour lists of one wave's rows).
+__global__ void csr_count_kernel(const int32_t* __restrict__ loc, const int* __restrict__ nS, int T,
+                                 int* __restrict__ cnt) {
+  const int64_t n = (int64_t)(*nS) * T;
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63LL; base < n;
+       base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = base + lane;
+    const int32_t u = e < n ? loc[e] : -1;
+    unsigned long long rem = __ballot(e < n);
+    while (rem) {
+      const int leader = __ffsll((long long)rem) - 1;
+      const int32_t v = __shfl(u, leader, 64);
+      const unsigned long long m = __ballot(u == v);
+      if (lane == leader) atomicAdd(cnt + v, __popcll(m));
+      rem &= ~m;
+    }
+  }
+}
+
+// exclusive scan of cnt[0..*n) into off[0..*n] (off[n] = total); one block per
+// 1024 entries, each block sums its predecessors' totals itself.
+constexpr int kScanB = 256, kScanPer = 4, kScanChunk = kScanB * kScanPer;
+__global__ __launch_bounds__(kScanB) void scan_block_sums_kernel(const int* __restrict__ cnt,
+                                                                 const int* __restrict__ n_dev,
+                                                                 int* __restrict__ bsum) {
+  __shared__ int red[kScanB / 64];
+  const int64_t n = *n_dev;
+  const int64_t i0 = (int64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  int c = 0;
+  for (int q = 0; q < kScanPer; ++q)
+    if (i0 + q < n) c += cnt[i0 + q];
+  c = wave_sum_i(c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ __launch_bounds__(kScanB) void scan_apply_kernel(const int* __restrict__ cnt,
+                                                            const int* __restrict__ n_dev,
+                                                            const int* __restrict__ bsum,
+                                                            int* __restrict__ off,
+                                                            int* __restrict__ cursor) {
+  __shared__ int ws[kScanB / 64];
+  __shared__ int base_sh;
+  const int64_t n = *n_dev;
+  if ((int64_t)blockIdx.x * kScanChunk > n) return;
+  int o = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += kScanB) o += bsum[i];
+  o = wave_sum_i(o);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = o;
+  __syncthreads();
+  if (threadIdx.x == 0) base_sh = ws[0] + ws[1] + ws[2] + ws[3];
+  __syncthreads();
+  const int base = base_sh;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  int v[kScanPer], c = 0;
+  for (int q = 0; q < kScanPer; ++q) {
+    v[q] = (i0 + q < n) ? cnt[i0 + q] : 0;
+    c += v[q];
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = c;
+  for (int s = 1; s < 64; s <<= 1) {
+    int y = __shfl_up(inc, s, 64);
+    if (lane >= s) inc += y;
+  }
+  if (lane == 63) ws[wv] = inc;
+  __syncthreads();
+  int wo = 0;
+  for (int i = 0; i < wv; ++i) wo += ws[i];
+  int p = base + wo + inc - c;
+  for (int q = 0; q < kScanPer; ++q) {
+    if (i0 + q < n) {
+      off[i0 + q] = p;
+      cursor[i0 + q] = p;
+    }
+    if (i0 + q == n) off[n] = p;
+    p += v[q];
+  }
+}
+__global__ void csr_fill_kernel(const int32_t* __restrict__ loc, const int* __restrict__ nS, int T,
+                                int* __restrict__ cursor, int32_t* __restrict__ occ,
+                                int32_t* __restrict__ occ_u) {
+  const int64_t n = (int64_t)(*nS) * T;
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63LL; base < n;
+       base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = base + lane;
+    const int32_t u = e < n ? loc[e] : -1;
+    unsigned long long rem = __ballot(e < n);
+    int pos = 0;
+    while (rem) {
+      const int leader = __ffsll((long long)rem) - 1;
+      const int32_t v = __shfl(u, leader, 64);
+      const unsigned long long m = __ballot(u == v);
+      int b = 0;
+      if (lane == leader) b = atomicAdd(cursor + v, __popcll(m));
+      b = __shfl(b, leader, 64);
+      if (u == v) pos = b + __popcll(m & ((1ull << lane) - 1));
+      rem &= ~m;
+    }
+    if (e < n) {
+      occ[pos] = (int32_t)e;
+      occ_u[pos] = u;
+    }
+  }
+}
+
+// dp_q[u][:] = lrelu'(q[u][:]) * sum_{e in occ(u)} wloc[e] * dagg[e / T][:]
+// Load-balanced segmented reduction over the occurrence list grouped by u:
+// every wave takes a fixed chunk of kSegChunk positions (popular tracks sit in
+// thousands of neighbour lists, so one-wave-per-u would serialise them).  A
+// segment wholly inside a chunk is stored; a segment cut by a chunk boundary
+// is added with f32 atomics into the pre-zeroed output.  lrelu' is applied to
+// each partial (it is a per-element factor).
+constexpr int kSegChunk = 32;
+
+// zero rows [0, *nrows) of a [rows][n] buffer (device-side row count)
+__global__ void zero_rows_kernel(float* __restrict__ x, int64_t n, const int* __restrict__ nrows) {
+  const int64_t total = (int64_t)(*nrows) * n / 4;
+  float4* x4 = reinterpret_cast<float4*>(x);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+template <int VEC>
+__global__ __launch_bounds__(256) void dq_segment_kernel(
+    const int32_t* __restrict__ occ, const int32_t* __restrict__ occ_u,
+    const float* __restrict__ wloc, int T, const float* __restrict__ dagg, int64_t ld_dagg,
+    const float* __restrict__ q, int hid, const int* __restrict__ nS, float* __restrict__ dpq) {
+  const int64_t total = (int64_t)(*nS) * T;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int h4 = hid >> 2;
+  for (int64_t ch = wid; ch * kSegChunk < total; ch += nw) {
+    const int64_t p0 = ch * kSegChunk;
+    const int n = (int)min((int64_t)kSegChunk, total - p0);
+    // indices of the chunk: lane j holds position p0 + j
+    int32_t my_u = -1, my_e = 0;
+    float my_w = 0.f;
+    if (lane < n) {
+      my_u = occ_u[p0 + lane];
+      my_e = occ[p0 + lane];
+      my_w = wloc[my_e];
+    }
+    const int32_t u_before = p0 > 0 ? occ_u[p0 - 1] : -1;
+    const int32_t u_after = p0 + n < total ? occ_u[p0 + n] : -1;
+    for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
+      float4 acc[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      int32_t cur = __shfl(my_u, 0, 64);
+      int seg_start = 0;
+      for (int j = 0; j < n; ++j) {
+        const int32_t u = __shfl(my_u, j, 64);
+        if (u != cur) {
+          // flush segment [seg_start, j) of row cur
+          const bool atom = (seg_start == 0 && cur == u_before);
+          const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)cur * hid);
+          float4* o = reinterpret_cast<float4*>(dpq + (int64_t)cur * hid);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) {
+            const int c = c0 + v * 64 + lane;
+            if (c < h4) {
+              const float4 qq = qr[c];
+              float4 r = make_float4(acc[v].x * lrelu_grad(qq.x), acc[v].y * lrelu_grad(qq.y),
+                                     acc[v].z * lrelu_grad(qq.z), acc[v].w * lrelu_grad(qq.w));
+              if (atom) {
+                float* of = reinterpret_cast<float*>(o + c);
+                atomicAdd(of, r.x);
+                atomicAdd(of + 1, r.y);
+                atomicAdd(of + 2, r.z);
+                atomicAdd(of + 3, r.w);
+              } else {
+                o[c] = r;
+              }
+            }
+            acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          cur = u;
+          seg_start = j;
+        }
+        const int32_t e = __shfl(my_e, j, 64);
+        const float w = __shfl(my_w, j, 64);
+        const float4* dr = reinterpret_cast<const float4*>(dagg + (int64_t)(e / T) * ld_dagg);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const int c = c0 + v * 64 + lane;
+          if (c < h4) {
+            const float4 x = dr[c];
+            acc[v].x = fmaf(w, x.x, acc[v].x);
+            acc[v].y = fmaf(w, x.y, acc[v].y);
+            acc[v].z = fmaf(w, x.z, acc[v].z);
+            acc[v].w = fmaf(w, x.w, acc[v].w);
+          }
+        }
+      }
+      {
+        const bool atom = (seg_start == 0 && cur == u_before) || cur == u_after;
+        const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)cur * hid);
+        float4* o = reinterpret_cast<float4*>(dpq + (int64_t)cur * hid);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const int c = c0 + v * 64 + lane;
+          if (c < h4) {
+            const float4 qq = qr[c];
+            float4 r = make_float4(acc[v].x * lrelu_grad(qq.x), acc[v].y * lrelu_grad(qq.y),
+                                   acc[v].z * lrelu_grad(qq.z), acc[v].w * lrelu_grad(qq.w));
+            if (atom) {
+              float* of = reinterpret_cast<float*>(o + c);
+              atomicAdd(of, r.x);
+              atomicAdd(of + 1, r.y);
+              atomicAdd(of + 2, r.z);
+              atomicAdd(of + 3, r.w);
+            } else {
+              o[c] = r;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- L2 norm + lrelu backward
+// y = lrelu(p) / ||lrelu(p)||:  dp = lrelu'(y) * (dy - y (y . dy)) / ||.||
+__global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __restrict__ y,
+                                                             const float* __restrict__ nrm,
+                                                             const float* __restrict__ dy, int n,
+                                                             const int* __restrict__ nrows,
+                                                             float* __restrict__ dp) {
+  const int64_t R = *nrows;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wid; r < R; r += nw) {
+    float dot = 0.f;
+    for (int c = lane; c < n; c += 64) dot += y[r * n + c] * dy[r * n + c];
+    dot = wave_sum(dot);
+    const float inv = 1.f / nrm[r];
+    for (int c = lane; c < n; c += 64) {
+      const float yy = y[r * n + c];
+      dp[r * n + c] = lrelu_grad(yy) * (dy[r * n + c] - yy * dot) * inv;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- column sums (bias grads)
+// partial[g][c] = sum over row chunk g of X[:, c]: grid (ceil(n/64), G), block
+// 256 = 64 columns x 4 row lanes; reduced later in a fixed order, so the
+// result is deterministic.
+constexpr int kColChunks = 32;
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ X, int n,
+                                                             int64_t ld, const int* __restrict__ nrows_dev,
+                                                             int nrows_host,
+                                                             float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int64_t R = nrows_dev ? *nrows_dev : nrows_host;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ty = threadIdx.x >> 6;
+  const int G = gridDim.y;
+  const int64_t rows_per = (R + G - 1) / G;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < n) {
+    int64_t r = r0 + ty;
+    for (; r + 4 < r1; r += 8) {
+      s0 += X[r * ld + c];
+      s1 += X[(r + 4) * ld + c];
+    }
+    for (; r < r1; r += 4) s0 += X[r * ld + c];
+  }
+  red[ty][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (ty == 0 && c < n)
+    partial[(int64_t)blockIdx.y * n + c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                           (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// out[i] = sum_s part[s * stride + i]  (fixed order)
+__global__ void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t stride,
+                                    int64_t len, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 3 < S; k += 4) {
+      s0 += part[k * stride + i];
+      s1 += part[(k + 1) * stride + i];
+      s2 += part[(k + 2) * stride + i];
+      s3 += part[(k + 3) * stride + i];
+    }
+    for (; k < S; ++k) s0 += part[k * stride + i];
+    out[i] = (s0 + s1) + (s2 + s3);
+  }
+}
+
+// ---------------------------------------------------------------- loss
+// One wave per triple b: rows rq, rp, rn of Z (head outputs of the unique top
+// nodes).  Per call c in {q, pos, neg} and position b, the reference's
+// backward hands the output row the SUM of the gradients of every position of
+// that call holding the same node (index_put backward, pinsage_model.py:29 then
+// :265), so G[c][rank] accumulates those sums and K[c][rank] the multiplicity;
+// loss_finish forms dZ = sum_c K[c] * G[c].
+__global__ __launch_bounds__(256) void loss_triple_kernel(
+    const float* __restrict__ Z, int d, const int32_t* __restrict__ pos_rank, int B, float margin,
+    const float* __restrict__ feats, int64_t ld_f, int d_in, const int64_t* __restrict__ batch,
+    float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ part,
+    float* __restrict__ colpart) {
+  __shared__ float red[4][4];  // per wave: loss, nfl, sum||h_q||^2, unused
+  // per-block column sums of the query rows (variance monitor), d <= 512
+  {
+    const int b0 = blockIdx.x * 4;
+    for (int c = threadIdx.x; c < d; c += blockDim.x) {
+      float s = 0.f;
+      for (int k = 0; k < 4; ++k)
+        if (b0 + k < B) s += Z[(int64_t)pos_rank[3 * (b0 + k)] * d + c];
+      colpart[(int64_t)blockIdx.x * d + c] = s;
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + wv;
+  float lossv = 0.f, nflv = 0.f, sq = 0.f;
+  if (b < B) {
+    const int rq = pos_rank[3 * b], rp = pos_rank[3 * b + 1], rn = pos_rank[3 * b + 2];
+    // --- max_margin_loss on the model outputs
+    float dq_ = 0.f, dp_ = 0.f, dn_ = 0.f, qp = 0.f, qn = 0.f;
+    for (int c = lane; c < d; c += 64) {
+      const float a = Z[(int64_t)rq * d + c], p = Z[(int64_t)rp * d + c], n = Z[(int64_t)rn * d + c];
+      dq_ += a * a;
+      dp_ += p * p;
+      dn_ += n * n;
+      qp += a * p;
+      qn += a * n;
+    }
+    dq_ = wave_sum(dq_);
+    dp_ = wave_sum(dp_);
+    dn_ = wave_sum(dn_);
+    qp = wave_sum(qp);
+    qn = wave_sum(qn);
+    sq = dq_;
+    const float nq = fmaxf(sqrtf(dq_), 1e-12f), np = fmaxf(sqrtf(dp_), 1e-12f),
+                nn = fmaxf(sqrtf(dn_), 1e-12f);
+    const float cqp = qp / (nq * np), cqn = qn / (nq * nn);
+    const float ds = cqn - cqp + margin;
+    lossv = ds >= 0.f ? ds : 0.f;
+    const float g = ds >= 0.f ? 1.f / (float)B : 0.f;
+    if (g != 0.f) {
+      // d/d(normalised rows): q_hat <- g(n_hat - p_hat), p_hat <- -g q_hat,
+      // n_hat <- g q_hat; then x_hat = x/||x||: dx = (g_hat - x_hat (x_hat.g_hat)) / ||x||
+      float pq = 0.f, pp = 0.f, pn = 0.f;
+      for (int c = lane; c < d; c += 64) {
+        const float a = Z[(int64_t)rq * d + c] / nq, p = Z[(int64_t)rp * d + c] / np,
+                    n = Z[(int64_t)rn * d + c] / nn;
+        pq += a * (g * (n - p));
+        pp += p * (-g * a);
+        pn += n * (g * a);
+      }
+      pq = wave_sum(pq);
+      pp = wave_sum(pp);
+      pn = wave_sum(pn);
+      for (int c = lane; c < d; c += 64) {
+        const float a = Z[(int64_t)rq * d + c] / nq, p = Z[(int64_t)rp * d + c] / np,
+                    n = Z[(int64_t)rn * d + c] / nn;
+        atomicAdd(G + ((int64_t)0 * S_max + rq) * d + c, (g * (n - p) - a * pq) / nq);
+        atomicAdd(G + ((int64_t)1 * S_max + rp) * d + c, (-g * a - p * pp) / np);
+        atomicAdd(G + ((int64_t)2 * S_max + rn) * d + c, (g * a - n * pn) / nn);
+      }
+    }
+    if (lane == 0) {
+      atomicAdd(Kc + 0 * S_max + rq, 1);
+      atomicAdd(Kc + 1 * S_max + rp, 1);
+      atomicAdd(Kc + 2 * S_max + rn, 1);
+    }
+    // --- monitor: cosine triplet loss on raw features (margin 1e-4)
+    if (feats) {
+      const int64_t iq = batch[3 * b], ip = batch[3 * b + 1], in = batch[3 * b + 2];
+      float fqq = 0.f, fpp = 0.f, fnn = 0.f, fqp = 0.f, fqn = 0.f;
+      for (int c = lane; c < d_in; c += 64) {
+        const float a = feats[iq * ld_f + c], p = feats[ip * ld_f + c], n = feats[in * ld_f + c];
+        fqq += a * a;
+        fpp += p * p;
+        fnn += n * n;
+        fqp += a * p;
+        fqn += a * n;
+      }
+      fqq = wave_sum(fqq);
+      fpp = wave_sum(fpp);
+      fnn = wave_sum(fnn);
+      fqp = wave_sum(fqp);
+      fqn = wave_sum(fqn);
+      // inputs are normalised first (F.normalize), then cosine similarity
+      const float aq = fmaxf(sqrtf(fqq), 1e-12f), ap = fmaxf(sqrtf(fpp), 1e-12f),
+                  an = fmaxf(sqrtf(fnn), 1e-12f);
+      const float hq2 = fqq / (aq * aq), hp2 = fpp / (ap * ap), hn2 = fnn / (an * an);
+      const float cp = (fqp / (aq * ap)) / fmaxf(sqrtf(hq2 * hp2), 1e-8f);
+      const float cn = (fqn / (aq * an)) / fmaxf(sqrtf(hq2 * hn2), 1e-8f);
+      const float v = (1.f - cp) - (1.f - cn) + 1e-4f;
+      nflv = v > 0.f ? v : 0.f;
+    }
+  }
+  if (lane == 0) {
+    red[wv][0] = lossv;
+    red[wv][1] = nflv;
+    red[wv][2] = sq;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 3; ++k) part[(int64_t)blockIdx.x * 4 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+// dZ[r] = sum_c K[c][r] * G[c][r];  block 0 also reduces the per-block loss
+// partials (fixed order) into scal[0] = loss, scal[1] = node-feature loss.
+__global__ __launch_bounds__(256) void loss_finish_kernel(const float* __restrict__ G,
+                                                          const int* __restrict__ Kc, int64_t S_max,
+                                                          const int* __restrict__ nS, int d,
+                                                          float* __restrict__ dZ,
+                                                          const float* __restrict__ part, int nparts,
+                                                          int B, float* __restrict__ scal) {
+  const int64_t S = *nS;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / d;
+    float v = 0.f;
+    for (int c = 0; c < 3; ++c) {
+      const int k = Kc[c * S_max + r];
+      if (k) v += (float)k * G[c * S_max * d + e];
+    }
+    dZ[e] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float l = 0.f, nf = 0.f, sq = 0.f;
+    for (int i = 0; i < nparts; ++i) {
+      l += part[i * 4 + 0];
+      nf += part[i * 4 + 1];
+      sq += part[i * 4 + 2];
+    }
+    scal[0] = l / (float)B;
+    scal[1] = nf / (float)B;
+    scal[2] = sq;
+  }
+}
+
+// batch_variance of h_q (pinsage_training.py:99-103): sum((h - mean)^2)/(B-1)
+// over the B query rows (duplicates included) = (sum |h|^2 - B |mean|^2)/(B-1),
+// from the loss kernel's per-block column sums and sum of squares (scal[2]).
+__global__ __launch_bounds__(256) void variance_finish_kernel(const float* __restrict__ colpart,
+                                                              int nparts, int d, int B,
+                                                              float* __restrict__ scal) {
+  __shared__ float red[4];
+  __shared__ float cs[4][128];
+  float acc = 0.f;
+  const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int c0 = 0; c0 < d; c0 += 64) {
+    const int c = c0 + l;
+    float s = 0.f;
+    if (c < d)
+      for (int g = q; g < nparts; g += 4) s += colpart[(int64_t)g * d + c];
+    cs[q][l] = s;
+    __syncthreads();
+    if (q == 0 && c < d) {
+      const float m = ((cs[0][l] + cs[1][l]) + (cs[2][l] + cs[3][l])) / (float)B;
+      acc += m * m;
+    }
+    __syncthreads();
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float msq = red[0] + red[1] + red[2] + red[3];
+    scal[3] = (scal[2] - (float)B * msq) / (float)(B - 1);
+  }
+}
+
+// ---------------------------------------------------------------- Adam
+// torch.optim.Adam (single-tensor math, weight_decay 0, amsgrad off):
+//   m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// lr comes from device memory (the scheduler updates it), the step counter is
+// bumped by loss_finish, so the whole train step can be graph-replayed.
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                            float* __restrict__ m, float* __restrict__ v, int64_t n,
+                            const float* __restrict__ lr_dev, const int* __restrict__ step_dev,
+                            float beta1, float beta2, float eps) {
+  const double step = (double)(*step_dev);
+  const double lr = (double)(*lr_dev);
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2s = sqrt(1.0 - pow((double)beta2, step));
+  const float step_size = (float)(lr / bc1);
+  const float bc2f = (float)bc2s;
+  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float mi = m[i];
+    mi = mi + omb1 * (gi - mi);
+    float vi = v[i] * beta2 + omb2 * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2f + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+__global__ void step_incr_kernel(int* step) { *step += 1; }
+
+// out[i][:] = Z[pos_rank[i]][:]
+__global__ void gather_out_kernel(const float* __restrict__ Z, int d, const int32_t* __restrict__ pr,
+                                  int64_t n, float* __restrict__ out) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * d;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / d, c = e - i * d;
+    out[e] = Z[(int64_t)pr[i] * d + c];
+  }
+}
+
+// one call: G[r] = sum of dout rows at positions of node r, K[r] = multiplicity
+__global__ void dout_accum_kernel(const float* __restrict__ dout, int d,
+                                  const int32_t* __restrict__ pr, int64_t n, float* __restrict__ G,
+                                  int* __restrict__ Kc) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * d;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / d, c = e - i * d;
+    atomicAdd(G + (int64_t)pr[i] * d + c, dout[e]);
+    if (c == 0) atomicAdd(Kc + pr[i], 1);
+  }
+}
+__global__ void dz_scale_kernel(const float* __restrict__ G, const int* __restrict__ Kc, int d,
+                                const int* __restrict__ nS, float* __restrict__ dZ) {
+  const int64_t S = *nS;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
+       e += (int64_t)gridDim.x * blockDim.x)
+    dZ[e] = (float)Kc[e / d] * G[e];
+}
+
+// out[m*ld + n] = sum_s part[s*stride + m*N + n]
+__global__ void reduce_slabs_2d_kernel(const float* __restrict__ part, int S, int64_t stride, int M,
+                                       int N, float* __restrict__ out, int64_t ld) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)M * N;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += part[k * stride + i];
+    const int64_t m = i / N, n = i - m * N;
+    out[m * ld + n] = s;
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+int launch_gather_out(const float* Z, int d, const int32_t* pr, int64_t n, float* out,
+                      hipStream_t st) {
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(gather_out_kernel, dim3(grid_for(n * d, 256)), dim3(256), 0, st, Z, d, pr, n,
+                     out);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, const int* nS,
+                        int64_t S_max, float* G, int* Kc, float* dZ, hipStream_t st) {
+  PS_CHECK_HIP(hipMemsetAsync(G, 0, (size_t)(S_max * d) * sizeof(float), st));
+  PS_CHECK_HIP(hipMemsetAsync(Kc, 0, (size_t)S_max * sizeof(int), st));
+  hipLaunchKernelGGL(dout_accum_kernel, dim3(grid_for(n * d, 256)), dim3(256), 0, st, dout, d, pr, n,
+                     G, Kc);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dz_scale_kernel, dim3(grid_for(S_max * d, 256)), dim3(256), 0, st, G, Kc, d, nS,
+                     dZ);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_reduce_slabs_2d(const float* part, int S, int64_t stride, int M, int N, float* out,
+                           int64_t ld, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_slabs_2d_kernel, dim3(grid_for((int64_t)M * N, 256, 1024)), dim3(256), 0,
+                     st, part, S, stride, M, N, out, ld);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+int launch_layer_prep(const int32_t* S_mem, const int* nS, int64_t S_max, const int32_t* N_mem,
+                      const int* nN, int64_t N_max, const unsigned long long* N_bits,
+                      const uint32_t* N_pref, const unsigned long long* P_bits,
+                      const uint32_t* P_pref, const int32_t* nb, const float* wn, int64_t ldT,
+                      int T, int32_t* self_src, int32_t* q_src, int32_t* loc, float* wloc,
+                      hipStream_t st) {
+  const int64_t tot = S_max * T + S_max + N_max;
+  hipLaunchKernelGGL(layer_prep_kernel, dim3(grid_for(tot, 256)), dim3(256), 0, st, S_mem, nS, N_mem,
+                     nN, N_bits, N_pref, P_bits, P_pref, nb, wn, ldT, T, self_src, q_src, loc, wloc);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, int T,
+               const int* nS, int64_t S_max, float* agg, hipStream_t st) {
+  PS_REQUIRE(hid % 4 == 0, kErrArg, "agg: hidden dim must be a multiple of 4");
+  if (S_max <= 0) return kOk;
+  const int grid = grid_for(S_max * 64, 256, 4096);
+  if (hid >= 512)
+    hipLaunchKernelGGL((agg_kernel<2>), dim3(grid), dim3(256), 0, st, q, hid, loc, wloc, T, nS,
+                       S_max, agg);
+  else
+    hipLaunchKernelGGL((agg_kernel<1>), dim3(grid), dim3(256), 0, st, q, hid, loc, wloc, T, nS,
+                       S_max, agg);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, const int* nN,
+                     int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int32_t* occ,
+                     int32_t* occ_u, hipStream_t st) {
+  PS_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)(N_max + 1) * sizeof(int), st));
+  hipLaunchKernelGGL(csr_count_kernel, dim3(grid_for(S_max * T, 256)), dim3(256), 0, st, loc, nS, T,
+                     cnt);
+  PS_CHECK_LAUNCH();
+  const int nb = ceil_div(N_max + 1, kScanChunk);
+  hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum, off, cursor);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(csr_fill_kernel, dim3(grid_for(S_max * T, 256)), dim3(256), 0, st, loc, nS, T,
+                     cursor, occ, occ_u);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_dq_segment(const int32_t* occ, const int32_t* occ_u, const float* wloc, int T,
+                      const float* dagg, int64_t ld_dagg, const float* q, int hid, const int* nS,
+                      int64_t S_max, const int* nN, int64_t N_max, float* dpq, hipStream_t st) {
+  PS_REQUIRE(hid % 4 == 0, kErrArg, "dq_segment: hidden dim must be a multiple of 4");
+  hipLaunchKernelGGL(zero_rows_kernel, dim3(grid_for(N_max * hid / 4, 256, 2048)), dim3(256), 0, st,
+                     dpq, (int64_t)hid, nN);
+  PS_CHECK_LAUNCH();
+  const int64_t chunks = (S_max * T + kSegChunk - 1) / kSegChunk;
+  const int grid = grid_for(chunks * 64, 256, 4096);
+  if (hid >= 512)
+    hipLaunchKernelGGL((dq_segment_kernel<2>), dim3(grid), dim3(256), 0, st, occ, occ_u, wloc, T, dagg,
+                       ld_dagg, q, hid, nS, dpq);
+  else
+    hipLaunchKernelGGL((dq_segment_kernel<1>), dim3(grid), dim3(256), 0, st, occ, occ_u, wloc, T, dagg,
+                       ld_dagg, q, hid, nS, dpq);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int n,
+                          const int* nrows, int64_t max_rows, float* dp, hipStream_t st) {
+  hipLaunchKernelGGL(norm_lrelu_bwd_kernel, dim3(grid_for(max_rows * 64, 256, 4096)), dim3(256), 0,
+                     st, y, nrm, dy, n, nrows, dp);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_colsum_partial(const float* X, int n, int64_t ld, const int* nrows_dev, int nrows_host,
+                          int G, float* partial, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(ceil_div(n, 64), G), dim3(256), 0, st, X, n, ld,
+                     nrows_dev, nrows_host, partial);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_reduce_slabs(const float* part, int S, int64_t stride, int64_t len, float* out,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(len, 256, 1024)), dim3(256), 0, st, part, S,
+                     stride, len, out);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float margin,
+                const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
+                int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
+                hipStream_t st) {
+  PS_CHECK_HIP(hipMemsetAsync(G, 0, (size_t)(3 * S_max * d) * sizeof(float), st));
+  PS_CHECK_HIP(hipMemsetAsync(Kc, 0, (size_t)(3 * S_max) * sizeof(int), st));
+  const int nblk = ceil_div(B, 4);
+  hipLaunchKernelGGL(loss_triple_kernel, dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, margin,
+                     feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(grid_for(S_max * d, 256, 1024)), dim3(256), 0, st, G,
+                     Kc, S_max, nS, d, dZ, part, nblk, B, scal);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(variance_finish_kernel, dim3(1), dim3(256), 0, st, colpart, nblk, d, B, scal);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* lr_dev,
+                int* step_dev, float beta1, float beta2, float eps, hipStream_t st) {
+  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, st, step_dev);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, p, g, m, v, n,
+                     lr_dev, step_dev, beta1, beta2, eps);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+}  // namespace ps

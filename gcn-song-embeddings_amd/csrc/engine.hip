@@ -1,0 +1,732 @@
+// PinSage train-step engine: sequences the frontier, convolution, head, loss,
+// backward and Adam kernels on one HIP stream with every data-dependent size
+// kept on the device, so a step needs no host synchronisation and can be
+// captured into a hipGraph.
+//
+// Forward over the UNION of the calls in one launch sequence: the reference
+// runs the model three times per step (pinsage_training.py:184-186) and each
+// output row depends only on its own node's subtree, so computing every
+// distinct frontier node once gives the same values.  The reference's gradient
+// semantics for repeated batch ids (index_put backward hands each repeated
+// output row the summed gradient, pinsage_model.py:29,265) are reproduced in
+// the loss kernel per call.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "gemm.h"
+
+namespace ps {
+
+// launchers from frontier.hip / conv.hip
+int64_t bitset_words(int64_t universe);
+int64_t bitset_blocks(int64_t universe);
+int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
+int launch_mark_table(unsigned long long*, const int32_t*, const int*, int64_t, const int32_t*,
+                      int64_t, int, hipStream_t);
+int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
+                        int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
+int launch_rank_list(const unsigned long long*, const uint32_t*, const int64_t*, int64_t, int32_t*,
+                     hipStream_t);
+int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const int*, int64_t,
+                      const unsigned long long*, const uint32_t*, const unsigned long long*,
+                      const uint32_t*, const int32_t*, const float*, int64_t, int, int32_t*,
+                      int32_t*, int32_t*, float*, hipStream_t);
+int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
+               hipStream_t);
+int launch_csr_build(const int32_t*, const int*, int64_t, int, const int*, int64_t, int*, int*,
+                     int*, int*, int32_t*, int32_t*, hipStream_t);
+int launch_dq_segment(const int32_t*, const int32_t*, const float*, int, const float*, int64_t,
+                      const float*, int, const int*, int64_t, const int*, int64_t, float*,
+                      hipStream_t);
+int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
+                          float*, hipStream_t);
+int launch_colsum_partial(const float*, int, int64_t, const int*, int, int, float*, hipStream_t);
+int launch_reduce_slabs(const float*, int, int64_t, int64_t, float*, hipStream_t);
+int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
+                const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
+                hipStream_t);
+int launch_adam(float*, const float*, float*, float*, int64_t, const float*, int*, float, float,
+                float, hipStream_t);
+int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, hipStream_t);
+int launch_gather_out(const float*, int, const int32_t*, int64_t, float*, hipStream_t);
+int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
+                        int*, float*, hipStream_t);
+
+struct EngineConfig {
+  int64_t n_items;   // rows of the feature table (track universe)
+  int64_t d_in;      // feature dim
+  int64_t hid;       // hidden_dim (Q output)
+  int64_t out;       // out_dim
+  int64_t n_layers;
+  int64_t T;         // neighbourhood size used by the model
+  int64_t max_pos;   // max ids per forward (e.g. 3 * batch_size)
+};
+
+struct SetBuf {
+  int64_t cap = 0;
+  size_t bits = 0, prefix = 0, members = 0, count = 0;
+};
+
+struct LayerBuf {
+  SetBuf S, N;      // frontier S_l and its neighbour set N_l
+  int64_t d = 0;    // input dim of the layer
+  size_t self_src = 0, q_src = 0, loc = 0, wloc = 0;
+  size_t q = 0, agg = 0, y = 0, nrm = 0;
+  // backward
+  size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, occ = 0,
+         occ_u = 0;
+  // parameter offsets (floats) into the flat param / grad buffers
+  int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
+};
+
+// Optional HIP-event timing of launch sites on the launch stream (bench only).
+struct TimingSite {
+  std::string name;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double ms = 0.0;
+  int64_t calls = 0;
+};
+
+struct Engine {
+  EngineConfig cfg{};
+  bool timing = false;
+  std::vector<TimingSite> sites;
+  std::vector<LayerBuf> L;
+  int64_t pG1w = 0, pG1b = 0, pG2w = 0, n_params = 0;
+  // workspace layout
+  size_t bits_begin = 0, bits_end = 0;  // all bitmaps contiguous (one memset)
+  size_t block_sums = 0, ids = 0, pos_rank = 0, H1 = 0, Z = 0, dZ = 0, dP1 = 0;
+  size_t G = 0, Kc = 0, part = 0, scal = 0, err = 0, slab = 0, colpart = 0, varpart = 0;
+  int64_t slab_floats = 0;
+  size_t total = 0;
+  int64_t max_bsum_blocks = 0;
+  // external device pointers (owned by the caller)
+  const float* feats = nullptr;
+  int64_t ld_f = 0;
+  const int32_t* nb = nullptr;
+  const float* wn = nullptr;
+  int64_t ldT = 0;
+  float* params = nullptr;
+  float* grads = nullptr;
+  float* adam_m = nullptr;
+  float* adam_v = nullptr;
+};
+
+struct Timed {
+  Engine& E;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  TimingSite* site = nullptr;
+  Timed(Engine& e, const std::string& name, hipStream_t s) : E(e), st(s) {
+    if (!E.timing) return;
+    for (auto& t : E.sites)
+      if (t.name == name) site = &t;
+    if (!site) {
+      E.sites.push_back(TimingSite{name, {}, 0.0, 0});
+      site = &E.sites.back();
+    }
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, st);
+  }
+  void stop() {
+    if (!site) return;
+    hipEventRecord(b, st);
+    site->pending.emplace_back(a, b);
+    site = nullptr;
+  }
+  ~Timed() { stop(); }
+};
+
+static std::string lname(const char* base, int l) { return std::string(base) + ".l" + std::to_string(l); }
+
+static size_t carve(size_t& cur, int64_t bytes) {
+  cur = (size_t)align_up((int64_t)cur, 256);
+  size_t at = cur;
+  cur += (size_t)std::max<int64_t>(bytes, 0);
+  return at;
+}
+
+constexpr int kColsumBlocks = 32;  // row chunks of the bias-gradient column sums
+
+static int choose_splits(int64_t M, int64_t N, int64_t Kmax) {
+  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int64_t s = std::max<int64_t>(1, 512 / std::max<int64_t>(1, tiles));
+  s = std::min<int64_t>(s, std::max<int64_t>(1, Kmax / 256));
+  return (int)std::min<int64_t>(s, 64);
+}
+
+static void layout(Engine& E) {
+  const EngineConfig& c = E.cfg;
+  const int64_t n = c.n_items, Lc = c.n_layers, T = c.T;
+  E.L.assign((size_t)Lc, LayerBuf());
+  // capacities, top-down
+  int64_t capS = std::min(n, c.max_pos);
+  for (int64_t l = Lc - 1; l >= 0; --l) {
+    LayerBuf& lb = E.L[(size_t)l];
+    lb.d = (l == 0) ? c.d_in : c.out;
+    lb.S.cap = capS;
+    lb.N.cap = std::min(n, capS * T);
+    capS = std::min(n, lb.N.cap + lb.S.cap);
+  }
+  // parameter offsets in state_dict order
+  int64_t po = 0;
+  for (int64_t l = 0; l < Lc; ++l) {
+    LayerBuf& lb = E.L[(size_t)l];
+    lb.pQw = po; po += c.hid * lb.d;
+    lb.pQb = po; po += c.hid;
+    lb.pWw = po; po += c.out * (lb.d + c.hid);
+    lb.pWb = po; po += c.out;
+  }
+  E.pG1w = po; po += c.out * c.out;
+  E.pG1b = po; po += c.out;
+  E.pG2w = po; po += c.out * c.out;
+  E.n_params = po;
+
+  size_t cur = 0;
+  const int64_t nw = bitset_words(n);
+  E.max_bsum_blocks = bitset_blocks(n);
+  E.bits_begin = carve(cur, 0);
+  for (auto& lb : E.L) {
+    lb.S.bits = carve(cur, nw * 8);
+    lb.N.bits = carve(cur, nw * 8);
+  }
+  E.bits_end = carve(cur, 0);
+  const int64_t scan_blocks = std::max<int64_t>(E.max_bsum_blocks, 1);
+  E.block_sums = carve(cur, scan_blocks * 4);
+  for (auto& lb : E.L) {
+    for (SetBuf* sb : {&lb.S, &lb.N}) {
+      sb->prefix = carve(cur, nw * 4);
+      sb->members = carve(cur, sb->cap * 4);
+      sb->count = carve(cur, 16);
+    }
+    const int64_t FS = lb.S.cap, FN = lb.N.cap;
+    lb.self_src = carve(cur, FS * 4);
+    lb.q_src = carve(cur, FN * 4);
+    lb.loc = carve(cur, FS * T * 4);
+    lb.wloc = carve(cur, FS * T * 4);
+    lb.q = carve(cur, FN * c.hid * 4);
+    lb.agg = carve(cur, FS * c.hid * 4);
+    lb.y = carve(cur, FS * c.out * 4);
+    lb.nrm = carve(cur, FS * 4);
+    lb.dY = carve(cur, FS * c.out * 4);
+    lb.dp = carve(cur, FS * c.out * 4);
+    lb.dagg = carve(cur, FS * c.hid * 4);
+    lb.dpq = carve(cur, FN * c.hid * 4);
+    lb.cnt = carve(cur, (FN + 1) * 4);
+    lb.bsum = carve(cur, (int64_t)ceil_div(FN + 1, 1024) * 4 + 16);
+    lb.off = carve(cur, (FN + 1) * 4);
+    lb.cursor = carve(cur, (FN + 1) * 4);
+    lb.occ = carve(cur, FS * T * 4);
+    lb.occ_u = carve(cur, FS * T * 4);
+  }
+  const int64_t top = E.L.back().S.cap;
+  E.ids = carve(cur, c.max_pos * 8);
+  E.pos_rank = carve(cur, c.max_pos * 4);
+  E.H1 = carve(cur, top * c.out * 4);
+  E.Z = carve(cur, top * c.out * 4);
+  E.dZ = carve(cur, top * c.out * 4);
+  E.dP1 = carve(cur, top * c.out * 4);
+  E.G = carve(cur, 3 * top * c.out * 4);
+  E.Kc = carve(cur, 3 * top * 4);
+  E.part = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * 4 * 4);
+  E.varpart = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * c.out * 4);
+  E.scal = carve(cur, 64);
+  E.err = carve(cur, 16);
+  // split-K slabs: max over the weight-gradient GEMMs
+  int64_t slab = 0;
+  for (auto& lb : E.L) {
+    slab = std::max(slab, (int64_t)choose_splits(c.hid, lb.d, lb.N.cap) * c.hid * lb.d);
+    slab = std::max(slab, (int64_t)choose_splits(c.out, lb.d + c.hid, lb.S.cap) * c.out *
+                              (lb.d + c.hid));
+  }
+  slab = std::max(slab, (int64_t)choose_splits(c.out, c.out, top) * c.out * c.out);
+  E.slab_floats = slab;
+  E.slab = carve(cur, slab * 4);
+  E.colpart = carve(cur, kColsumBlocks * std::max(c.hid, c.out) * 4);
+  E.total = (size_t)align_up((int64_t)cur, 256);
+}
+
+template <class T>
+static inline T* at(void* ws, size_t off) {
+  return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+// ---------------------------------------------------------------- forward
+int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st) {
+  const EngineConfig& c = E.cfg;
+  PS_REQUIRE(E.feats && E.nb && E.wn && E.params, kErrArg, "engine: pointers not set");
+  PS_REQUIRE(n_pos > 0 && n_pos <= c.max_pos, kErrArg, "engine: n_pos out of range");
+  const int Lc = (int)c.n_layers, T = (int)c.T;
+  const int64_t n = c.n_items;
+  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.bits_begin), 0, E.bits_end - E.bits_begin, st));
+  PS_CHECK_HIP(hipMemsetAsync(at<int>(ws, E.err), 0, 16, st));
+  if (ids_dev != at<int64_t>(ws, E.ids))
+    PS_CHECK_HIP(hipMemcpyAsync(at<int64_t>(ws, E.ids), ids_dev, (size_t)n_pos * 8,
+                                hipMemcpyDeviceToDevice, st));
+  const int64_t* ids = at<int64_t>(ws, E.ids);
+  uint32_t* bsum = at<uint32_t>(ws, E.block_sums);
+  auto bits = [&](const SetBuf& s) { return at<unsigned long long>(ws, s.bits); };
+  auto pref = [&](const SetBuf& s) { return at<uint32_t>(ws, s.prefix); };
+  auto mem = [&](const SetBuf& s) { return at<int32_t>(ws, s.members); };
+  auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
+
+  // frontier, top-down
+  LayerBuf& top = E.L[(size_t)Lc - 1];
+  Timed t_front(E, "fwd.frontier", st);
+  PS_TRY(launch_mark_i64(bits(top.S), ids, n_pos, n, at<int>(ws, E.err), st));
+  PS_TRY(launch_set_finalize(bits(top.S), bits(top.S), nullptr, n, bsum, pref(top.S), mem(top.S),
+                             cnt(top.S), st));
+  for (int l = Lc - 1; l >= 0; --l) {
+    LayerBuf& lb = E.L[(size_t)l];
+    PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, E.nb, E.ldT, T, st));
+    PS_TRY(launch_set_finalize(bits(lb.N), bits(lb.N), nullptr, n, bsum, pref(lb.N), mem(lb.N),
+                               cnt(lb.N), st));
+    if (l > 0) {
+      LayerBuf& lo = E.L[(size_t)l - 1];
+      PS_TRY(launch_set_finalize(bits(lo.S), bits(lb.N), bits(lb.S), n, bsum, pref(lo.S), mem(lo.S),
+                                 cnt(lo.S), st));
+    }
+  }
+  PS_TRY(launch_rank_list(bits(top.S), pref(top.S), ids, n_pos, at<int32_t>(ws, E.pos_rank), st));
+  t_front.stop();
+
+  // layers, bottom-up
+  for (int l = 0; l < Lc; ++l) {
+    LayerBuf& lb = E.L[(size_t)l];
+    const SetBuf* prev = l > 0 ? &E.L[(size_t)l - 1].S : nullptr;
+    PS_TRY(launch_layer_prep(mem(lb.S), cnt(lb.S), lb.S.cap, mem(lb.N), cnt(lb.N), lb.N.cap,
+                             bits(lb.N), pref(lb.N), prev ? bits(*prev) : nullptr,
+                             prev ? pref(*prev) : nullptr, E.nb, E.wn, E.ldT, T,
+                             at<int32_t>(ws, lb.self_src), at<int32_t>(ws, lb.q_src),
+                             at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), st));
+    const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
+    const int64_t ldh = l == 0 ? E.ld_f : c.out;
+    // Q projection of the distinct neighbours: lrelu(h[u] Q^T + b)
+    GemmParams q;
+    q.M_dev = cnt(lb.N);
+    q.M_max = (int)lb.N.cap;
+    q.N = (int)c.hid;
+    q.K = (int)lb.d;
+    q.a = h;
+    q.lda = ldh;
+    q.a_idx = at<int32_t>(ws, lb.q_src);
+    q.b = E.params + lb.pQw;
+    q.ldb = lb.d;
+    q.c = at<float>(ws, lb.q);
+    q.ldc = c.hid;
+    q.bias = E.params + lb.pQb;
+    q.act = true;
+    {
+      Timed tt(E, lname("fwd.q_gemm", l), st);
+      PS_TRY(launch_gemm(q, st));
+    }
+    Timed t_agg(E, lname("fwd.agg", l), st);
+    PS_TRY(launch_agg(at<float>(ws, lb.q), (int)c.hid, at<int32_t>(ws, lb.loc),
+                      at<float>(ws, lb.wloc), T, cnt(lb.S), lb.S.cap, at<float>(ws, lb.agg), st));
+    t_agg.stop();
+    // W projection of [h_self || agg] with bias, lrelu and row L2 norm fused
+    GemmParams w;
+    w.M_dev = cnt(lb.S);
+    w.M_max = (int)lb.S.cap;
+    w.N = (int)c.out;
+    w.K = (int)(lb.d + c.hid);
+    w.a = h;
+    w.lda = ldh;
+    w.a_idx = at<int32_t>(ws, lb.self_src);
+    w.K1 = (int)lb.d;
+    w.a2 = at<float>(ws, lb.agg);
+    w.lda2 = c.hid;
+    w.b = E.params + lb.pWw;
+    w.ldb = lb.d + c.hid;
+    w.c = at<float>(ws, lb.y);
+    w.ldc = c.out;
+    w.bias = E.params + lb.pWb;
+    w.epi = kEpiL2Norm;
+    w.norms = at<float>(ws, lb.nrm);
+    Timed tw(E, lname("fwd.w_gemm", l), st);
+    PS_TRY(launch_gemm(w, st));
+  }
+  // head: G2(lrelu(G1 y))
+  Timed t_head(E, "fwd.head", st);
+  GemmParams g1;
+  g1.M_dev = cnt(top.S);
+  g1.M_max = (int)top.S.cap;
+  g1.N = (int)c.out;
+  g1.K = (int)c.out;
+  g1.a = at<float>(ws, top.y);
+  g1.lda = c.out;
+  g1.b = E.params + E.pG1w;
+  g1.ldb = c.out;
+  g1.c = at<float>(ws, E.H1);
+  g1.ldc = c.out;
+  g1.bias = E.params + E.pG1b;
+  g1.act = true;
+  PS_TRY(launch_gemm(g1, st));
+  GemmParams g2 = g1;
+  g2.a = at<float>(ws, E.H1);
+  g2.b = E.params + E.pG2w;
+  g2.c = at<float>(ws, E.Z);
+  g2.bias = nullptr;
+  g2.act = false;
+  PS_TRY(launch_gemm(g2, st));
+  return kOk;
+}
+
+// weight gradient dst[M][N] (+ column offset) = A^T B over the device row count
+static int weight_grad(Engine& E, void* ws, const float* A, int64_t lda, int M, const float* B,
+                       int64_t ldb, const int32_t* b_idx, int N, const int* K_dev, int64_t K_max,
+                       float* dst, int64_t ld_dst, hipStream_t st) {
+  const int S = choose_splits(M, N, K_max);
+  GemmParams p;
+  p.M = M;
+  p.N = N;
+  p.K_dev = K_dev;
+  p.K_max = (int)K_max;
+  p.a_kmajor = false;
+  p.a = A;
+  p.lda = lda;
+  p.b_kmajor = false;
+  p.b = B;
+  p.ldb = ldb;
+  p.b_idx = b_idx;
+  p.c = at<float>(ws, E.slab);
+  p.ldc = N;
+  p.epi = kEpiPartial;
+  p.splits = S;
+  PS_REQUIRE((int64_t)S * M * N <= E.slab_floats, kErrWorkspace, "engine: split-K slab too small");
+  PS_TRY(launch_gemm(p, st));
+  return launch_reduce_slabs_2d(at<float>(ws, E.slab), S, (int64_t)M * N, M, N, dst, ld_dst, st);
+}
+
+static int bias_grad(Engine& E, void* ws, const float* X, int n, const int* rows_dev, float* dst,
+                     hipStream_t st) {
+  PS_TRY(launch_colsum_partial(X, n, n, rows_dev, 0, kColsumBlocks, at<float>(ws, E.colpart), st));
+  return launch_reduce_slabs(at<float>(ws, E.colpart), kColsumBlocks, n, n, dst, st);
+}
+
+// ---------------------------------------------------------------- backward
+// Starts from dZ (gradient of the head output rows of the unique top nodes).
+int engine_backward(Engine& E, void* ws, hipStream_t st) {
+  const EngineConfig& c = E.cfg;
+  PS_REQUIRE(E.grads, kErrArg, "engine: grad buffer not set");
+  const int Lc = (int)c.n_layers, T = (int)c.T;
+  auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
+  LayerBuf& top = E.L[(size_t)Lc - 1];
+  const int o = (int)c.out, hd = (int)c.hid;
+  float* gr = E.grads;
+  Timed t_hb(E, "bwd.head", st);
+  // head: Z = H1 G2^T, H1 = lrelu(y G1^T + b1)
+  PS_TRY(weight_grad(E, ws, at<float>(ws, E.dZ), o, o, at<float>(ws, E.H1), o, nullptr, o,
+                     cnt(top.S), top.S.cap, gr + E.pG2w, o, st));
+  {
+    GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
+    p.M_dev = cnt(top.S);
+    p.M_max = (int)top.S.cap;
+    p.N = o;
+    p.K = o;
+    p.a = at<float>(ws, E.dZ);
+    p.lda = o;
+    p.b_kmajor = false;
+    p.b = E.params + E.pG2w;
+    p.ldb = o;
+    p.c = at<float>(ws, E.dP1);
+    p.ldc = o;
+    p.mask = at<float>(ws, E.H1);
+    p.ldm = o;
+    PS_TRY(launch_gemm(p, st));
+  }
+  PS_TRY(weight_grad(E, ws, at<float>(ws, E.dP1), o, o, at<float>(ws, top.y), o, nullptr, o,
+                     cnt(top.S), top.S.cap, gr + E.pG1w, o, st));
+  PS_TRY(bias_grad(E, ws, at<float>(ws, E.dP1), o, cnt(top.S), gr + E.pG1b, st));
+  {
+    GemmParams p;  // dY_top = dP1 G1
+    p.M_dev = cnt(top.S);
+    p.M_max = (int)top.S.cap;
+    p.N = o;
+    p.K = o;
+    p.a = at<float>(ws, E.dP1);
+    p.lda = o;
+    p.b_kmajor = false;
+    p.b = E.params + E.pG1w;
+    p.ldb = o;
+    p.c = at<float>(ws, top.dY);
+    p.ldc = o;
+    PS_TRY(launch_gemm(p, st));
+  }
+  t_hb.stop();
+  for (int l = Lc - 1; l >= 0; --l) {
+    Timed tb(E, lname("bwd.layer", l), st);
+    LayerBuf& lb = E.L[(size_t)l];
+    const int d = (int)lb.d;
+    const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
+    const int64_t ldh = l == 0 ? E.ld_f : c.out;
+    float* dp = at<float>(ws, lb.dp);
+    PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
+                                 o, cnt(lb.S), lb.S.cap, dp, st));
+    // dW = dp^T [h_self || agg]
+    PS_TRY(weight_grad(E, ws, dp, o, o, h, ldh, at<int32_t>(ws, lb.self_src), d, cnt(lb.S),
+                       lb.S.cap, gr + lb.pWw, d + hd, st));
+    PS_TRY(weight_grad(E, ws, dp, o, o, at<float>(ws, lb.agg), hd, nullptr, hd, cnt(lb.S), lb.S.cap,
+                       gr + lb.pWw + d, d + hd, st));
+    PS_TRY(bias_grad(E, ws, dp, o, cnt(lb.S), gr + lb.pWb, st));
+    float* dYprev = l > 0 ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr;
+    if (l > 0) {
+      PS_CHECK_HIP(hipMemsetAsync(dYprev, 0, (size_t)E.L[(size_t)l - 1].S.cap * o * 4, st));
+      GemmParams p;  // d_self = dp W[:, :d]  -> scatter-add into the rows of layer l-1
+      p.M_dev = cnt(lb.S);
+      p.M_max = (int)lb.S.cap;
+      p.N = d;
+      p.K = o;
+      p.a = dp;
+      p.lda = o;
+      p.b_kmajor = false;
+      p.b = E.params + lb.pWw;
+      p.ldb = d + hd;
+      p.c = dYprev;
+      p.ldc = o;
+      p.c_idx = at<int32_t>(ws, lb.self_src);
+      p.epi = kEpiAccum;
+      PS_TRY(launch_gemm(p, st));
+    }
+    {
+      GemmParams p;  // d_agg = dp W[:, d:]
+      p.M_dev = cnt(lb.S);
+      p.M_max = (int)lb.S.cap;
+      p.N = hd;
+      p.K = o;
+      p.a = dp;
+      p.lda = o;
+      p.b_kmajor = false;
+      p.b = E.params + lb.pWw + d;
+      p.ldb = d + hd;
+      p.c = at<float>(ws, lb.dagg);
+      p.ldc = hd;
+      PS_TRY(launch_gemm(p, st));
+    }
+    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
+                            at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
+                            at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
+                            st));
+    PS_TRY(launch_dq_segment(at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u), at<float>(ws, lb.wloc),
+                             T, at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, cnt(lb.S),
+                             lb.S.cap, cnt(lb.N), lb.N.cap, at<float>(ws, lb.dpq), st));
+    // dQ = dpq^T h[q_src]
+    Timed tq(E, lname("bwd.q_wgrad", l), st);
+    PS_TRY(weight_grad(E, ws, at<float>(ws, lb.dpq), hd, hd, h, ldh, at<int32_t>(ws, lb.q_src), d,
+                       cnt(lb.N), lb.N.cap, gr + lb.pQw, d, st));
+    PS_TRY(bias_grad(E, ws, at<float>(ws, lb.dpq), hd, cnt(lb.N), gr + lb.pQb, st));
+    if (l > 0) {
+      GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
+      p.M_dev = cnt(lb.N);
+      p.M_max = (int)lb.N.cap;
+      p.N = d;
+      p.K = hd;
+      p.a = at<float>(ws, lb.dpq);
+      p.lda = hd;
+      p.b_kmajor = false;
+      p.b = E.params + lb.pQw;
+      p.ldb = d;
+      p.c = dYprev;
+      p.ldc = o;
+      p.c_idx = at<int32_t>(ws, lb.q_src);
+      p.epi = kEpiAccum;
+      PS_TRY(launch_gemm(p, st));
+    }
+  }
+  return kOk;
+}
+
+}  // namespace ps
+
+// ============================================================================ C-ABI
+#include "../../include/pinsage_hip.h"
+
+using namespace ps;
+
+extern "C" {
+
+int pinsage_engine_create(const pinsage_engine_config* cfg, pinsage_engine** out) {
+  if (!cfg || !out) {
+    set_error("engine_create: null argument");
+    return kErrArg;
+  }
+  if (cfg->n_items <= 0 || cfg->d_in <= 0 || cfg->hid <= 0 || cfg->out <= 0 || cfg->n_layers <= 0 ||
+      cfg->T <= 0 || cfg->max_pos <= 0) {
+    set_error("engine_create: all sizes must be positive");
+    return kErrArg;
+  }
+  if (cfg->d_in % 4 || cfg->hid % 4 || cfg->out % 4) {
+    set_error("engine_create: d_in, hidden_dim and out_dim must be multiples of 4");
+    return kErrArg;
+  }
+  if (cfg->out > 128) {
+    set_error("engine_create: out_dim > 128 is not supported by the fused L2-norm epilogue");
+    return kErrArg;
+  }
+  if (cfg->d_in < cfg->out) {
+    // put_embeddings pads the conv output to the feature width (pinsage_model.py:27-29)
+    set_error("engine_create: d_in < out_dim (the reference fails in put_embeddings)");
+    return kErrArg;
+  }
+  auto* E = new Engine();
+  E->cfg = EngineConfig{cfg->n_items, cfg->d_in, cfg->hid, cfg->out, cfg->n_layers, cfg->T,
+                        cfg->max_pos};
+  layout(*E);
+  *out = reinterpret_cast<pinsage_engine*>(E);
+  return kOk;
+}
+
+void pinsage_engine_destroy(pinsage_engine* e) { delete reinterpret_cast<Engine*>(e); }
+
+int64_t pinsage_engine_workspace_bytes(const pinsage_engine* e) {
+  return (int64_t) reinterpret_cast<const Engine*>(e)->total;
+}
+
+int64_t pinsage_engine_num_params(const pinsage_engine* e) {
+  return reinterpret_cast<const Engine*>(e)->n_params;
+}
+
+int pinsage_engine_set_tensors(pinsage_engine* e, const float* feats, int64_t ld_feats,
+                               const int32_t* nb_table, const float* w_table, int64_t ld_table,
+                               float* params, float* grads, float* adam_m, float* adam_v) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  if (ld_table < E->cfg.T || ld_feats < E->cfg.d_in) {
+    set_error("engine_set_tensors: leading dimension too small");
+    return kErrArg;
+  }
+  E->feats = feats;
+  E->ld_f = ld_feats;
+  E->nb = nb_table;
+  E->wn = w_table;
+  E->ldT = ld_table;
+  E->params = params;
+  E->grads = grads;
+  E->adam_m = adam_m;
+  E->adam_v = adam_v;
+  return kOk;
+}
+
+int pinsage_engine_offsets(const pinsage_engine* e, pinsage_engine_offsets_t* o) {
+  const Engine* E = reinterpret_cast<const Engine*>(e);
+  o->ids = (int64_t)E->ids;
+  o->pos_rank = (int64_t)E->pos_rank;
+  o->z = (int64_t)E->Z;
+  o->dz = (int64_t)E->dZ;
+  o->scalars = (int64_t)E->scal;
+  o->err = (int64_t)E->err;
+  o->n_layers = E->cfg.n_layers;
+  for (int64_t l = 0; l < E->cfg.n_layers && l < 8; ++l) {
+    o->count_S[l] = (int64_t)E->L[(size_t)l].S.count;
+    o->count_N[l] = (int64_t)E->L[(size_t)l].N.count;
+    o->members_S[l] = (int64_t)E->L[(size_t)l].S.members;
+    o->members_N[l] = (int64_t)E->L[(size_t)l].N.members;
+    o->cap_S[l] = E->L[(size_t)l].S.cap;
+    o->cap_N[l] = E->L[(size_t)l].N.cap;
+    o->y[l] = (int64_t)E->L[(size_t)l].y;
+  }
+  for (int l = 0; l < 8; ++l) o->param_offsets[l] = 0;
+  return kOk;
+}
+
+int pinsage_engine_timing(pinsage_engine* e, int enable) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  for (auto& t : E->sites)
+    for (auto& pr : t.pending) {
+      hipEventDestroy(pr.first);
+      hipEventDestroy(pr.second);
+    }
+  E->sites.clear();
+  E->timing = enable != 0;
+  return kOk;
+}
+
+int pinsage_engine_timing_collect(pinsage_engine* e) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  for (auto& t : E->sites) {
+    for (auto& pr : t.pending) {
+      PS_CHECK_HIP(hipEventSynchronize(pr.second));
+      float ms = 0.f;
+      PS_CHECK_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+      t.ms += ms;
+      t.calls += 1;
+      hipEventDestroy(pr.first);
+      hipEventDestroy(pr.second);
+    }
+    t.pending.clear();
+  }
+  return kOk;
+}
+
+int pinsage_engine_timing_get(const pinsage_engine* e, int idx, char* name, int64_t name_len,
+                              double* ms, int64_t* calls) {
+  const Engine* E = reinterpret_cast<const Engine*>(e);
+  if (idx < 0 || idx >= (int)E->sites.size()) return kErrArg;
+  const TimingSite& t = E->sites[(size_t)idx];
+  std::strncpy(name, t.name.c_str(), (size_t)name_len - 1);
+  name[name_len - 1] = 0;
+  *ms = t.ms;
+  *calls = t.calls;
+  return kOk;
+}
+
+int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
+                           void* stream) {
+  return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
+}
+
+int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
+                                 void* stream) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  return launch_gather_out(at<float>(ws, E->Z), (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
+                           out, (hipStream_t)stream);
+}
+
+int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float margin,
+                        int with_monitors, void* stream) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  const EngineConfig& c = E->cfg;
+  if (3 * batch_size > c.max_pos || batch_size < 2) {
+    set_error("engine_loss: batch_size out of range (the reference needs B >= 2)");
+    return kErrArg;
+  }
+  LayerBuf& top = E->L.back();
+  Timed t(*E, "loss", (hipStream_t)stream);
+  return launch_loss(at<float>(ws, E->Z), (int)c.out, at<int32_t>(ws, E->pos_rank), (int)batch_size,
+                     margin, with_monitors ? E->feats : nullptr, E->ld_f, (int)c.d_in,
+                     at<int64_t>(ws, E->ids), at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap,
+                     at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
+                     at<float>(ws, E->varpart), at<float>(ws, E->scal), (hipStream_t)stream);
+}
+
+int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,
+                                   void* stream) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  LayerBuf& top = E->L.back();
+  return launch_dz_from_dout(dout, (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
+                             at<int>(ws, top.S.count), top.S.cap, at<float>(ws, E->G),
+                             at<int>(ws, E->Kc), at<float>(ws, E->dZ), (hipStream_t)stream);
+}
+
+int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream) {
+  return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
+}
+
+int pinsage_engine_adam(pinsage_engine* e, const float* lr_dev, int32_t* step_dev, float beta1,
+                        float beta2, float eps, void* stream) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  Timed t(*E, "adam", (hipStream_t)stream);
+  if (!E->adam_m || !E->adam_v) {
+    set_error("engine_adam: optimizer state not set");
+    return kErrArg;
+  }
+  return launch_adam(E->params, E->grads, E->adam_m, E->adam_v, E->n_params, lr_dev, step_dev, beta1,
+                     beta2, eps, (hipStream_t)stream);
+}
+
+}  // extern "C"

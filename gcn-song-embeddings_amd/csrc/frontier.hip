@@ -1,0 +1,225 @@
+// Frontier construction on gfx950 (relevant_nodes_per_layer_precomp,
+// pinsage_model.py:156-168): the reference builds each lower layer as
+// unique(cat(nb.flatten(), nodeset)) with a sort.  Here a node set over the
+// track universe [0, n) is a bitmap: marking is one atomicOr per id, the
+// sorted unique list and every id's rank come from a per-word popcount prefix,
+// so no sort runs and ranks are O(1) lookups (bitmap + prefix stay in L2).
+#include "common.h"
+
+namespace ps {
+
+constexpr int kScanBlock = 256;
+constexpr int kWordsPerThread = 4;
+constexpr int kWordsPerBlock = kScanBlock * kWordsPerThread;  // 1024 words = 64k ids
+
+// test before set: popular ids are marked by thousands of lanes; a plain load
+// of an already-set bit avoids serialising them on one atomic word
+__device__ __forceinline__ void mark(unsigned long long* bits, int64_t v) {
+  const unsigned long long bit = 1ull << (v & 63);
+  if (!(__hip_atomic_load(bits + (v >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+    atomicOr(bits + (v >> 6), bit);
+}
+
+__device__ __forceinline__ int32_t rank_of(const unsigned long long* bits, const uint32_t* prefix,
+                                           int64_t v) {
+  const unsigned long long w = bits[v >> 6];
+  return (int32_t)(prefix[v >> 6] + __popcll(w & ((1ull << (v & 63)) - 1ull)));
+}
+
+// mark a list of int64 ids (host-known count)
+__global__ void bits_mark_i64_kernel(unsigned long long* __restrict__ bits,
+                                     const int64_t* __restrict__ ids, int64_t n, int64_t limit,
+                                     int* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = ids[i];
+    if (v < 0 || v >= limit) {
+      atomicExch(err, 1);
+      continue;
+    }
+    mark(bits, v);
+  }
+}
+
+// mark nb_table[members[f]][t] for f < *count, t < T (table row stride ld)
+__global__ void bits_mark_table_kernel(unsigned long long* __restrict__ bits,
+                                       const int32_t* __restrict__ members,
+                                       const int* __restrict__ count, const int32_t* __restrict__ nb,
+                                       int64_t ld, int T) {
+  const int64_t n = (int64_t)(*count) * T;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = e / T, t = e - f * T;
+    mark(bits, nb[(int64_t)members[f] * ld + t]);
+  }
+}
+
+// mark nb_table[ids[i]][t] for an int64 id list (API frontier step)
+__global__ void bits_mark_table_i64_kernel(unsigned long long* __restrict__ bits,
+                                           const int64_t* __restrict__ ids, int64_t n,
+                                           const int32_t* __restrict__ nb, int64_t ld, int T,
+                                           int64_t limit, int* __restrict__ err) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * T;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = e / T, t = e - f * T;
+    const int64_t v = nb[ids[f] * ld + t];
+    if (v < 0 || v >= limit) {
+      atomicExch(err, 1);
+      continue;
+    }
+    mark(bits, v);
+  }
+}
+
+// dst = a | b (b may be null); per-block popcount totals
+__global__ __launch_bounds__(kScanBlock) void bits_or_count_kernel(
+    unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ a,
+    const unsigned long long* __restrict__ b, int64_t nwords, uint32_t* __restrict__ block_sums) {
+  __shared__ int red[kScanBlock / 64];
+  const int64_t w0 = (int64_t)blockIdx.x * kWordsPerBlock + threadIdx.x * kWordsPerThread;
+  int c = 0;
+#pragma unroll
+  for (int q = 0; q < kWordsPerThread; ++q) {
+    const int64_t w = w0 + q;
+    if (w < nwords) {
+      unsigned long long x = a[w];
+      if (b) x |= b[w];
+      if (dst != a || b) dst[w] = x;
+      c += __popcll(x);
+    }
+  }
+  c = wave_sum_i(c);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int i = 0; i < kScanBlock / 64; ++i) t += red[i];
+    block_sums[blockIdx.x] = (uint32_t)t;
+  }
+}
+
+// per-word exclusive prefix + sorted member list + total count
+__global__ __launch_bounds__(kScanBlock) void bits_scan_compact_kernel(
+    const unsigned long long* __restrict__ bits, int64_t nwords,
+    const uint32_t* __restrict__ block_sums, uint32_t* __restrict__ prefix,
+    int32_t* __restrict__ members, int* __restrict__ count_out) {
+  __shared__ uint32_t wsum[kScanBlock / 64];
+  __shared__ uint32_t base_sh;
+  // offset of this block = sum of the preceding blocks' totals
+  uint32_t off = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += kScanBlock) off += block_sums[i];
+  off = (uint32_t)wave_sum_i((int)off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = off;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < kScanBlock / 64; ++i) t += wsum[i];
+    base_sh = t;
+  }
+  __syncthreads();
+  const uint32_t base = base_sh;
+  __syncthreads();
+  const int64_t w0 = (int64_t)blockIdx.x * kWordsPerBlock + threadIdx.x * kWordsPerThread;
+  unsigned long long x[kWordsPerThread];
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < kWordsPerThread; ++q) {
+    x[q] = (w0 + q < nwords) ? bits[w0 + q] : 0ull;
+    c += __popcll(x[q]);
+  }
+  // inclusive wave scan of c
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t wo = 0;
+  for (int i = 0; i < wv; ++i) wo += wsum[i];
+  uint32_t p = base + wo + inc - c;
+#pragma unroll
+  for (int q = 0; q < kWordsPerThread; ++q) {
+    const int64_t w = w0 + q;
+    if (w < nwords) {
+      prefix[w] = p;
+      unsigned long long m = x[q];
+      uint32_t j = p;
+      while (m) {
+        const int bit = __ffsll((long long)m) - 1;
+        members[j++] = (int32_t)(w * 64 + bit);
+        m &= m - 1;
+      }
+      p += __popcll(x[q]);
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) *count_out = (int)p;
+}
+
+// ranks of an int64 id list (e.g. batch positions -> rows of the top set)
+__global__ void rank_list_kernel(const unsigned long long* __restrict__ bits,
+                                 const uint32_t* __restrict__ prefix, const int64_t* __restrict__ ids,
+                                 int64_t n, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = rank_of(bits, prefix, ids[i]);
+}
+
+// ---------------------------------------------------------------- host side
+int64_t bitset_words(int64_t universe) { return (universe + 63) / 64; }
+int64_t bitset_blocks(int64_t universe) { return ceil_div(bitset_words(universe), kWordsPerBlock); }
+
+int launch_mark_i64(unsigned long long* bits, const int64_t* ids, int64_t n, int64_t limit,
+                    int* err, hipStream_t st) {
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(bits_mark_i64_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, bits, ids, n,
+                     limit, err);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_mark_table(unsigned long long* bits, const int32_t* members, const int* count,
+                      int64_t max_count, const int32_t* nb, int64_t ld, int T, hipStream_t st) {
+  if (max_count <= 0) return kOk;
+  hipLaunchKernelGGL(bits_mark_table_kernel, dim3(grid_for(max_count * T, 256)), dim3(256), 0, st,
+                     bits, members, count, nb, ld, T);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_mark_table_i64(unsigned long long* bits, const int64_t* ids, int64_t n,
+                          const int32_t* nb, int64_t ld, int T, int64_t limit, int* err,
+                          hipStream_t st) {
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(bits_mark_table_i64_kernel, dim3(grid_for(n * T, 256)), dim3(256), 0, st, bits,
+                     ids, n, nb, ld, T, limit, err);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+// Finalise a set: dst = a | b, prefix, sorted members, device count.
+int launch_set_finalize(unsigned long long* dst, const unsigned long long* a,
+                        const unsigned long long* b, int64_t universe, uint32_t* block_sums,
+                        uint32_t* prefix, int32_t* members, int* count, hipStream_t st) {
+  const int64_t nw = bitset_words(universe);
+  const int nb = (int)bitset_blocks(universe);
+  hipLaunchKernelGGL(bits_or_count_kernel, dim3(nb), dim3(kScanBlock), 0, st, dst, a, b, nw,
+                     block_sums);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bits_scan_compact_kernel, dim3(nb), dim3(kScanBlock), 0, st, dst, nw,
+                     block_sums, prefix, members, count);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_rank_list(const unsigned long long* bits, const uint32_t* prefix, const int64_t* ids,
+                     int64_t n, int32_t* out, hipStream_t st) {
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(rank_list_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, bits, prefix, ids,
+                     n, out);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+}  // namespace ps

@@ -1,0 +1,54 @@
+// fp32 MFMA GEMM for the PinSage projections (Q, W, G1, G2 and their
+// backward products).  C[M,N] = op(A)[M,K] * op(B)[K,N] with:
+//   A K-major  ("N"): A(m,k) = a[row(m)*lda + k], row(m) = a_idx ? a_idx[m] : m
+//   A M-major  ("T"): A(m,k) = a[row(k)*lda + m], row(k) = a_idx ? a_idx[k] : k
+//   B K-major  ("T", nn.Linear weight [N][K]): B(k,n) = b[n*ldb + k]
+//   B N-major  ("N"): B(k,n) = b[row(k)*ldb + n], row(k) = b_idx ? b_idx[k] : k
+// An optional second K segment (K-major A only) implements torch.cat along K
+// without a concat buffer (pinsage_model.py:208).  M and K may be device-side
+// counts (data-dependent frontier sizes): the kernel is persistent and reads
+// them at run time, so no host sync is needed between frontier and GEMM.
+#pragma once
+#include "common.h"
+
+namespace ps {
+
+enum GemmEpi : int {
+  kEpiStore = 0,    // C = acc (+bias) (lrelu) (*lrelu'(mask))   [C row via c_idx]
+  kEpiAccum = 1,    // C += acc (same options)
+  kEpiL2Norm = 2,   // y = normalize(lrelu(acc + bias)) per row; norms[m] = ||.||  (N <= 128)
+  kEpiPartial = 3,  // split-K slab: C[split][M][N] = acc
+};
+
+struct GemmParams {
+  int M = 0, N = 0, K = 0;
+  const int* M_dev = nullptr;  // if set, M = *M_dev (<= M_max for the grid)
+  const int* K_dev = nullptr;  // if set, K = *K_dev
+  int M_max = 0, K_max = 0;
+  bool a_kmajor = true, b_kmajor = true;
+  const float* a = nullptr;
+  int64_t lda = 0;
+  const int32_t* a_idx = nullptr;
+  // second K segment of A (K-major only): used for k >= K1
+  int K1 = -1;
+  const float* a2 = nullptr;
+  int64_t lda2 = 0;
+  const int32_t* a2_idx = nullptr;
+  const float* b = nullptr;
+  int64_t ldb = 0;
+  const int32_t* b_idx = nullptr;
+  float* c = nullptr;
+  int64_t ldc = 0;
+  const int32_t* c_idx = nullptr;  // output row scatter
+  int epi = kEpiStore;
+  const float* bias = nullptr;
+  bool act = false;               // leaky_relu
+  const float* mask = nullptr;    // multiply by lrelu'(mask[m*ldm + n])
+  int64_t ldm = 0;
+  float* norms = nullptr;         // kEpiL2Norm: per-row L2 norms
+  int splits = 1;                 // kEpiPartial: split-K count
+};
+
+int launch_gemm(const GemmParams& p, hipStream_t st);
+
+}  // namespace ps

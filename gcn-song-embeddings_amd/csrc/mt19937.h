@@ -1,0 +1,109 @@
+// Host-side MT19937 with torch's CPU-generator semantics (at::mt19937 and the
+// 5056-byte torch.get_rng_state() layout).  The product uses it to reproduce
+// the reference's RNG stream exactly (rng_mode "mt19937"):
+//   torch.randint(n, ())  -> raw % n             (n < 2^28: one 32-bit draw)
+//   torch.rand(())        -> (raw & 0xFFFFFF) * 2^-24 as float
+//   torch.randperm(n)     -> Fisher-Yates, one draw per step (n-1 draws)
+// (pinsage_model.py:42,45,50; pinsage_training.py:58,74).
+#pragma once
+#include <cstdint>
+#include <cstring>
+
+namespace ps {
+
+struct MTState {
+  static constexpr int N = 624;
+  static constexpr int M = 397;
+  uint64_t seed = 5489;
+  int32_t left = 1;    // draws until the next twist, torch convention (1 = twist due)
+  int32_t seeded = 1;
+  uint32_t next = 0;   // index of the next state word to temper
+  uint32_t s[N];
+
+  static inline uint32_t twist1(uint32_t u, uint32_t v) {
+    uint32_t y = (u & 0x80000000u) | (v & 0x7fffffffu);
+    return (y >> 1) ^ ((v & 1u) ? 0x9908b0dfu : 0u);
+  }
+  static inline uint32_t temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  void twist() {
+    int i = 0;
+    for (; i < N - M; ++i) s[i] = s[i + M] ^ twist1(s[i], s[i + 1]);
+    for (; i < N - 1; ++i) s[i] = s[i + M - N] ^ twist1(s[i], s[i + 1]);
+    s[N - 1] = s[M - 1] ^ twist1(s[N - 1], s[0]);
+    left = N;
+    next = 0;
+  }
+  void seed_with(uint64_t sd) {
+    seed = sd;
+    seeded = 1;
+    s[0] = (uint32_t)(sd & 0xffffffffu);
+    for (int j = 1; j < N; ++j) s[j] = 1812433253u * (s[j - 1] ^ (s[j - 1] >> 30)) + (uint32_t)j;
+    left = 1;
+    next = 0;
+  }
+  inline uint32_t draw() {
+    if (--left == 0) twist();
+    return temper(s[next++]);
+  }
+  // words available without a twist
+  inline int64_t avail() const { return (int64_t)left - 1; }
+  // Advance by n draws without tempering (twist-only); same end state as n draw()s.
+  void skip(int64_t n) {
+    while (n > 0) {
+      int64_t a = avail();
+      if (a == 0) {
+        twist();
+        left = N + 1;  // pretend the twisting draw has not consumed yet
+        a = N;
+      }
+      int64_t take = n < a ? n : a;
+      next += (uint32_t)take;
+      left -= (int32_t)take;
+      n -= take;
+    }
+  }
+
+  static constexpr int kTorchBytes = 5056;
+  bool from_torch(const uint8_t* b, int64_t nbytes) {
+    if (nbytes < 24 + 8 * N) return false;
+    uint64_t nx, st;
+    std::memcpy(&seed, b + 0, 8);
+    std::memcpy(&left, b + 8, 4);
+    std::memcpy(&seeded, b + 12, 4);
+    std::memcpy(&nx, b + 16, 8);
+    next = (uint32_t)nx;
+    for (int i = 0; i < N; ++i) {
+      std::memcpy(&st, b + 24 + 8 * i, 8);
+      s[i] = (uint32_t)st;
+    }
+    return left > 0 && left <= N + 1 && next <= (uint32_t)N;
+  }
+  void to_torch(uint8_t* b) const {
+    uint64_t nx = next, st;
+    std::memcpy(b + 0, &seed, 8);
+    std::memcpy(b + 8, &left, 4);
+    std::memcpy(b + 12, &seeded, 4);
+    std::memcpy(b + 16, &nx, 8);
+    for (int i = 0; i < N; ++i) {
+      st = s[i];
+      std::memcpy(b + 24 + 8 * i, &st, 8);
+    }
+  }
+};
+
+// Device-side chunk descriptor: the state words plus where the next draw comes
+// from.  A generator workgroup expands it into a run of raw draws.
+struct MTChunk {
+  uint32_t s[MTState::N];
+  uint32_t next;   // next word index
+  uint32_t avail;  // words usable before a twist
+  uint32_t pad[2];
+};
+
+}  // namespace ps

@@ -1,0 +1,539 @@
+"""Drop-in ``pinsage_model`` (reference ``pinsage_model.py``) on MI355X.
+
+Same names, signatures, return types and RNG consumption as the reference; the
+work runs in hand-written gfx950 kernels through ``libpinsage_hip.so``:
+
+* ``do_random_walks`` / ``sample_neighborhood[_topt]`` /
+  ``precompute_neighborhoods_topt`` -> walk + visit-count + libstdc++-exact
+  top-k kernels.  RNG mode ``"mt19937"`` (default) consumes torch's global CPU
+  generator draw-for-draw like the reference (bit-exact outputs); ``"philox"``
+  is a counter-based stream for throughput (``set_rng_mode``).
+* ``relevant_nodes_per_layer[_precomp]`` -> bitmap frontier kernels.
+* ``PinSageModel.forward`` -> the fused engine (frontier, fp32-MFMA Q/W
+  projections with fused epilogues, weighted aggregation, head), with a HIP
+  backward for autograd.
+
+Inputs may be CPU tensors (as the reference's callers pass); results come back
+on the device of the input.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+import _native as nat
+
+DEF_T_PRECOMP = 100
+DEF_HOPS = 500
+DEF_ALPHA = 0.85
+
+_RNG_MODE = "mt19937"
+_PHILOX_OFFSET = [0]
+
+
+def set_rng_mode(mode: str):
+    """'mt19937' (reference-exact, default) or 'philox' (counter-based, faster)."""
+    global _RNG_MODE
+    if mode not in ("mt19937", "philox"):
+        raise ValueError("rng mode must be 'mt19937' or 'philox'")
+    _RNG_MODE = mode
+
+
+def get_rng_mode() -> str:
+    return _RNG_MODE
+
+
+# ----------------------------------------------------------------------------- embeddings
+def get_embeddings(h, nodeset, d):
+    """h[nodeset, :d] (pinsage_model.py:21-22)."""
+    return h[nodeset, :d]
+
+
+def put_embeddings(h, nodeset, nodeset_new_h):
+    """Copy of h with rows ``nodeset`` replaced by zero-padded new rows
+    (pinsage_model.py:24-30).  The fused forward never materialises this copy;
+    the function is kept for API compatibility."""
+    new_h = h.clone().detach()
+    pad_cols = new_h.shape[1] - nodeset_new_h.shape[1]
+    pad = torch.zeros(nodeset.shape[0], pad_cols, dtype=nodeset_new_h.dtype, device=nodeset_new_h.device)
+    new_h[nodeset, :] = torch.cat([nodeset_new_h, pad], 1)
+    return new_h
+
+
+# ----------------------------------------------------------------------------- sampler
+def _as_csr(g):
+    if hasattr(g, "indptr") and hasattr(g, "indices"):
+        return g
+    raise TypeError("graph must be a graph.CSRGraph (spotify_graph.SpotifyGraph.to_dgl_graph())")
+
+
+def _walk_device(g, nodeset, n_hops, alpha):
+    """int32 trace [n, n_hops] on the GPU; consumes RNG like the reference."""
+    g = _as_csr(g)
+    dev = nat.device()
+    indptr, indices = g.device_csr(dev)
+    src = torch.as_tensor(nodeset).reshape(-1).to(device=dev, dtype=torch.int64)
+    n = int(src.shape[0])
+    n_all = g.number_of_nodes()
+    trace = torch.empty((n, int(n_hops)), dtype=torch.int32, device=dev)
+    if n == 0:
+        return src, trace
+    alpha32 = float(np.float32(alpha))
+    L = nat.lib()
+    if _RNG_MODE == "mt19937":
+        if g.max_degree() >= (1 << 28):
+            raise RuntimeError("degree >= 2^28: torch.randint switches to 64-bit draws; "
+                               "use rng mode 'philox'")
+        need = L.pinsage_walk_mt_workspace(n, int(n_hops))
+        cap = 2 << 30  # <= 2 GiB of raw MT words per round
+        ws = torch.empty(min(need, cap), dtype=torch.uint8, device=dev)
+        with nat.torch_rng() as mt:
+            nat.check(L.pinsage_walk_mt(nat.ptr(indptr), nat.ptr(indices), n_all, nat.ptr(src), n,
+                                        int(n_hops), alpha32, mt.p, nat.ptr(ws), ws.numel(),
+                                        nat.ptr(trace), nat.stream_ptr()), "walk")
+    else:
+        with nat.torch_rng() as mt:
+            d = mt.draws(2)
+        seed = (int(d[0]) << 32) | int(d[1])
+        nat.check(L.pinsage_walk_philox(nat.ptr(indptr), nat.ptr(indices), n_all, nat.ptr(src), n,
+                                        int(n_hops), alpha32, seed, 0, 0, nat.ptr(trace),
+                                        nat.stream_ptr()), "walk")
+    return src, trace
+
+
+def do_random_walks(g, nodeset, n_hops, alpha):
+    """Random walks with restart; int64 trace [len(nodeset), n_hops]
+    (pinsage_model.py:32-53)."""
+    _, trace = _walk_device(g, nodeset, n_hops, alpha)
+    out_dev = torch.as_tensor(nodeset).device
+    return trace.to(torch.int64).to(out_dev)
+
+
+def sample_neighborhood(g, n_items, nodeset, n_hops, alpha):
+    """Dense normalised visit counts, self column zeroed: f64 [n, N_all]
+    (pinsage_model.py:88-101)."""
+    src, trace = _walk_device(g, nodeset, n_hops, alpha)
+    n, n_all = int(src.shape[0]), g.number_of_nodes()
+    dense = torch.empty((n, n_all), dtype=torch.float64, device=src.device)
+    nat.check(nat.lib().pinsage_visit_dense(nat.ptr(trace), nat.ptr(src), n, int(n_hops), n_all,
+                                            nat.ptr(dense), nat.stream_ptr()), "visit_dense")
+    return dense.to(torch.as_tensor(nodeset).device)
+
+
+def _topk_device(src, trace, n_all, n_hops, T, t_norm=0):
+    dev = src.device
+    n = int(src.shape[0])
+    L = nat.lib()
+    scratch_b = L.pinsage_visit_topk_scratch(n, n_all, T)
+    scratch = torch.empty(max(scratch_b, 1), dtype=torch.uint8, device=dev)
+    w = torch.empty((n, T), dtype=torch.float64, device=dev)
+    nb = torch.empty((n, T), dtype=torch.int64, device=dev)
+    wn = nb32 = None
+    if t_norm:
+        wn = torch.empty((n, t_norm), dtype=torch.float32, device=dev)
+        nb32 = torch.empty((n, t_norm), dtype=torch.int32, device=dev)
+    nat.check(L.pinsage_visit_topk(nat.ptr(trace), nat.ptr(src), n, int(n_hops), n_all, int(T),
+                                   nat.ptr(scratch) if scratch_b else None, nat.ptr(w), nat.ptr(nb),
+                                   nat.ptr(wn), nat.ptr(nb32), t_norm, nat.stream_ptr()), "visit_topk")
+    return w, nb, wn, nb32
+
+
+def sample_neighborhood_topt(g, n_items, nodeset, n_hops, alpha, T):
+    """visit_prob.topk(T, 1) as a ``torch.return_types.topk`` (pinsage_model.py:103-107)."""
+    src, trace = _walk_device(g, nodeset, n_hops, alpha)
+    w, nb, _, _ = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T))
+    out_dev = torch.as_tensor(nodeset).device
+    return torch.return_types.topk((w.to(out_dev), nb.to(out_dev)))
+
+
+def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
+    """Top-T PPR neighbourhoods of all items, cached at ``path`` as
+    ``(weights f64 [n,T], nodes i64 [n,T])`` (pinsage_model.py:109-132)."""
+    if path and os.path.isfile(path):
+        a, b = torch.load(path, weights_only=True)
+        if b.shape[0] == n_items and b.shape[1] == T:
+            return (a, b)
+    t0 = time.time()
+    dev = nat.device()
+    all_w = torch.empty((n_items, T), dtype=torch.float64)
+    all_nb = torch.empty((n_items, T), dtype=torch.int64)
+    # sources in order, as the reference's 256-source batches consume the stream
+    chunk = 1 << 18
+    for i in range(0, n_items, chunk):
+        ids = torch.arange(i, min(i + chunk, n_items), dtype=torch.int64, device=dev)
+        src, trace = _walk_device(g, ids, n_hops, alpha)
+        w, nb, _, _ = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T))
+        all_w[i:i + ids.shape[0]] = w.cpu()
+        all_nb[i:i + ids.shape[0]] = nb.cpu()
+        print(f"{min(i + chunk, n_items)}/{n_items} done.")
+    print(f"{time.time() - t0}s elapsed.")
+    if path:
+        torch.save((all_w, all_nb), path)
+    return (all_w, all_nb)
+
+
+def sample_hard_negatives(g, n_items, visit_prob, hn_per_query, min_rank, max_rank):
+    """(NOT USED in the reference either; pinsage_model.py:135-140)"""
+    rng = visit_prob.topk(max_rank, 1)[1][:, min_rank:]
+    sample = torch.randint(0, rng.shape[1], (hn_per_query,))
+    return rng[:, sample]
+
+
+# ----------------------------------------------------------------------------- frontier
+def _frontier_step(nodeset_dev, nb32, T, n_items):
+    L = nat.lib()
+    n = int(nodeset_dev.shape[0])
+    cap = min(n_items, n * (T + 1))
+    ws = torch.empty(L.pinsage_frontier_workspace(n_items), dtype=torch.uint8, device=nodeset_dev.device)
+    out = torch.empty(max(cap, 1), dtype=torch.int32, device=nodeset_dev.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=nodeset_dev.device)
+    nat.check(L.pinsage_frontier_step(nat.ptr(nodeset_dev), n, nat.ptr(nb32), nb32.shape[1], int(T),
+                                      n_items, nat.ptr(ws), nat.ptr(out), nat.ptr(cnt),
+                                      nat.stream_ptr()), "frontier")
+    return out[:int(cnt.item())].to(torch.int64)
+
+
+def relevant_nodes_per_layer(g, n_items, nodeset, n_layers, n_hops, alpha, T):
+    """Computation graph with on-the-fly sampling (pinsage_model.py:142-154)."""
+    out_dev = torch.as_tensor(nodeset).device
+    dev = nat.device()
+    S = []
+    cur = torch.as_tensor(nodeset).to(dev, torch.int64)
+    for _ in reversed(range(0, n_layers)):
+        src, trace = _walk_device(g, cur, n_hops, alpha)
+        w, nb, _, nb32 = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T), t_norm=int(T))
+        S.insert(0, (cur.to(out_dev), w.to(out_dev), nb.to(out_dev)))
+        # unique(cat(nb.flatten(), cur)): rows of nb belong to cur's positions
+        table = torch.zeros((g.number_of_nodes(), int(T)), dtype=torch.int32, device=dev)
+        table[cur] = nb32
+        cur = _frontier_step(cur, table, int(T), g.number_of_nodes())
+    return S
+
+
+class _DeviceTable:
+    """Device mirror of a precomputed (weights, nodes) table: first T columns,
+    nodes int32, weights f32 normalised by their f64 row sum."""
+
+    def __init__(self, nbhds, T, n_items, dev):
+        w, nb = nbhds
+        self.src = (w, nb)
+        self.T = int(T)
+        nb_t = torch.as_tensor(nb)[:, :T]
+        w_t = torch.as_tensor(w)[:, :T].to(torch.float64)
+        if nb_t.shape[0] < n_items:
+            raise ValueError("neighbourhood table has fewer rows than n_items")
+        if int(nb_t.min()) < 0 or int(nb_t.max()) >= n_items:
+            # the reference's h[nb] raises IndexError for these (collection ids
+            # in the zero-weight tail of a tiny graph)
+            raise IndexError("neighbourhood table references ids >= n_items")
+        self.nb32 = nb_t.to(torch.int32).contiguous().to(dev)
+        self.wn = (w_t / w_t.sum(1, keepdim=True)).to(torch.float32).contiguous().to(dev)
+
+
+def relevant_nodes_per_layer_precomp(nodeset, n_layers, T, nbhds):
+    """Per-layer (nodeset, w[:, :T], nb[:, :T]) from the precomputed table;
+    index 0 = bottom layer (pinsage_model.py:156-168)."""
+    all_w, all_nb = nbhds
+    n_items = int(all_nb.shape[0])
+    out_dev = torch.as_tensor(nodeset).device
+    dev = nat.device()
+    nb32 = torch.as_tensor(all_nb)[:, :T].to(torch.int32).contiguous().to(dev)
+    S = []
+    cur = torch.as_tensor(nodeset).to(torch.int64)
+    for _ in reversed(range(0, n_layers)):
+        cur_c = cur.to(all_w.device)
+        S.insert(0, (cur.to(out_dev), all_w[cur_c, :T].to(out_dev), all_nb[cur_c, :T].to(out_dev)))
+        cur = _frontier_step(cur.to(dev), nb32, int(T), n_items)
+    return S
+
+
+# ----------------------------------------------------------------------------- modules
+class ConvLayer(nn.Module):
+    """A single PinSage convolution (pinsage_model.py:171-212).  Parameters and
+    their initialisation (xavier_uniform_, bias 0.3) match the reference."""
+
+    def __init__(self, in_dim, out_dim, hidden_dim):
+        super().__init__()
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.hidden_dim = hidden_dim
+        self.Q = nn.Linear(in_dim, hidden_dim)
+        torch.nn.init.xavier_uniform_(self.Q.weight)
+        self.Q.bias.data.fill_(0.3)
+        self.W = nn.Linear(in_dim + hidden_dim, out_dim)
+        torch.nn.init.xavier_uniform_(self.W.weight)
+        self.W.bias.data.fill_(0.3)
+
+    def forward(self, h, nodeset, nb_nodes, nb_weights):
+        """Standalone call (inside PinSageModel the fused engine runs all layers).
+        Runs a one-layer engine over a table made of the given neighbourhood
+        rows and returns the layer output rows in nodeset order."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("standalone ConvLayer backward: call it under torch.no_grad() "
+                                      "or train through PinSageModel")
+        return _conv_layer_forward(self, h, nodeset, nb_nodes, nb_weights)
+
+
+def _conv_layer_forward(layer, h, nodeset, nb_nodes, nb_weights):
+    dev = nat.device()
+    ns = torch.as_tensor(nodeset).reshape(-1).to(torch.int64)
+    n_items = int(h.shape[0])
+    T = int(nb_nodes.shape[1])
+    # a table indexed by node id holding this call's rows
+    nb_tab = torch.zeros((n_items, T), dtype=torch.int64)
+    w_tab = torch.ones((n_items, T), dtype=torch.float64)
+    nb_tab[ns.cpu()] = torch.as_tensor(nb_nodes).cpu().to(torch.int64)
+    w_tab[ns.cpu()] = torch.as_tensor(nb_weights).cpu().to(torch.float64)
+    table = _DeviceTable((w_tab, nb_tab), T, n_items, dev)
+    d, hd, o = layer.in_dim, layer.hidden_dim, layer.out_dim
+    eng = _Engine(n_items, d, hd, o, 1, T, max(int(ns.shape[0]), 1))
+    head = torch.zeros(o * o * 2 + o, device=dev)
+    flat = torch.cat([layer.Q.weight.detach().reshape(-1).to(dev), layer.Q.bias.detach().to(dev),
+                      layer.W.weight.detach().reshape(-1).to(dev), layer.W.bias.detach().to(dev),
+                      head]).float().contiguous()
+    feats = h.detach().to(dev, torch.float32).contiguous()
+    nat.check(nat.lib().pinsage_engine_set_tensors(eng.h, nat.ptr(feats), feats.stride(0),
+                                                   nat.ptr(table.nb32), nat.ptr(table.wn), T,
+                                                   nat.ptr(flat), None, None, None), "set_tensors")
+    ws = eng.new_workspace(dev)
+    ids = ns.to(dev)
+    nat.check(nat.lib().pinsage_engine_forward(eng.h, nat.ptr(ws), nat.ptr(ids), ids.shape[0],
+                                               nat.stream_ptr()), "forward")
+    cap = int(eng.off.cap_S[0])
+    y = eng.view(ws, int(eng.off.y[0]), torch.float32, cap * o).view(cap, o)
+    pr = eng.view(ws, int(eng.off.pos_rank), torch.int32, ids.shape[0]).long()
+    return y[pr].to(h.device)
+
+
+class PinSageModel(nn.Module):
+    """PinSage model (pinsage_model.py:215-265): ``n_layers`` ConvLayers and the
+    head G2(lrelu(G1 x)).  Same parameter names, init order and state_dict keys
+    as the reference; forward runs the fused HIP engine."""
+
+    def __init__(self, g, n_items, n_layers, dimensions, n_hops, alpha, T, nbhds):
+        super().__init__()
+        self.g = g
+        self.n_items = n_items
+        self.T = T
+        self.n_hops = n_hops
+        self.alpha = alpha
+        self.nbhds = nbhds
+        self.n_layers = n_layers
+        self.in_dim = dimensions[0]
+        self.hidden_dim = dimensions[1]
+        self.out_dim = dimensions[2]
+        self.in_dim_per_layer = [self.in_dim] + [self.out_dim for _ in range(n_layers - 1)]
+        self.conv_layers = nn.ModuleList()
+        for i in range(0, self.n_layers):
+            self.conv_layers.append(ConvLayer(self.in_dim_per_layer[i], self.out_dim, self.hidden_dim))
+        self.G1 = nn.Linear(self.out_dim, self.out_dim)
+        torch.nn.init.xavier_uniform_(self.G1.weight)
+        self.G1.bias.data.fill_(0.3)
+        self.G2 = nn.Linear(self.out_dim, self.out_dim, bias=False)
+        torch.nn.init.xavier_uniform_(self.G2.weight)
+        self._runner = None
+        if torch.cuda.is_available():
+            self.to(nat.device())
+
+    def runner(self):
+        if self._runner is None:
+            self._runner = _EngineRunner(self)
+        return self._runner
+
+    def forward(self, initial_h, nodeset):
+        return self.runner()(initial_h, nodeset, self.nbhds)
+
+
+# ----------------------------------------------------------------------------- engine glue
+def _param_order(module_like_n_layers):
+    names = []
+    for i in range(module_like_n_layers):
+        names += [f"conv_layers.{i}.Q.weight", f"conv_layers.{i}.Q.bias",
+                  f"conv_layers.{i}.W.weight", f"conv_layers.{i}.W.bias"]
+    return names + ["G1.weight", "G1.bias", "G2.weight"]
+
+
+class _Engine:
+    """Owns a native engine handle for one configuration."""
+
+    def __init__(self, n_items, d_in, hid, out, n_layers, T, max_pos):
+        self.cfg = nat.EngineConfig(n_items, d_in, hid, out, n_layers, T, max_pos)
+        h = ctypes.c_void_p()
+        nat.check(nat.lib().pinsage_engine_create(ctypes.byref(self.cfg), ctypes.byref(h)),
+                  "engine_create")
+        self.h = h
+        self.ws_bytes = nat.lib().pinsage_engine_workspace_bytes(h)
+        self.n_params = nat.lib().pinsage_engine_num_params(h)
+        self.off = nat.EngineOffsets()
+        nat.lib().pinsage_engine_offsets(h, ctypes.byref(self.off))
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                nat.lib().pinsage_engine_destroy(self.h)
+        except Exception:
+            pass
+
+    def new_workspace(self, dev):
+        return torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+
+    def view(self, ws, off, dtype, n):
+        nbytes = n * torch.empty((), dtype=dtype).element_size()
+        return ws[off:off + nbytes].view(dtype)
+
+
+class _EngineRunner:
+    """Binds a PinSageModel's parameters (packed into one flat fp32 buffer in
+    state_dict order), its features and its neighbourhood table to an engine."""
+
+    def __init__(self, model):
+        self.model = model
+        self.dev = nat.device()
+        self.engine = None
+        self.flat = None
+        self.grad_flat = None
+        self._feat_key = None
+        self._feat = None
+        self._table_key = None
+        self._table = None
+        self._ws = None
+
+    # -- parameters
+    def names(self):
+        return _param_order(self.model.n_layers)
+
+    def params(self):
+        sd = dict(self.model.named_parameters())
+        return [sd[n] for n in self.names()]
+
+    def pack(self):
+        """(Re)pack parameters into the flat device buffer if they are not
+        already views of it (e.g. after .to() or assignment)."""
+        ps = self.params()
+        if self.flat is not None:
+            ok = True
+            off = 0
+            base = self.flat.data_ptr()
+            for p in ps:
+                if p.data.data_ptr() != base + 4 * off or p.device != self.flat.device:
+                    ok = False
+                    break
+                off += p.numel()
+            if ok:
+                return
+        flat = torch.cat([p.detach().reshape(-1).to(self.dev, torch.float32) for p in ps])
+        off = 0
+        for p in ps:
+            n = p.numel()
+            p.data = flat[off:off + n].view(p.shape)
+            off += n
+        self.flat = flat
+
+    # -- inputs
+    def features(self, h):
+        key = (id(h), h.data_ptr(), getattr(h, "_version", 0), tuple(h.shape))
+        if key != self._feat_key:
+            f = h.detach()
+            if f.device != self.dev or f.dtype != torch.float32 or not f.is_contiguous():
+                f = f.to(self.dev, torch.float32).contiguous()
+            self._feat = f
+            self._feat_key = key
+        return self._feat
+
+    def table(self, nbhds):
+        m = self.model
+        key = (id(nbhds[0]), id(nbhds[1]), int(m.T))
+        if key != self._table_key:
+            self._table = _DeviceTable(nbhds, m.T, m.n_items, self.dev)
+            self._table_key = key
+        return self._table
+
+    def ensure_engine(self, n_pos):
+        m = self.model
+        need = max(n_pos, 1)
+        if self.engine is None or self.engine.cfg.max_pos < need:
+            cap = max(need, self.engine.cfg.max_pos * 2 if self.engine else need)
+            self.engine = _Engine(m.n_items, m.in_dim, m.hidden_dim, m.out_dim, m.n_layers, m.T, cap)
+            self._ws = None
+        return self.engine
+
+    def bind(self, feats, table, grads=None, adam_m=None, adam_v=None):
+        e = self.engine
+        nat.check(nat.lib().pinsage_engine_set_tensors(
+            e.h, nat.ptr(feats), feats.stride(0), nat.ptr(table.nb32), nat.ptr(table.wn),
+            table.nb32.shape[1], nat.ptr(self.flat), nat.ptr(grads), nat.ptr(adam_m),
+            nat.ptr(adam_v)), "engine_set_tensors")
+
+    def run_forward(self, ws, ids_dev):
+        e = self.engine
+        nat.check(nat.lib().pinsage_engine_forward(e.h, nat.ptr(ws), nat.ptr(ids_dev),
+                                                   ids_dev.shape[0], nat.stream_ptr()), "forward")
+
+    def __call__(self, initial_h, nodeset, nbhds):
+        m = self.model
+        out_dev = initial_h.device
+        feats = self.features(initial_h)
+        if feats.shape[1] < m.in_dim:
+            raise ValueError("features narrower than in_dim")
+        if m.out_dim > feats.shape[1]:
+            raise RuntimeError("zeros: Dimension size must be non-negative (out_dim > feature dim, "
+                               "as the reference's put_embeddings)")
+        table = self.table(nbhds)
+        ids = torch.as_tensor(nodeset).reshape(-1).to(self.dev, torch.int64)
+        n = int(ids.shape[0])
+        if n == 0:
+            return torch.empty((0, m.out_dim), device=out_dev)
+        self.pack()
+        self.ensure_engine(n)
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.params())
+        if need_grad:
+            out = _EngineFn.apply(self, feats, table, ids, *self.params())
+        else:
+            if self._ws is None:
+                self._ws = self.engine.new_workspace(self.dev)
+            self.bind(feats, table)
+            self.run_forward(self._ws, ids)
+            out = torch.empty((n, m.out_dim), dtype=torch.float32, device=self.dev)
+            nat.check(nat.lib().pinsage_engine_gather_output(self.engine.h, nat.ptr(self._ws), n,
+                                                             nat.ptr(out), nat.stream_ptr()), "gather")
+        return out.to(out_dev)
+
+
+class _EngineFn(torch.autograd.Function):
+    """Forward + HIP backward of PinSageModel for autograd callers."""
+
+    @staticmethod
+    def forward(ctx, runner, feats, table, ids, *params):
+        e = runner.engine
+        ws = e.new_workspace(runner.dev)
+        runner.bind(feats, table)
+        runner.run_forward(ws, ids)
+        n = int(ids.shape[0])
+        out = torch.empty((n, runner.model.out_dim), dtype=torch.float32, device=runner.dev)
+        nat.check(nat.lib().pinsage_engine_gather_output(e.h, nat.ptr(ws), n, nat.ptr(out),
+                                                         nat.stream_ptr()), "gather")
+        ctx.runner, ctx.ws, ctx.feats, ctx.table, ctx.n = runner, ws, feats, table, n
+        ctx.engine = e
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        runner, e, ws = ctx.runner, ctx.engine, ctx.ws
+        grads = torch.zeros(e.n_params, dtype=torch.float32, device=runner.dev)
+        runner.bind(ctx.feats, ctx.table, grads=grads)
+        dout = dout.contiguous().to(torch.float32)
+        nat.check(nat.lib().pinsage_engine_set_output_grad(e.h, nat.ptr(ws), nat.ptr(dout), ctx.n,
+                                                           nat.stream_ptr()), "set_output_grad")
+        nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(ws), nat.stream_ptr()), "backward")
+        out = []
+        off = 0
+        for p in runner.params():
+            k = p.numel()
+            out.append(grads[off:off + k].view(p.shape))
+            off += k
+        return (None, None, None, None, *out)

@@ -1,0 +1,405 @@
+"""Drop-in ``pinsage_training`` (reference ``pinsage_training.py:31-339``) on MI355X.
+
+``PinSage.train_batch`` runs ONE fused device step: frontier of the union of
+the query/positive/negative ids, fp32-MFMA convolutions, head, max-margin loss
+with the reference's gradient semantics, HIP backward and a fused Adam update
+on a flat parameter buffer -- no host synchronisation inside the step.  Batch
+sampling reproduces the reference's torch RNG consumption exactly (native
+Fisher-Yates prefix), so a seeded run draws the same batches.
+
+Data parallel: when ``torch.distributed`` is initialised, every rank draws the
+same global batch (world * batch_size triples, shared seed) and trains on its
+slice; gradients are averaged with one RCCL all-reduce of the flat buffer.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import _native as nat
+import pinsage_model as psm
+
+BASE_RUN_DIR = "./runs"
+
+TEST_TRACK_INFO = None
+TEST_IDS = None
+
+
+def max_margin_loss(h_q, h_pos, h_neg, margin):
+    """Hinge on normalised dot products, batch mean (pinsage_training.py:31-41).
+    Device tensors go through torch ops (small); the train step uses the fused kernel."""
+    norm = torch.nn.functional.normalize
+    h_q, h_pos, h_neg = norm(h_q, dim=1), norm(h_pos, dim=1), norm(h_neg, dim=1)
+    dot = (h_q * h_neg).sum(1) - (h_q * h_pos).sum(1) + margin
+    return torch.clamp(dot, min=0.0).mean()
+
+
+def cosine_dissimilarity(a, b):
+    return 1 - F.cosine_similarity(a, b)
+
+
+TRIPLET_LOSS = torch.nn.TripletMarginLoss(0.0001, reduction="mean")
+COSINE_TRIPLET_LOSS = torch.nn.TripletMarginWithDistanceLoss(distance_function=cosine_dissimilarity,
+                                                             margin=0.0001, reduction="mean")
+
+
+# ----------------------------------------------------------------------------- batches
+def sample_positives_with_rep(positives, batch_size):
+    """positives[randperm(P)[:batch_size]] (pinsage_training.py:53-62)."""
+    P = positives.shape[0]
+    with nat.torch_rng() as mt:
+        sel = mt.randperm_prefix(P, batch_size)
+    return positives[torch.from_numpy(sel), :].to(torch.int64)
+
+
+def sample_easy_negatives(all_ids, pos_batch):
+    """One random non-batch id per pair (pinsage_training.py:64-77)."""
+    n = all_ids.shape[0]
+    members = pos_batch.flatten().unique()
+    mask = torch.ones((n,)).bool()
+    mask[members] = False
+    possible_neg = all_ids[mask].to(torch.int64)
+    with nat.torch_rng() as mt:
+        sel = mt.randperm_prefix(possible_neg.shape[0], pos_batch.shape[0])
+    negatives = possible_neg[torch.from_numpy(sel)]
+    batch = torch.cat((pos_batch, negatives.unsqueeze(1)), dim=1)
+    return batch, batch.flatten().unique().to(torch.int64)
+
+
+def sample_hard_negatives(all_ids, pos_batch, nbhds, min_rank, max_rank):
+    """pinsage_training.py:79-87, including its row-gather behaviour (the
+    reference gathers rows 0..B-1 of the table, not the query rows)."""
+    queries = pos_batch[:, 0]
+    rnd_ranks = torch.randint(min_rank, max_rank, (queries.shape[0],))
+    hard_neg = torch.gather(nbhds[1], 1, rnd_ranks.view(-1, 1)).squeeze()
+    batch = torch.cat((pos_batch, hard_neg.unsqueeze(1)), dim=1)
+    return batch, batch.flatten().unique().to(torch.int64)
+
+
+def sample_batch(all_ids, positives, batch_size, nbhds, hard_negatives=True, hn_min=10, hn_max=100):
+    """pinsage_training.py:89-97.  The easy-negative path runs natively
+    (same draws as the reference, without materialising randperm(P))."""
+    if hard_negatives:
+        pos_batch = sample_positives_with_rep(positives, batch_size)
+        return sample_hard_negatives(all_ids, pos_batch, nbhds, hn_min, hn_max)
+    pos = positives.to(torch.int64).contiguous()
+    n_items = int(all_ids.shape[0])
+    B = min(int(batch_size), int(pos.shape[0]))
+    out = np.empty((B, 3), np.int64)
+    pos_np = pos.numpy() if pos.device.type == "cpu" else pos.cpu().numpy()
+    if not _all_ids_is_range(all_ids):
+        batch, nodeset = sample_easy_negatives(all_ids, sample_positives_with_rep(positives, batch_size))
+        return batch, nodeset
+    with nat.torch_rng() as mt:
+        nat.check(nat.lib().pinsage_sample_batch_easy(
+            mt.p, pos_np.ctypes.data_as(nat.vp), pos_np.shape[0], n_items, int(batch_size),
+            out.ctypes.data_as(nat.vp)), "sample_batch")
+    batch = torch.from_numpy(out)
+    return batch, batch.flatten().unique()
+
+
+def _all_ids_is_range(all_ids):
+    n = int(all_ids.shape[0])
+    return torch.equal(all_ids.cpu().to(torch.int64), torch.arange(n, dtype=torch.int64))
+
+
+def batch_variance(h):
+    """Monitor of collapse to a constant (pinsage_training.py:99-103)."""
+    mean = torch.mean(h, dim=0)
+    var = torch.sum(torch.pow(h - mean, 2)) / (h.shape[0] - 1)
+    return torch.prod(var)
+
+
+# ----------------------------------------------------------------------------- trainer
+class _FusedStep:
+    """Device state of the fused train step: flat param/grad/Adam buffers,
+    engine workspace, batch staging and scalar outputs."""
+
+    def __init__(self, trainer):
+        self.tr = trainer
+        model = trainer.model
+        self.runner = model.runner()
+        self.dev = self.runner.dev
+        self.B = 0
+        self.ws = None
+        self.m = self.v = None
+        self.grads = None
+        self.lr_dev = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._lr_host = None
+        self.host_batch = None
+        self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+
+    def ensure(self, B):
+        r = self.runner
+        r.pack()
+        n_params = r.flat.numel()
+        if self.grads is None or self.grads.numel() != n_params:
+            self.grads = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
+            self.m = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
+            self.v = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
+            self.adopt_optimizer_state()
+        if self.ws is None or r.engine is None or r.engine.cfg.max_pos < 3 * B:
+            r.ensure_engine(3 * B)
+            self.ws = r.engine.new_workspace(self.dev)
+            self.B = B
+            off = r.engine.off
+            self.ids_view = r.engine.view(self.ws, int(off.ids), torch.int64, r.engine.cfg.max_pos)
+            self.scal = r.engine.view(self.ws, int(off.scalars), torch.float32, 4)
+            self.host_batch = torch.empty(3 * r.engine.cfg.max_pos, dtype=torch.int64).pin_memory()
+
+    def adopt_optimizer_state(self):
+        """Use the optimizer's Adam state (if any, e.g. after load_state_dict) as
+        the initial flat m/v, then make the optimizer state views of them."""
+        opt = self.tr.optimizer
+        off = 0
+        step = 0
+        for p in self.runner.params():
+            k = p.numel()
+            st = opt.state.get(p)
+            if st and "exp_avg" in st:
+                self.m[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                self.v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                step = int(float(st["step"]))
+            opt.state[p] = {"step": torch.tensor(float(step)),
+                            "exp_avg": self.m[off:off + k].view(p.shape),
+                            "exp_avg_sq": self.v[off:off + k].view(p.shape)}
+            p.grad = self.grads[off:off + k].view(p.shape)
+            off += k
+        self.step_dev.fill_(step)
+        self.host_step = step
+
+    def sync_optimizer_step(self):
+        for p in self.runner.params():
+            st = self.tr.optimizer.state.get(p)
+            if st is not None:
+                st["step"] = torch.tensor(float(self.host_step))
+
+    def __call__(self, batch):
+        tr = self.tr
+        batch = torch.as_tensor(batch)
+        B = int(batch.shape[0])
+        self.ensure(B)
+        r = self.runner
+        feats = r.features(tr.features)
+        table = r.table(tr.nbhds)
+        r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)
+        # stage the [B, 3] batch into the engine's id buffer
+        hb = self.host_batch[:3 * B]
+        hb.copy_(batch.reshape(-1).to(torch.int64))
+        self.ids_view[:3 * B].copy_(hb, non_blocking=True)
+        e = r.engine
+        st = nat.stream_ptr()
+        L = nat.lib()
+        nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
+                  "forward")
+        nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
+        nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.ws), st), "backward")
+        if self.dist:
+            ws = torch.distributed.get_world_size()
+            torch.distributed.all_reduce(self.grads)
+            self.grads.mul_(1.0 / ws)
+        lr = float(tr.optimizer.param_groups[0]["lr"])
+        if lr != self._lr_host:
+            self.lr_dev.fill_(lr)
+            self._lr_host = lr
+        g = tr.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        nat.check(L.pinsage_engine_adam(e.h, nat.ptr(self.lr_dev), nat.ptr(self.step_dev), float(b1),
+                                        float(b2), float(g["eps"]), st), "adam")
+        self.host_step += 1
+        return self.scal[0], self.scal[1], self.scal[3]
+
+
+class PinSage:
+    """The PinSage trainer (pinsage_training.py:108-295): same attributes,
+    defaults and file formats; hyperparameters are bound at construction
+    (T, n_layers, dims, lr, decay) exactly as in the reference."""
+
+    def __init__(self, g, n_items, features, positives, log=True, load_save=True):
+        self.run_name = "pinsage_randomft_intersect"
+        self.precomp_path = g.nbhds_path
+
+        self.g = g
+        self.n = n_items
+        self.all_ids = torch.arange(0, n_items, 1, dtype=torch.int64)
+        self.features = features
+        self.positives = positives
+
+        self.n_layers = 2
+        self.in_dim = features.shape[1]
+        self.hidden_dim = 512
+        self.out_dim = 128
+        self.dimensions = (self.in_dim, self.hidden_dim, self.out_dim)
+        self.n_hops = 500
+        self.alpha = 0.85
+        self.T = 3
+        self.hard_negatives = False
+        self.hn_min = 10
+        self.hn_max = 100
+
+        self.nbhds = psm.precompute_neighborhoods_topt(self.g, self.n, self.n_hops, self.alpha,
+                                                       psm.DEF_T_PRECOMP, self.precomp_path)
+        self.model = psm.PinSageModel(self.g, self.n, self.n_layers, self.dimensions, self.n_hops,
+                                      self.alpha, self.T, self.nbhds)
+        self.lr = 1e-4
+        self.decay = 0.95
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lr)
+        self.scheduler = torch.optim.lr_scheduler.ExponentialLR(self.optimizer, self.decay)
+        self.margin = 1e-5
+        self.epochs = 30
+        self.batch_size = 128
+        self.b_per_e = 500
+
+        self.embeddings = None
+        run_dir = os.path.join(BASE_RUN_DIR, self.run_name)
+        os.makedirs(os.path.join(run_dir, "board"), exist_ok=True)
+        self.e = 0
+        self.b = 0
+
+        self.log = log
+        if self.log:
+            try:
+                import wandb
+                wandb.config = {"learning_rate": self.lr, "epochs": self.epochs,
+                                "batch_size": self.batch_size}
+                wandb.init(project='gcn-song-embeddings', name=self.run_name)
+                wandb.watch(self.model, log="all", log_freq=10, log_graph=True)
+                self._wandb = wandb
+            except Exception as ex:  # no network / not installed: keep training
+                print(f"wandb unavailable ({ex}); logging disabled")
+                self.log = False
+        self._fused = None
+        self.load_save = load_save
+        if self.load_save:
+            self.load_model()
+
+    # ---- the train step
+    def _dp(self):
+        d = torch.distributed
+        if d.is_available() and d.is_initialized():
+            return d.get_rank(), d.get_world_size()
+        return 0, 1
+
+    def next_batch(self):
+        """Sample this rank's slice of the global batch (same draws on every rank)."""
+        rank, world = self._dp()
+        batch, nodeset = sample_batch(self.all_ids, self.positives, self.batch_size * world, self.nbhds,
+                                      hard_negatives=self.hard_negatives, hn_min=self.hn_min,
+                                      hn_max=self.hn_max)
+        if world > 1:
+            B = batch.shape[0] // world
+            batch = batch[rank * B:(rank + 1) * B]
+            nodeset = batch.flatten().unique()
+        return batch, nodeset
+
+    def train_batch(self, batch):
+        """Fetch and train one batch of (q, pos, neg) triples: returns
+        (loss, node_feat_loss, variance) as device scalars (no host sync)."""
+        if self._fused is None:
+            self._fused = _FusedStep(self)
+        return self._fused(batch)
+
+    def train(self):
+        from tqdm import tqdm
+        print("\033[0;33mTraining PinSage...\033[0m")
+        while self.e < self.epochs:
+            print(f"Training epoch {self.e+1}/{self.epochs}...")
+            cur_lr = self.optimizer.param_groups[0]["lr"]
+            t1 = time.time()
+            pbar = tqdm(total=self.b_per_e)
+            pbar.update(1)
+            while self.b < self.b_per_e:
+                batch, nodeset = self.next_batch()
+                loss, node_feat_loss, variance = self.train_batch(batch)
+                pbar.update(1)
+                if self.b % 50 == 0 or self.b == self.b_per_e - 1:
+                    pbar.set_description(f"Loss = {float(loss)}, bathes done")
+                if self.log:
+                    self._wandb.log({'Train Loss': float(loss), 'Node Features Loss': float(node_feat_loss),
+                                     'Batch Variance': float(variance), 'Learning Rate': cur_lr})
+                if self.load_save:
+                    self.save_model()
+                self.b += 1
+            print(f"{time.time() - t1}s elapsed.")
+            pbar.close()
+            self.b = 0
+            self.e += 1
+            self.scheduler.step()
+
+    def embed(self, ids=None, bsize=None):
+        """Node embeddings, optionally in bsize batches (pinsage_training.py:258-275,
+        including its reset of ``ids`` to a range in the batched branch)."""
+        if ids is None:
+            ids = self.all_ids
+        self.model.eval()
+        n = len(ids)
+        with torch.no_grad():
+            if not bsize:
+                self.embeddings = self.model(self.features, ids)
+            else:
+                self.embeddings = torch.zeros((n, self.out_dim))
+                for i in range(0, n, bsize):
+                    ids = torch.arange(i, min(i + bsize, n))
+                    self.embeddings[ids, :] = self.model(self.features, ids).to(self.embeddings.device)
+        return self.embeddings
+
+    def _sync_state(self):
+        if self._fused is not None:
+            self._fused.sync_optimizer_step()
+
+    def load_model(self):
+        load_path = os.path.join(BASE_RUN_DIR, self.run_name, "state.pt")
+        if os.path.isfile(load_path):
+            prog = torch.load(load_path, map_location="cpu", weights_only=True)
+            self.e = prog["epochs_done"]
+            self.b = prog["batches_done"]
+            self.model.load_state_dict(prog["model_state"])
+            self.optimizer.load_state_dict(prog["optimizer_state"])
+            if self._fused is not None and self._fused.grads is not None:
+                self._fused.adopt_optimizer_state()
+            print(f"Loaded existing model from {load_path}.")
+
+    def save_model(self):
+        self._sync_state()
+        opt_sd = self.optimizer.state_dict()
+        opt_sd = {"state": {k: {kk: (vv.detach().cpu().clone() if torch.is_tensor(vv) else vv)
+                                for kk, vv in v.items()} for k, v in opt_sd["state"].items()},
+                  "param_groups": opt_sd["param_groups"]}
+        prog = {
+            "epochs_done": self.e,
+            "batches_done": self.b,
+            "model_state": {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()},
+            "optimizer_state": opt_sd,
+        }
+        torch.save(prog, os.path.join(BASE_RUN_DIR, self.run_name, "state.pt"))
+
+
+def save_embeddings(trainer, dataset, base_run_dir=BASE_RUN_DIR, override_run_name=None):
+    """One ``<track_id>.pt`` per track, skipping existing files
+    (pinsage_training.py:297-327)."""
+    track_ids = list(dataset.tracks)
+    n = len(track_ids)
+    bsize = 256
+    run_name = override_run_name if override_run_name else trainer.run_name
+    emb_dir = os.path.join(base_run_dir, run_name, "emb")
+    os.makedirs(emb_dir, exist_ok=True)
+    for i in range(0, n, bsize):
+        ids = torch.arange(i, min(i + bsize, n))
+        emb = trainer.embed(ids).detach().cpu()
+        for j, tid in enumerate(ids.tolist()):
+            save_path = os.path.join(emb_dir, track_ids[tid] + ".pt")
+            if os.path.isfile(save_path):
+                continue
+            torch.save(emb[j, :].clone(), save_path)
+
+
+def load_embeddings(trainer, dataset, base_run_dir=BASE_RUN_DIR):
+    emb_dir = os.path.join(base_run_dir, trainer.run_name, "emb")
+    return torch.stack([torch.load(os.path.join(emb_dir, t + ".pt"), weights_only=True)
+                        for t in dataset.tracks], dim=0)

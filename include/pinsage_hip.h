@@ -1,0 +1,184 @@
+/*
+ * pinsage_hip.h -- C-ABI of the MI355X (gfx950) PinSage convolution engine.
+ *
+ * The reference (MatejBevec/gcn-song-embeddings) is pure Python; its train-step
+ * path calls into DGL (g.successors) and ATen CPU ops.  These entry points are
+ * what a maintainer binds (ctypes stub in INTEGRATION.md) to replace those
+ * call sites.  Plain pointers and sizes only; every device pointer is HIP
+ * device memory (e.g. a torch tensor's data_ptr()), every `stream` a
+ * hipStream_t.  Functions return 0 on success or a negative pinsage_status;
+ * pinsage_last_error() gives the message of the calling thread's last failure.
+ * No call synchronises the stream unless its comment says so.
+ */
+#ifndef PINSAGE_HIP_H
+#define PINSAGE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum pinsage_status {
+  PINSAGE_OK = 0,
+  PINSAGE_ERR_HIP = -1,
+  PINSAGE_ERR_ARG = -2,
+  PINSAGE_ERR_WORKSPACE = -3,
+  PINSAGE_ERR_GRAPH = -4, /* zero-degree node met by a walk (reference: torch.randint(0) raises) */
+  PINSAGE_ERR_INDEX = -5, /* id out of range (reference: IndexError in h[nodeset]) */
+};
+
+/* ------------------------------------------------------------------ library */
+int pinsage_version(void);
+const char* pinsage_last_error(void);
+/* number of visible HIP devices (0 when none); never fails */
+int pinsage_device_count(void);
+
+/* ------------------------------------------------------------------ RNG (host, no GPU needed)
+ * Opaque MT19937 state with torch's CPU-generator semantics.  Replaces the
+ * global generator the reference draws from in pinsage_model.py:42,45,50 and
+ * pinsage_training.py:58,74 (torch.randint / torch.rand / torch.randperm).
+ * torch_state is torch.get_rng_state() (5056 bytes). */
+int pinsage_mt_state_bytes(void);
+int pinsage_mt_from_torch(void* mt, const uint8_t* torch_state, int64_t nbytes);
+int pinsage_mt_to_torch(const void* mt, uint8_t* torch_state, int64_t nbytes);
+int pinsage_mt_seed(void* mt, uint64_t seed);
+int pinsage_mt_skip(void* mt, int64_t n_draws);
+int pinsage_mt_draws(void* mt, uint32_t* out, int64_t n);
+/* torch.randperm(n)[:k] (pinsage_training.py:58,74): writes the first k entries
+ * of the Fisher-Yates permutation and advances mt by the full n-1 draws. */
+int pinsage_mt_randperm_prefix(void* mt, int64_t n, int64_t k, int64_t* out);
+
+/* sample_batch with easy negatives (pinsage_training.py:53-77, 89-97) on the
+ * host: positives is [P][2] int64, batch_out is [B][3] int64 (query, positive,
+ * negative).  Consumes exactly the draws the reference does. */
+int pinsage_sample_batch_easy(void* mt, const int64_t* positives, int64_t n_pos_pairs,
+                              int64_t n_items, int64_t batch_size, int64_t* batch_out);
+
+/* ------------------------------------------------------------------ sampler (device)
+ * do_random_walks (pinsage_model.py:32-53).  CSR: indptr int64 [n_all+1],
+ * indices int32 [E], successors in edge-insertion order (DGL g.successors,
+ * pinsage_model.py:41,44).  sources int64 [n_src], trace int32 [n_src][n_hops].
+ *
+ * MT mode: `mt` (host state) is advanced by exactly 3*n_hops*n_src draws, as
+ * the reference consumes.  `ws` is device scratch of pinsage_walk_mt_workspace
+ * bytes (the raw MT words of one round of sources; smaller workspaces run in
+ * more rounds).  Synchronises the stream (host prepares each round's chunk
+ * states while the previous round runs). */
+int64_t pinsage_walk_mt_workspace(int64_t n_src, int64_t n_hops);
+int pinsage_walk_mt(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                    const int64_t* sources, int64_t n_src, int64_t n_hops, float alpha, void* mt,
+                    void* ws, int64_t ws_bytes, int32_t* trace, void* stream);
+/* Philox mode: draws for (source position src_base+i, hop j) = Philox4x32-10
+ * (key=seed, counter={j, pos_lo, pos_hi, offset}).  Synchronises the stream to
+ * check for zero-degree nodes. */
+int pinsage_walk_philox(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                        const int64_t* sources, int64_t n_src, int64_t n_hops, float alpha,
+                        uint64_t seed, uint32_t offset, int64_t src_base, int32_t* trace,
+                        void* stream);
+
+/* visit_prob.topk(k, 1) on the walks (pinsage_model.py:96-107): counts visits
+ * per source, zeroes the source's own column, selects the top k with the exact
+ * libstdc++ tie order of torch's CPU topk.  Outputs (any may be null):
+ *   w_out f64 [n_src][k] = count / n_hops, nb_out int64 [n_src][k]   (reference dtypes)
+ *   wn_out f32 [n_src][t_norm], nb32_out int32 [n_src][t_norm]: the first
+ *     t_norm columns with weights divided by their row sum (device table)
+ * dense_scratch: device bytes >= pinsage_visit_topk_scratch(n_src, n_all, k). */
+int64_t pinsage_visit_topk_scratch(int64_t n_src, int64_t n_all, int64_t k);
+int pinsage_visit_topk(const int32_t* trace, const int64_t* sources, int64_t n_src,
+                       int64_t n_hops, int64_t n_all, int64_t k, void* dense_scratch,
+                       double* w_out, int64_t* nb_out, float* wn_out, int32_t* nb32_out,
+                       int64_t t_norm, void* stream);
+/* sample_neighborhood (pinsage_model.py:88-101): dense f64 [n_src][n_all]. */
+int pinsage_visit_dense(const int32_t* trace, const int64_t* sources, int64_t n_src,
+                        int64_t n_hops, int64_t n_all, double* dense, void* stream);
+
+/* ------------------------------------------------------------------ frontier (device)
+ * relevant_nodes_per_layer_precomp (pinsage_model.py:156-168) for the API:
+ * one step nodes_out = unique(cat(nb[nodeset, :T].flatten(), nodeset)), sorted.
+ * nb_table int32 [n_items][ld]; nodes_out int32 capacity >= n*(T+1) (and
+ * <= n_items); *count_out (device int) receives the size.  ws: device bytes >=
+ * pinsage_frontier_workspace(n_items). */
+int64_t pinsage_frontier_workspace(int64_t n_items);
+int pinsage_frontier_step(const int64_t* nodeset, int64_t n, const int32_t* nb_table, int64_t ld,
+                          int64_t T, int64_t n_items, void* ws, int32_t* nodes_out,
+                          int32_t* count_out, void* stream);
+
+/* ------------------------------------------------------------------ kernels exposed for tests
+ * fp32 MFMA GEMM: C[M][N] = A[M][K] * W[N][K]^T (+bias) (leaky_relu if act),
+ * A rows gathered by a_idx (nullable) -- nn.Linear on gathered rows
+ * (pinsage_model.py:196,201). */
+int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
+                   const float* W, const float* bias, int64_t N, int act, float* C, int64_t ldc,
+                   void* stream);
+/* agg[f] = sum_t w[f][t] * q[loc[f][t]]  (weights already normalised;
+ * pinsage_model.py:202). */
+int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
+                         int64_t n_rows, int64_t T, float* agg, void* stream);
+
+/* ------------------------------------------------------------------ train-step engine
+ * PinSageModel.forward / PinSage.train_batch (pinsage_model.py:246-265,
+ * pinsage_training.py:181-214) with device-resident sizes.  Parameters live in
+ * one flat fp32 buffer in state_dict order: conv_layers.{i}.Q.weight, Q.bias,
+ * W.weight, W.bias (i = 0..n_layers-1), G1.weight, G1.bias, G2.weight; the
+ * gradient and Adam buffers use the same layout. */
+typedef struct pinsage_engine pinsage_engine;
+typedef struct {
+  int64_t n_items;  /* feature-table rows (tracks) */
+  int64_t d_in;     /* feature dim (dimensions[0]) */
+  int64_t hid;      /* hidden_dim (dimensions[1]) */
+  int64_t out;      /* out_dim (dimensions[2], <= 128) */
+  int64_t n_layers;
+  int64_t T;        /* neighbourhood size used by the model */
+  int64_t max_pos;  /* max ids per forward (3 * batch_size for a train step) */
+} pinsage_engine_config;
+typedef struct {
+  int64_t ids, pos_rank, z, dz, scalars, err, n_layers;
+  int64_t count_S[8], count_N[8], members_S[8], members_N[8], cap_S[8], cap_N[8], y[8];
+  int64_t param_offsets[8];
+} pinsage_engine_offsets_t;
+
+int pinsage_engine_create(const pinsage_engine_config* cfg, pinsage_engine** out);
+void pinsage_engine_destroy(pinsage_engine* e);
+int64_t pinsage_engine_workspace_bytes(const pinsage_engine* e);
+int64_t pinsage_engine_num_params(const pinsage_engine* e);
+/* byte offsets of engine outputs inside a workspace (ids int64, pos_rank int32,
+ * z/dz f32 [rows][out], scalars f32 {loss, node_feat_loss, sum|h_q|^2, variance}). */
+int pinsage_engine_offsets(const pinsage_engine* e, pinsage_engine_offsets_t* out);
+/* features f32 [n_items][ld_feats]; tables: nb int32 / normalised weights f32
+ * [n_items][ld_table] (first T columns used); grads / adam buffers may be null
+ * for inference. */
+int pinsage_engine_set_tensors(pinsage_engine* e, const float* feats, int64_t ld_feats,
+                               const int32_t* nb_table, const float* w_table, int64_t ld_table,
+                               float* params, float* grads, float* adam_m, float* adam_v);
+/* forward of all ids (a train step passes the [B][3] batch flattened) */
+int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
+                           void* stream);
+int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
+                                 void* stream);
+/* max_margin_loss + monitors on the last forward of a [B][3] batch; writes dZ */
+int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float margin,
+                        int with_monitors, void* stream);
+/* dZ from an upstream gradient of gather_output (single call, autograd path) */
+int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,
+                                   void* stream);
+/* all parameter gradients from dZ into the grad buffer (overwritten) */
+int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
+/* torch.optim.Adam step over the flat buffers; lr_dev f32 and step_dev int32
+ * live in device memory (step is incremented first) so the step can be
+ * graph-replayed. */
+int pinsage_engine_adam(pinsage_engine* e, const float* lr_dev, int32_t* step_dev, float beta1,
+                        float beta2, float eps, void* stream);
+
+/* Per-launch-site HIP-event timing on the launch stream (bench/profiling):
+ * enable (also clears), collect after the work (synchronises the events), then
+ * read site idx = 0.. until PINSAGE_ERR_ARG: name, total ms, number of calls. */
+int pinsage_engine_timing(pinsage_engine* e, int enable);
+int pinsage_engine_timing_collect(pinsage_engine* e);
+int pinsage_engine_timing_get(const pinsage_engine* e, int idx, char* name, int64_t name_len,
+                              double* ms, int64_t* calls);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PINSAGE_HIP_H */
