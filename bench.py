@@ -202,7 +202,9 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = 3 * cfg["batch"] * world * args.steps / elapsed
 
-        # per-kernel timing pass (HIP events on the launch stream), separate from the timed loop
+        # per-kernel timing pass (HIP events on the launch stream), separate from the timed
+        # loop; runs the same kernels eagerly (events are not recorded inside the graph)
+        tr._fused.use_graph = False
         eng = tr.model.runner().engine
         nat.lib().pinsage_engine_timing(eng.h, 1)
         n_t = max(5, min(20, args.steps))

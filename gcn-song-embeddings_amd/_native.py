@@ -73,6 +73,8 @@ _SIGS = {
     "pinsage_engine_set_output_grad": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_backward": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_adam": (ctypes.c_int, [vp, vp, vp, f32, f32, f32, vp]),
+    "pinsage_engine_read_counts": (ctypes.c_int, [vp, vp, vp, vp, vp]),
+    "pinsage_engine_set_hints": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_timing": (ctypes.c_int, [vp, ctypes.c_int]),
     "pinsage_engine_timing_collect": (ctypes.c_int, [vp]),
     "pinsage_engine_timing_get": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_char_p, i64,

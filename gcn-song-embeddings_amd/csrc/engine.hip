@@ -69,6 +69,7 @@ struct EngineConfig {
 
 struct SetBuf {
   int64_t cap = 0;
+  int64_t hint = 0;  // expected size (from a previous step), picks GEMM tile configs
   size_t bits = 0, prefix = 0, members = 0, count = 0;
 };
 
@@ -310,6 +311,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
     // Q projection of the distinct neighbours: lrelu(h[u] Q^T + b)
     GemmParams q;
     q.M_dev = cnt(lb.N);
+    q.M_hint = (int)lb.N.hint;
     q.M_max = (int)lb.N.cap;
     q.N = (int)c.hid;
     q.K = (int)lb.d;
@@ -333,6 +335,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
     // W projection of [h_self || agg] with bias, lrelu and row L2 norm fused
     GemmParams w;
     w.M_dev = cnt(lb.S);
+    w.M_hint = (int)lb.S.hint;
     w.M_max = (int)lb.S.cap;
     w.N = (int)c.out;
     w.K = (int)(lb.d + c.hid);
@@ -356,6 +359,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   Timed t_head(E, "fwd.head", st);
   GemmParams g1;
   g1.M_dev = cnt(top.S);
+  g1.M_hint = (int)top.S.hint;
   g1.M_max = (int)top.S.cap;
   g1.N = (int)c.out;
   g1.K = (int)c.out;
@@ -427,6 +431,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
   {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
+    p.M_hint = (int)top.S.hint;
     p.M_max = (int)top.S.cap;
     p.N = o;
     p.K = o;
@@ -447,6 +452,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
   {
     GemmParams p;  // dY_top = dP1 G1
     p.M_dev = cnt(top.S);
+    p.M_hint = (int)top.S.hint;
     p.M_max = (int)top.S.cap;
     p.N = o;
     p.K = o;
@@ -480,6 +486,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       PS_CHECK_HIP(hipMemsetAsync(dYprev, 0, (size_t)E.L[(size_t)l - 1].S.cap * o * 4, st));
       GemmParams p;  // d_self = dp W[:, :d]  -> scatter-add into the rows of layer l-1
       p.M_dev = cnt(lb.S);
+      p.M_hint = (int)lb.S.hint;
       p.M_max = (int)lb.S.cap;
       p.N = d;
       p.K = o;
@@ -497,6 +504,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     {
       GemmParams p;  // d_agg = dp W[:, d:]
       p.M_dev = cnt(lb.S);
+      p.M_hint = (int)lb.S.hint;
       p.M_max = (int)lb.S.cap;
       p.N = hd;
       p.K = o;
@@ -524,6 +532,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     if (l > 0) {
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
       p.M_dev = cnt(lb.N);
+      p.M_hint = (int)lb.N.hint;
       p.M_max = (int)lb.N.cap;
       p.N = d;
       p.K = hd;
@@ -672,6 +681,29 @@ int pinsage_engine_timing_get(const pinsage_engine* e, int idx, char* name, int6
   name[name_len - 1] = 0;
   *ms = t.ms;
   *calls = t.calls;
+  return kOk;
+}
+
+int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, int64_t* N,
+                               void* stream) {
+  const Engine* E = reinterpret_cast<const Engine*>(e);
+  PS_CHECK_HIP(hipStreamSynchronize((hipStream_t)stream));
+  for (size_t l = 0; l < E->L.size(); ++l) {
+    int v = 0;
+    PS_CHECK_HIP(hipMemcpy(&v, at<int>(ws, E->L[l].S.count), 4, hipMemcpyDeviceToHost));
+    S[l] = v;
+    PS_CHECK_HIP(hipMemcpy(&v, at<int>(ws, E->L[l].N.count), 4, hipMemcpyDeviceToHost));
+    N[l] = v;
+  }
+  return kOk;
+}
+
+int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t* N) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  for (size_t l = 0; l < E->L.size(); ++l) {
+    E->L[l].S.hint = S ? S[l] : 0;
+    E->L[l].N.hint = N ? N[l] : 0;
+  }
   return kOk;
 }
 

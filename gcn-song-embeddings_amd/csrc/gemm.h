@@ -47,7 +47,15 @@ struct GemmParams {
   int64_t ldm = 0;
   float* norms = nullptr;         // kEpiL2Norm: per-row L2 norms
   int splits = 1;                 // kEpiPartial: split-K count
+  int M_hint = 0;                 // expected M (device-side M): picks the block tile
+  int cfg = -1;                   // force a tile config (tests); -1 = choose by size
 };
+
+// Block-tile configurations (4 waves each): rows x cols, k-depth per stage.
+//   0: 128 x 128 x 16  (2x2 waves of 64x64)      large M
+//   1:  64 x 128 x 32  (2x2 waves of 32x64)      medium M
+//   2:  32 x 128 x 32  (1x4 waves of 32x32)      small M, N = 128 (W projection)
+int gemm_pick_config(int M, int N, int splits);
 
 int launch_gemm(const GemmParams& p, hipStream_t st);
 

@@ -11,80 +11,99 @@
 // an XCD's L2 (blocks b and b+8 land on one XCD).
 #include "gemm.h"
 
+#include <algorithm>
+
 namespace ps {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 16, PADF = 4;
-constexpr int LDS_W = 128 + PADF;  // floats per k-row of a staged tile
+constexpr int PADF = 4;  // LDS row padding (floats): conflict-free b32 fragment reads, 16-B aligned rows
 
-// Rows of a K-major operand ([row][k] in memory) for this thread: 2 float4 per tile.
-// p2 is the row base in the second K segment (k >= K1), if any.
+// Rows of a K-major operand ([row][k] in memory) handled by this thread.
+template <int NV>
 struct KRows {
-  const float* p[2];
-  const float* p2[2];
+  const float* p[NV];
+  const float* p2[NV];
 };
 
-__device__ __forceinline__ void kmajor_rows(KRows& R, int tid, int r0, int rmax, const float* a,
-                                            int64_t lda, const int32_t* idx, const float* a2,
-                                            int64_t lda2, const int32_t* idx2) {
+template <int R, int BK>
+struct Shape {
+  static constexpr int KV = BK / 4;               // float4 per row per stage (K-major)
+  static constexpr int TOT_K = R * KV;            // float4 per stage, K-major
+  static constexpr int MV = R / 4;                // float4 per k-row (MN-major)
+  static constexpr int TOT_MN = BK * MV;          // float4 per stage, MN-major
+  static constexpr int NV = (TOT_K + 255) / 256;  // float4 per thread (same count both layouts)
+  static constexpr int W = R + PADF;              // floats per staged k-row
+};
+
+template <int R, int BK>
+__device__ __forceinline__ void kmajor_rows(KRows<(Shape<R, BK>::NV)>& Rw, int tid, int r0, int rmax,
+                                            const float* a, int64_t lda, const int32_t* idx,
+                                            const float* a2, int64_t lda2, const int32_t* idx2) {
+  using S = Shape<R, BK>;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < S::NV; ++i) {
     const int lin = tid + 256 * i;
-    const int row = r0 + (lin >> 2);
-    if (row < rmax) {
+    const int row = r0 + lin / S::KV;
+    Rw.p[i] = nullptr;
+    Rw.p2[i] = nullptr;
+    if (lin < S::TOT_K && row < rmax) {
       const int64_t r = idx ? idx[row] : row;
-      R.p[i] = a + r * lda;
+      Rw.p[i] = a + r * lda;
       if (a2) {
         const int64_t r2 = idx2 ? idx2[row] : row;
-        R.p2[i] = a2 + r2 * lda2;
-      } else {
-        R.p2[i] = nullptr;
+        Rw.p2[i] = a2 + r2 * lda2;
       }
-    } else {
-      R.p[i] = nullptr;
-      R.p2[i] = nullptr;
     }
   }
 }
 
-// K-major operand tile -> registers (k0 = absolute k of the tile).  Each float4
-// chunk picks its segment on its own, so K1 only has to be a multiple of 4.
-__device__ __forceinline__ void kmajor_load(float4 (&v)[2], const KRows& R, int tid, int k0,
+// K-major operand stage -> registers.  Each float4 chunk picks its K segment
+// on its own (torch.cat along K without a concat buffer), so K1 % 4 == 0 suffices.
+template <int R, int BK>
+__device__ __forceinline__ void kmajor_load(float4 (&v)[(Shape<R, BK>::NV)],
+                                            const KRows<(Shape<R, BK>::NV)>& Rw, int tid, int k0,
                                             int kend, int K1) {
+  using S = Shape<R, BK>;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int kc = (tid + 256 * i) & 3;
-    const int k = k0 + kc * 4;
+  for (int i = 0; i < S::NV; ++i) {
+    const int lin = tid + 256 * i;
+    const int k = k0 + (lin % S::KV) * 4;
     const bool seg2 = K1 >= 0 && k >= K1;
-    const float* base = seg2 ? R.p2[i] : R.p[i];
-    if (R.p[i] && k < kend) v[i] = *reinterpret_cast<const float4*>(base + (seg2 ? k - K1 : k));
+    const float* base = seg2 ? Rw.p2[i] : Rw.p[i];
+    if (Rw.p[i] && k < kend) v[i] = *reinterpret_cast<const float4*>(base + (seg2 ? k - K1 : k));
     else v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
-__device__ __forceinline__ void kmajor_store(float (*S)[LDS_W], const float4 (&v)[2], int tid) {
+template <int R, int BK>
+__device__ __forceinline__ void kmajor_store(float (*Sm)[(Shape<R, BK>::W)],
+                                             const float4 (&v)[(Shape<R, BK>::NV)], int tid) {
+  using S = Shape<R, BK>;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < S::NV; ++i) {
     const int lin = tid + 256 * i;
-    const int row = lin >> 2, kc = lin & 3;
-    S[kc * 4 + 0][row] = v[i].x;
-    S[kc * 4 + 1][row] = v[i].y;
-    S[kc * 4 + 2][row] = v[i].z;
-    S[kc * 4 + 3][row] = v[i].w;
+    if (lin >= S::TOT_K) continue;
+    const int row = lin / S::KV, kc = (lin % S::KV) * 4;
+    Sm[kc + 0][row] = v[i].x;
+    Sm[kc + 1][row] = v[i].y;
+    Sm[kc + 2][row] = v[i].z;
+    Sm[kc + 3][row] = v[i].w;
   }
 }
 
 // MN-major operand ([k][col] in memory, k rows optionally gathered)
-__device__ __forceinline__ void mnmajor_load(float4 (&v)[2], int tid, const float* a, int64_t lda,
-                                             const int32_t* idx, int c0, int cmax, int k0,
-                                             int kend) {
+template <int R, int BK>
+__device__ __forceinline__ void mnmajor_load(float4 (&v)[(Shape<R, BK>::NV)], int tid, const float* a,
+                                             int64_t lda, const int32_t* idx, int c0, int cmax,
+                                             int k0, int kend) {
+  using S = Shape<R, BK>;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < S::NV; ++i) {
     const int lin = tid + 256 * i;
-    const int kr = lin >> 5, cc = lin & 31;
+    const int kr = lin / S::MV, cc = lin % S::MV;
     const int k = k0 + kr;
     const int c = c0 + cc * 4;
-    if (k < kend && c < cmax) {
+    if (lin < S::TOT_MN && k < kend && c < cmax) {
       const int64_t r = idx ? idx[k] : k;
       v[i] = *reinterpret_cast<const float4*>(a + r * lda + c);
     } else {
@@ -92,21 +111,29 @@ __device__ __forceinline__ void mnmajor_load(float4 (&v)[2], int tid, const floa
     }
   }
 }
-__device__ __forceinline__ void mnmajor_store(float (*S)[LDS_W], const float4 (&v)[2], int tid) {
+template <int R, int BK>
+__device__ __forceinline__ void mnmajor_store(float (*Sm)[(Shape<R, BK>::W)],
+                                              const float4 (&v)[(Shape<R, BK>::NV)], int tid) {
+  using S = Shape<R, BK>;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < S::NV; ++i) {
     const int lin = tid + 256 * i;
-    const int kr = lin >> 5, cc = lin & 31;
-    *reinterpret_cast<float4*>(&S[kr][cc * 4]) = v[i];
+    if (lin >= S::TOT_MN) continue;
+    const int kr = lin / S::MV, cc = lin % S::MV;
+    *reinterpret_cast<float4*>(&Sm[kr][cc * 4]) = v[i];
   }
 }
 
-template <bool AK, bool BKM>
+// WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK.
+template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) float As[2][BK][LDS_W];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDS_W];
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  using SA = Shape<BM, BK>;
+  using SB = Shape<BN, BK>;
+  __shared__ __attribute__((aligned(16))) float As[2][BK][SA::W];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][SB::W];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int M = p.M_dev ? *p.M_dev : p.M;
   const int K = p.K_dev ? *p.K_dev : p.K;
   const int N = p.N;
@@ -121,6 +148,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     G = tiles_m;
     W = tiles_n;
   }
+  // tiles of one row panel (or one split) are dealt to blocks b, b+8, ...:
+  // one XCD under round-robin placement, so they share its L2 (speed only)
   const int iters = 8 * ((G + 7) / 8) * W;
   for (int t = blockIdx.x; t < iters; t += gridDim.x) {
     const int xcd = t & 7, s = t >> 3;
@@ -141,30 +170,31 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     const int ke = min(K, kb + kchunk);
     const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
 
-    KRows RA, RB;
-    if (AK) kmajor_rows(RA, tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
-    if (BKM) kmajor_rows(RB, tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
+    KRows<SA::NV> RA;
+    KRows<SB::NV> RB;
+    if (AK) kmajor_rows<BM, BK>(RA, tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
+    if (BKM) kmajor_rows<BN, BK>(RB, tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
 
-    f32x16 acc[2][2];
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float4 va[2], vb[2];
+    float4 va[SA::NV], vb[SB::NV];
     auto load = [&](int k0) {
-      if (AK) kmajor_load(va, RA, tid, k0, ke, p.K1);
-      else mnmajor_load(va, tid, p.a, p.lda, p.a_idx, m0, M, k0, ke);
-      if (BKM) kmajor_load(vb, RB, tid, k0, ke, -1);
-      else mnmajor_load(vb, tid, p.b, p.ldb, p.b_idx, n0, N, k0, ke);
+      if (AK) kmajor_load<BM, BK>(va, RA, tid, k0, ke, p.K1);
+      else mnmajor_load<BM, BK>(va, tid, p.a, p.lda, p.a_idx, m0, M, k0, ke);
+      if (BKM) kmajor_load<BN, BK>(vb, RB, tid, k0, ke, -1);
+      else mnmajor_load<BN, BK>(vb, tid, p.b, p.ldb, p.b_idx, n0, N, k0, ke);
     };
     auto store = [&](int buf) {
-      if (AK) kmajor_store(As[buf], va, tid);
-      else mnmajor_store(As[buf], va, tid);
-      if (BKM) kmajor_store(Bs[buf], vb, tid);
-      else mnmajor_store(Bs[buf], vb, tid);
+      if (AK) kmajor_store<BM, BK>(As[buf], va, tid);
+      else mnmajor_store<BM, BK>(As[buf], va, tid);
+      if (BKM) kmajor_store<BN, BK>(Bs[buf], vb, tid);
+      else mnmajor_store<BN, BK>(Bs[buf], vb, tid);
     };
     if (nk > 0) {
       load(kb);
@@ -178,46 +208,47 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
         const int k = 2 * kk + h;
-        const float a0 = As[cur][k][wm * 64 + l32];
-        const float a1 = As[cur][k][wm * 64 + 32 + l32];
-        const float b0 = Bs[cur][k][wn * 64 + l32];
-        const float b1 = Bs[cur][k][wn * 64 + 32 + l32];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[cur][k][(wm * TM + i) * 32 + l32];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][k][(wn * TN + j) * 32 + l32];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
       if (it + 1 < nk) store(cur ^ 1);
       __syncthreads();
     }
 
     // ------------------------------------------------------------ epilogue
-    // acc[i][j][r] -> row m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*h, col n0 + wn*64 + j*32 + l32
+    // acc[i][j][r] -> row m0 + (wm*TM+i)*32 + (r&3) + 8*(r>>2) + 4*h, col n0 + (wn*TN+j)*32 + l32
     if (p.epi == kEpiPartial) {
       float* C = p.c + (int64_t)split * M * p.ldc;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           if (row >= M) continue;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + l32;
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + (wn * TN + j) * 32 + l32;
             if (col < N) C[(int64_t)row * p.ldc + col] = acc[i][j][r];
           }
         }
     } else if (p.epi == kEpiL2Norm) {
-      float* red = &As[0][0][0];  // [2][128] row partial sums (LDS free after the k loop)
-      float ss[2][16];
+      float* red = &As[0][0][0];  // [WN][BM] row partial sums (LDS free after the k loop)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float s2 = 0.f;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + l32;
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + (wn * TN + j) * 32 + l32;
             float v = acc[i][j][r] + (p.bias && col < N ? p.bias[col] : 0.f);
             v = lrelu(v);
             if (col >= N) v = 0.f;
@@ -226,28 +257,24 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
           }
 #pragma unroll
           for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
-          ss[i][r] = s2;
+          if (l32 == 0) red[wn * BM + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h] = s2;
         }
-      if (l32 == 0) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            red[wn * 128 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h] = ss[i][r];
-      }
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int lrow = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int lrow = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           const int row = m0 + lrow;
           if (row >= M) continue;
-          const float nrm = sqrtf(red[lrow] + red[128 + lrow]);
+          float tot = 0.f;
+#pragma unroll
+          for (int q = 0; q < WN; ++q) tot += red[q * BM + lrow];
+          const float nrm = sqrtf(tot);
           const int64_t dst = p.c_idx ? p.c_idx[row] : row;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + l32;
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + (wn * TN + j) * 32 + l32;
             if (col < N) p.c[dst * p.ldc + col] = acc[i][j][r] / nrm;
           }
           if (p.norms && wn == 0 && l32 == 0) p.norms[row] = nrm;
@@ -255,15 +282,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     } else {
       const bool accum = p.epi == kEpiAccum;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           if (row >= M) continue;
           const int64_t dst = p.c_idx ? p.c_idx[row] : row;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + l32;
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + (wn * TN + j) * 32 + l32;
             if (col >= N) continue;
             float v = acc[i][j][r];
             if (p.bias) v += p.bias[col];
@@ -278,6 +305,37 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   }
 }
 
+constexpr int kCfgBM[3] = {128, 64, 32};
+
+// Cost model: tiles are dealt round-robin over 256 CUs, so a launch takes
+// ~ceil(tiles / 256) tile-times and a tile-time is ~ BM (fixed BN, same K).
+// Pick the cheapest; ties go to the larger tile (fewer operand re-reads).
+int gemm_pick_config(int M, int N, int splits) {
+  if (splits > 1) return 0;
+  const int64_t tn = (N + 127) / 128;
+  int best = 0;
+  int64_t best_cost = -1;
+  for (int c = 0; c < 3; ++c) {
+    const int64_t tiles = ((M + kCfgBM[c] - 1) / kCfgBM[c]) * tn;
+    const int64_t cost = ((tiles + 255) / 256) * kCfgBM[c];
+    if (best_cost < 0 || cost < best_cost) {
+      best = c;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+template <bool AK, bool BKM>
+static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
+  if (cfg == 0)
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16>), g, dim3(256), 0, st, p);
+  else if (cfg == 1)
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 32>), g, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32>), g, dim3(256), 0, st, p);
+}
+
 int launch_gemm(const GemmParams& p, hipStream_t st) {
   const int Mmax = p.M_dev ? p.M_max : p.M;
   const int Kmax = p.K_dev ? p.K_max : p.K;
@@ -289,24 +347,23 @@ int launch_gemm(const GemmParams& p, hipStream_t st) {
   PS_REQUIRE(p.a_kmajor || (p.M % 4 == 0 && !p.M_dev), kErrArg,
              "gemm: M-major A needs a static M that is a multiple of 4");
   PS_REQUIRE(p.b_kmajor || p.N % 4 == 0, kErrArg, "gemm: N-major B needs N % 4 == 0");
-  PS_REQUIRE(p.epi != kEpiL2Norm || p.N <= BN, kErrArg, "gemm: L2-norm epilogue needs N <= 128");
+  PS_REQUIRE(p.epi != kEpiL2Norm || p.N <= 128, kErrArg, "gemm: L2-norm epilogue needs N <= 128");
   PS_REQUIRE(p.epi != kEpiPartial || (!p.M_dev && !p.c_idx), kErrArg,
              "gemm: split-K partials need a static M");
-  const int tiles_m = (Mmax + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
+  const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
+  const int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, splits);
+  const int BMc = kCfgBM[cfg];
+  const int tiles_m = (Mmax + BMc - 1) / BMc, tiles_n = (p.N + 127) / 128;
   int G = splits > 1 ? splits : tiles_m, W = splits > 1 ? tiles_m * tiles_n : tiles_n;
   int64_t iters = 8LL * ((G + 7) / 8) * W;
   int grid = (int)(iters < 1024 ? iters : 1024);
   grid = (grid + 7) / 8 * 8;
-  dim3 g(grid), b(256);
-  if (p.a_kmajor && p.b_kmajor)
-    hipLaunchKernelGGL((gemm_f32_kernel<true, true>), g, b, 0, st, p);
-  else if (p.a_kmajor && !p.b_kmajor)
-    hipLaunchKernelGGL((gemm_f32_kernel<true, false>), g, b, 0, st, p);
-  else if (!p.a_kmajor && p.b_kmajor)
-    hipLaunchKernelGGL((gemm_f32_kernel<false, true>), g, b, 0, st, p);
-  else
-    hipLaunchKernelGGL((gemm_f32_kernel<false, false>), g, b, 0, st, p);
+  dim3 g(grid);
+  if (p.a_kmajor && p.b_kmajor) launch_cfg<true, true>(cfg, g, st, p);
+  else if (p.a_kmajor && !p.b_kmajor) launch_cfg<true, false>(cfg, g, st, p);
+  else if (!p.a_kmajor && p.b_kmajor) launch_cfg<false, true>(cfg, g, st, p);
+  else launch_cfg<false, false>(cfg, g, st, p);
   PS_CHECK_LAUNCH();
   return kOk;
 }

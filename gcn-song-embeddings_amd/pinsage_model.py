@@ -382,6 +382,24 @@ class _Engine:
     def new_workspace(self, dev):
         return torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
 
+    def counts(self, ws):
+        """Frontier sizes (|S_l|, |N_l|) of the last forward in ws (synchronises)."""
+        L = int(self.cfg.n_layers)
+        S = (ctypes.c_int64 * L)()
+        N = (ctypes.c_int64 * L)()
+        nat.check(nat.lib().pinsage_engine_read_counts(self.h, nat.ptr(ws), S, N, nat.stream_ptr()),
+                  "read_counts")
+        return list(S), list(N)
+
+    def tune(self, ws, margin=1.15):
+        """Use the last forward's frontier sizes as GEMM tile hints (speed only)."""
+        S, N = self.counts(ws)
+        L = len(S)
+        hs = (ctypes.c_int64 * L)(*[int(x * margin) + 1 for x in S])
+        hn = (ctypes.c_int64 * L)(*[int(x * margin) + 1 for x in N])
+        nat.lib().pinsage_engine_set_hints(self.h, hs, hn)
+        return S, N
+
     def view(self, ws, off, dtype, n):
         nbytes = n * torch.empty((), dtype=dtype).element_size()
         return ws[off:off + nbytes].view(dtype)

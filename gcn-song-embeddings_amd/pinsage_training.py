@@ -133,7 +133,13 @@ class _FusedStep:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self._lr_host = None
         self.host_batch = None
+        self._tuned = False
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        # the device step (forward, loss, backward, Adam) is captured once into a
+        # hipGraph and replayed: one launch instead of ~90 per step
+        self.use_graph = os.environ.get("PINSAGE_HIPGRAPH", "1") != "0"
+        self.graph = None
+        self.graph_B = None
 
     def ensure(self, B):
         r = self.runner
@@ -151,7 +157,14 @@ class _FusedStep:
             off = r.engine.off
             self.ids_view = r.engine.view(self.ws, int(off.ids), torch.int64, r.engine.cfg.max_pos)
             self.scal = r.engine.view(self.ws, int(off.scalars), torch.float32, 4)
-            self.host_batch = torch.empty(3 * r.engine.cfg.max_pos, dtype=torch.int64).pin_memory()
+            # two pinned staging buffers: the host fills one while the previous
+            # step's H2D copy from the other may still be queued
+            self.host_batch = [torch.empty(r.engine.cfg.max_pos, dtype=torch.int64).pin_memory()
+                               for _ in range(2)]
+            self.host_ev = [None, None]
+            self.slot = 0
+            self._tuned = False
+            self.graph = None
 
     def adopt_optimizer_state(self):
         """Use the optimizer's Adam state (if any, e.g. after load_state_dict) as
@@ -180,6 +193,51 @@ class _FusedStep:
             if st is not None:
                 st["step"] = torch.tensor(float(self.host_step))
 
+    def _stage(self, batch, B):
+        """Copy the [B, 3] batch into the engine's device id buffer."""
+        k = self.slot
+        self.slot ^= 1
+        if self.host_ev[k] is not None:
+            self.host_ev[k].synchronize()
+        hb = self.host_batch[k][:3 * B]
+        hb.copy_(batch.reshape(-1).to(torch.int64))
+        self.ids_view[:3 * B].copy_(hb, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.host_ev[k] = ev
+
+    def _device_step(self, B, with_adam):
+        tr = self.tr
+        e = self.runner.engine
+        st = nat.stream_ptr()
+        L = nat.lib()
+        nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
+                  "forward")
+        nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
+        nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.ws), st), "backward")
+        if with_adam:
+            self._adam()
+
+    def _adam(self):
+        g = self.tr.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, nat.ptr(self.lr_dev),
+                                                nat.ptr(self.step_dev), float(b1), float(b2),
+                                                float(g["eps"]), nat.stream_ptr()), "adam")
+
+    def _signature(self, feats, table):
+        return (self.runner.flat.data_ptr(), self.grads.data_ptr(), self.m.data_ptr(),
+                self.v.data_ptr(), feats.data_ptr(), table.nb32.data_ptr(), table.wn.data_ptr(),
+                self.ws.data_ptr(), id(self.runner.engine))
+
+    def _capture(self, B, sig):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._device_step(B, with_adam=not self.dist)
+        self.graph = g
+        self.graph_B = B
+        self.graph_sig = sig
+
     def __call__(self, batch):
         tr = self.tr
         batch = torch.as_tensor(batch)
@@ -189,31 +247,39 @@ class _FusedStep:
         feats = r.features(tr.features)
         table = r.table(tr.nbhds)
         r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)
-        # stage the [B, 3] batch into the engine's id buffer
-        hb = self.host_batch[:3 * B]
-        hb.copy_(batch.reshape(-1).to(torch.int64))
-        self.ids_view[:3 * B].copy_(hb, non_blocking=True)
-        e = r.engine
-        st = nat.stream_ptr()
-        L = nat.lib()
-        nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
-                  "forward")
-        nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
-        nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.ws), st), "backward")
-        if self.dist:
-            ws = torch.distributed.get_world_size()
-            torch.distributed.all_reduce(self.grads)
-            self.grads.mul_(1.0 / ws)
         lr = float(tr.optimizer.param_groups[0]["lr"])
         if lr != self._lr_host:
             self.lr_dev.fill_(lr)
             self._lr_host = lr
-        g = tr.optimizer.param_groups[0]
-        b1, b2 = g["betas"]
-        nat.check(L.pinsage_engine_adam(e.h, nat.ptr(self.lr_dev), nat.ptr(self.step_dev), float(b1),
-                                        float(b2), float(g["eps"]), st), "adam")
+        self._stage(batch, B)
+        sig = self._signature(feats, table)
+        if self.graph is not None and (self.graph_B != B or self.graph_sig != sig or not self.use_graph):
+            self.graph = None  # buffers moved: the captured pointers are stale
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            e = r.engine
+            st = nat.stream_ptr()
+            L = nat.lib()
+            nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
+                      "forward")
+            nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
+            if not self._tuned:  # once: frontier sizes of a real batch pick the GEMM tiles
+                e.tune(self.ws)
+                self._tuned = True
+            nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.ws), st), "backward")
+            if not self.dist:
+                self._adam()
+            if self.use_graph and self._tuned and self.graph is None:
+                self._capture(B, sig)
+        if self.dist:
+            ws = torch.distributed.get_world_size()
+            torch.distributed.all_reduce(self.grads)
+            self.grads.mul_(1.0 / ws)
+            self._adam()
         self.host_step += 1
-        return self.scal[0], self.scal[1], self.scal[3]
+        out = self.scal.clone()
+        return out[0], out[1], out[3]
 
 
 class PinSage:

@@ -170,6 +170,14 @@ int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
 int pinsage_engine_adam(pinsage_engine* e, const float* lr_dev, int32_t* step_dev, float beta1,
                         float beta2, float eps, void* stream);
 
+/* Frontier sizes of the last forward in ws (synchronises the stream): S[l] =
+ * |S_l| (nodes convolved at layer l), N[l] = |N_l| (distinct neighbours). */
+int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, int64_t* N,
+                               void* stream);
+/* Expected frontier sizes (e.g. from read_counts): choose GEMM block tiles
+ * that fill the chip; sizes stay device-side, hints only affect speed. */
+int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t* N);
+
 /* Per-launch-site HIP-event timing on the launch stream (bench/profiling):
  * enable (also clears), collect after the work (synchronises the events), then
  * read site idx = 0.. until PINSAGE_ERR_ARG: name, total ms, number of calls. */
