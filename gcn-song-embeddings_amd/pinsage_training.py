@@ -115,6 +115,17 @@ def batch_variance(h):
     return torch.prod(var)
 
 
+# ----------------------------------------------------------------------------- data parallel
+def average_gradients(flat):
+    """Mean of a flat gradient buffer over the process group: ONE all-reduce
+    (RCCL over xGMI on MI355X nodes; gloo on CPU)."""
+    d = torch.distributed
+    if d.is_available() and d.is_initialized() and d.get_world_size() > 1:
+        d.all_reduce(flat)
+        flat.mul_(1.0 / d.get_world_size())
+    return flat
+
+
 # ----------------------------------------------------------------------------- trainer
 class _FusedStep:
     """Device state of the fused train step: flat param/grad/Adam buffers,
@@ -273,9 +284,7 @@ class _FusedStep:
             if self.use_graph and self._tuned and self.graph is None:
                 self._capture(B, sig)
         if self.dist:
-            ws = torch.distributed.get_world_size()
-            torch.distributed.all_reduce(self.grads)
-            self.grads.mul_(1.0 / ws)
+            average_gradients(self.grads)
             self._adam()
         self.host_step += 1
         out = self.scal.clone()

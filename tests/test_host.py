@@ -1,0 +1,195 @@
+"""CPU-side checks of the product: the C-ABI library loads and exports what
+include/pinsage_hip.h declares, host RNG / batch sampling reproduce torch and
+the reference draw for draw, the JSON loader and CSR graph match the reference,
+and compute entry points fail loudly without a GPU (no CPU fallback)."""
+import os
+import re
+import shutil
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, golden
+
+
+def _header_functions():
+    txt = open(os.path.join(REPO, "include", "pinsage_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(pinsage_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    import _native
+    L = _native.lib()
+    names = _header_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(L, n), n
+    # the ctypes binding covers exactly the header
+    assert sorted(_native.EXPORTED) == names
+
+
+def test_library_loads_without_gpu():
+    import _native
+    assert _native.lib().pinsage_version() >= 100
+    assert _native.lib().pinsage_device_count() >= 0
+
+
+def test_native_mt_matches_torch_and_skip():
+    import _native as nat
+    torch.manual_seed(77)
+    mt = nat.MT.from_torch()
+    ref = [int(torch.randint(1000, ())) for _ in range(3000)]
+    assert (mt.draws(3000) % 1000).tolist() == ref
+    # skip == draw-and-discard, across twist boundaries
+    for n in (0, 1, 623, 624, 625, 1247, 5000):
+        a = nat.MT().seed(5)
+        b = nat.MT().seed(5)
+        a.draws(n)
+        b.skip(n)
+        assert (a.draws(700) == b.draws(700)).all(), n
+
+
+def test_native_mt_state_roundtrip():
+    import _native as nat
+    torch.manual_seed(3)
+    with nat.torch_rng() as mt:
+        mt.draws(1234)
+    x = int(torch.randint(1000, ()))
+    torch.manual_seed(3)
+    for _ in range(1234):
+        torch.randint(1000, ())
+    assert int(torch.randint(1000, ())) == x
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (2, 2), (37, 37), (5000, 17), (100000, 512), (300, 0)])
+def test_randperm_prefix_matches_torch(n, k):
+    import _native as nat
+    torch.manual_seed(n + k)
+    with nat.torch_rng() as mt:
+        got = mt.randperm_prefix(n, k)
+    after = int(torch.randint(1000, ()))
+    torch.manual_seed(n + k)
+    ref = torch.randperm(n)[:k].numpy()
+    assert (got == ref).all()
+    assert int(torch.randint(1000, ())) == after
+
+
+def test_sample_batch_matches_golden():
+    import pinsage_training as pt
+    d = golden("batch")
+    pos = torch.from_numpy(d["positives"])
+    all_ids = torch.arange(int(d["n_items"]))
+    torch.manual_seed(5)
+    for i in range(3):
+        b, ns = pt.sample_batch(all_ids, pos, int(d[f"b{i}_bs"]), None, hard_negatives=False)
+        assert (b.numpy() == d[f"b{i}_batch"]).all()
+        assert (ns.numpy() == d[f"b{i}_nodeset"]).all()
+    got = np.array([int(torch.randint(2 ** 31, ())) for _ in range(len(d["after"]))])
+    assert (got == d["after"]).all()
+
+
+def test_sample_batch_component_functions_match_torch():
+    import pinsage_training as pt
+    d = golden("batch")
+    pos = torch.from_numpy(d["positives"])
+    all_ids = torch.arange(int(d["n_items"]))
+    torch.manual_seed(8)
+    pb = pt.sample_positives_with_rep(pos, 64)
+    b, ns = pt.sample_easy_negatives(all_ids, pb)
+    torch.manual_seed(8)
+    b2, ns2 = pt.sample_batch(all_ids, pos, 64, None, hard_negatives=False)
+    assert torch.equal(b, b2) and torch.equal(ns, ns2)
+
+
+def test_max_margin_loss_matches_golden():
+    import pinsage_training as pt
+    d = golden("loss")
+    for i in range(3):
+        hq, hp, hn = (torch.from_numpy(d[f"c{i}_{k}"]).requires_grad_() for k in ("hq", "hp", "hn"))
+        loss = pt.max_margin_loss(hq, hp, hn, float(d[f"c{i}_margin"]))
+        loss.backward()
+        assert abs(loss.item() - float(d[f"c{i}_loss"])) <= 1e-6 * max(1.0, abs(float(d[f"c{i}_loss"])))
+        np.testing.assert_allclose(hq.grad.numpy(), d[f"c{i}_gq"], rtol=1e-5, atol=1e-7)
+
+
+def test_spotify_graph_matches_reference_loader():
+    import spotify_graph
+    import synthetic
+    d = golden("dataset")
+    ids = [str(x) for x in d["track_ids"]]
+    pg = synthetic.make_playlist_graph(len(ids), int(d["n_cols"]), 9000, seed=int(d["graph_seed"]))
+    tmp = tempfile.mkdtemp()
+    try:
+        ds_dir = os.path.join(tmp, "ds")
+        synthetic.write_spotify_dataset(ds_dir, pg, track_ids=ids, seed=int(d["json_seed"]))
+        fdir = os.path.join(ds_dir, "features_test")
+        os.makedirs(fdir)
+        raw = np.random.default_rng(int(d["feat_seed"])).standard_normal((len(ids), 8)).astype(np.float32) * 3 + 1
+        for i, tid in enumerate(ids):
+            torch.save(torch.from_numpy(raw[i].copy()), os.path.join(fdir, tid + ".pt"))
+        # positives of the real dataset_micro ids, re-serialised from the fixture pairs
+        import json
+        pairs = [{"a": ids[a], "b": ids[b]} for a, b in d["positives"]]
+        with open(os.path.join(ds_dir, "positives.json"), "w") as f:
+            json.dump(pairs, f)
+        ds = spotify_graph.SpotifyGraph(ds_dir, fdir)
+        g, track_ids, col_ids, features = ds.to_dgl_graph()
+        assert track_ids == ids and col_ids == [str(x) for x in d["col_ids"]]
+        src, dst = g.edges()
+        assert (src.numpy() == d["src"]).all() and (dst.numpy() == d["dst"]).all()
+        assert (g.successors(69).numpy() == d["succ69"]).all()
+        np.testing.assert_allclose(features.numpy(), d["features"], rtol=1e-6, atol=1e-6)
+        torch.manual_seed(3)
+        positives = ds.load_positives(os.path.join(ds_dir, "positives.json"))
+        assert (positives.numpy() == d["positives"]).all()
+        got = np.array([int(torch.randint(2 ** 31, ())) for _ in range(len(d["after"]))])
+        assert (got == d["after"]).all()
+        tr, te = ds.load_positives_split(os.path.join(ds_dir, "positives.json"))
+        assert (tr.numpy() == d["split_train"]).all() and (te.numpy() == d["split_test"]).all()
+    finally:
+        shutil.rmtree(tmp)
+
+
+def test_csr_graph_api():
+    import graph
+    src = [5, 0, 0, 3, 5, 1, 0]
+    dst = [1, 4, 2, 0, 0, 0, 1]
+    g = graph.CSRGraph(6, src, dst)
+    assert g.number_of_nodes() == 6 and g.num_edges() == 7 and len(g) == 6
+    assert g.successors(0).tolist() == [4, 2, 1]      # edge-insertion order
+    assert g.successors(5).tolist() == [1, 0]
+    assert g.predecessors(0).tolist() == [3, 5, 1]
+    assert g.in_degrees(0) == 3 and g.in_degrees().tolist() == [3, 2, 1, 0, 1, 0]
+    s, d = g.edges()
+    assert sorted(zip(s.tolist(), d.tolist())) == sorted(zip(src, dst))
+    a = g.adj(scipy_fmt="csr")
+    assert a.shape == (6, 6) and a[0, 4] == 1 and a[4, 0] == 0
+    with pytest.raises(ValueError):
+        graph.CSRGraph(3, [0, 7], [1, 1])
+
+
+def test_synthetic_graph_invariants():
+    import synthetic
+    pg = synthetic.make_playlist_graph(2000, 300, 20000, seed=4)
+    indptr, indices = pg.csr()
+    deg = np.diff(indptr)
+    assert deg[:2000].min() >= 1 and deg[2000:].min() >= 2
+    # both directions present, in JSON edge order
+    src, dst = pg.edge_arrays()
+    assert (src[0::2] == dst[1::2]).all() and (dst[0::2] == src[1::2]).all()
+    pos = synthetic.make_positives(pg, 5000, seed=1)
+    assert (pos[:, 0] != pos[:, 1]).all()
+    pg2 = synthetic.make_playlist_graph(2000, 300, 20000, seed=4)
+    assert (pg2.mem_track == pg.mem_track).all()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_compute_fails_loudly_without_gpu():
+    import graph
+    import pinsage_model as pm
+    g = graph.CSRGraph(4, [0, 1, 2, 3], [2, 3, 0, 1])
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        pm.do_random_walks(g, torch.tensor([0]), 3, 0.85)
