@@ -12,6 +12,8 @@
 //   adam            torch.optim.Adam step (pinsage_training.py:147,191)
 #include "common.h"
 
+#include <algorithm>
+
 namespace ps {
 
 __device__ __forceinline__ int32_t rank_in(const unsigned long long* bits, const uint32_t* prefix,
@@ -105,11 +107,30 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
 }
 
 // ---------------------------------------------------------------- transpose (CSR by q row)
-// Lanes of a wave holding the same q row combine into one atomic (popular
-// tracks sit in many neighbour lists of one wave's rows).
-__global__ void csr_count_kernel(const int32_t* __restrict__ loc, const int* __restrict__ nS, int T,
-                                 int* __restrict__ cnt) {
+// Popular tracks sit in thousands of neighbour lists, so global per-row
+// counters are hot.  When the distinct-neighbour count fits (<= kLdsRows), each
+// block counts its contiguous slice of occurrences in an LDS histogram and
+// flushes one global atomic per row it touched; otherwise lanes of a wave with
+// the same row combine into one global atomic.
+constexpr int kLdsRows = 16384;
+__global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restrict__ loc,
+                                                         const int* __restrict__ nS, int T,
+                                                         const int* __restrict__ nN,
+                                                         int* __restrict__ cnt) {
+  extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
+  const int U = *nN;
+  if (U <= kLdsRows) {
+    for (int u = threadIdx.x; u < U; u += blockDim.x) hist[u] = 0;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(n, e0 + per);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) atomicAdd(hist + loc[e], 1);
+    __syncthreads();
+    for (int u = threadIdx.x; u < U; u += blockDim.x)
+      if (hist[u]) atomicAdd(cnt + u, hist[u]);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63LL; base < n;
        base += (int64_t)gridDim.x * blockDim.x) {
@@ -187,10 +208,34 @@ __global__ __launch_bounds__(kScanB) void scan_apply_kernel(const int* __restric
     p += v[q];
   }
 }
-__global__ void csr_fill_kernel(const int32_t* __restrict__ loc, const int* __restrict__ nS, int T,
-                                int* __restrict__ cursor, int32_t* __restrict__ occ,
-                                int32_t* __restrict__ occ_u) {
+__global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restrict__ loc,
+                                                        const int* __restrict__ nS, int T,
+                                                        const int* __restrict__ nN,
+                                                        int* __restrict__ cursor,
+                                                        int32_t* __restrict__ occ,
+                                                        int32_t* __restrict__ occ_u) {
+  extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
+  const int U = *nN;
+  if (U <= kLdsRows) {
+    for (int u = threadIdx.x; u < U; u += blockDim.x) hist[u] = 0;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(n, e0 + per);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) atomicAdd(hist + loc[e], 1);
+    __syncthreads();
+    // reserve this block's slots per row: hist[u] becomes the block's base
+    for (int u = threadIdx.x; u < U; u += blockDim.x)
+      if (hist[u]) hist[u] = atomicAdd(cursor + u, hist[u]);
+    __syncthreads();
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      const int32_t u = loc[e];
+      const int pos = atomicAdd(hist + u, 1);
+      occ[pos] = (int32_t)e;
+      occ_u[pos] = u;
+    }
+    return;
+  }
   const int lane = threadIdx.x & 63;
   for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63LL; base < n;
        base += (int64_t)gridDim.x * blockDim.x) {
@@ -233,10 +278,38 @@ __global__ void zero_rows_kernel(float* __restrict__ x, int64_t n, const int* __
     x4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 template <int VEC>
+__device__ __forceinline__ void dq_flush(float* __restrict__ dpq, const float* __restrict__ q, int hid,
+                                         int h4, int c0, int lane, int32_t row, bool atom,
+                                         float4 (&acc)[VEC]) {
+  const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)row * hid);
+  float4* o = reinterpret_cast<float4*>(dpq + (int64_t)row * hid);
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    const int c = c0 + v * 64 + lane;
+    if (c < h4) {
+      const float4 qq = qr[c];
+      const float4 r = make_float4(acc[v].x * lrelu_grad(qq.x), acc[v].y * lrelu_grad(qq.y),
+                                   acc[v].z * lrelu_grad(qq.z), acc[v].w * lrelu_grad(qq.w));
+      if (atom) {
+        float* of = reinterpret_cast<float*>(o + c);
+        atomicAdd(of, r.x);
+        atomicAdd(of + 1, r.y);
+        atomicAdd(of + 2, r.z);
+        atomicAdd(of + 3, r.w);
+      } else {
+        o[c] = r;
+      }
+    }
+    acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int VEC>
 __global__ __launch_bounds__(256) void dq_segment_kernel(
     const int32_t* __restrict__ occ, const int32_t* __restrict__ occ_u,
     const float* __restrict__ wloc, int T, const float* __restrict__ dagg, int64_t ld_dagg,
     const float* __restrict__ q, int hid, const int* __restrict__ nS, float* __restrict__ dpq) {
+  constexpr int G = 4;  // occurrences whose rows are loaded together
   const int64_t total = (int64_t)(*nS) * T;
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -245,7 +318,6 @@ __global__ __launch_bounds__(256) void dq_segment_kernel(
   for (int64_t ch = wid; ch * kSegChunk < total; ch += nw) {
     const int64_t p0 = ch * kSegChunk;
     const int n = (int)min((int64_t)kSegChunk, total - p0);
-    // indices of the chunk: lane j holds position p0 + j
     int32_t my_u = -1, my_e = 0;
     float my_w = 0.f;
     if (lane < n) {
@@ -260,74 +332,45 @@ __global__ __launch_bounds__(256) void dq_segment_kernel(
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       int32_t cur = __shfl(my_u, 0, 64);
-      int seg_start = 0;
-      for (int j = 0; j < n; ++j) {
-        const int32_t u = __shfl(my_u, j, 64);
-        if (u != cur) {
-          // flush segment [seg_start, j) of row cur
-          const bool atom = (seg_start == 0 && cur == u_before);
-          const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)cur * hid);
-          float4* o = reinterpret_cast<float4*>(dpq + (int64_t)cur * hid);
+      bool first = true;  // the current segment started at this chunk's first position
+      for (int j0 = 0; j0 < n; j0 += G) {
+        float4 x[G][VEC];
+        int32_t uu[G];
+        float ww[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int j = j0 + g;
+          const int jj = j < n ? j : n - 1;
+          uu[g] = __shfl(my_u, jj, 64);
+          ww[g] = __shfl(my_w, jj, 64);
+          const int32_t e = __shfl(my_e, jj, 64);
+          const float4* dr = reinterpret_cast<const float4*>(dagg + (int64_t)(e / T) * ld_dagg);
 #pragma unroll
           for (int v = 0; v < VEC; ++v) {
             const int c = c0 + v * 64 + lane;
-            if (c < h4) {
-              const float4 qq = qr[c];
-              float4 r = make_float4(acc[v].x * lrelu_grad(qq.x), acc[v].y * lrelu_grad(qq.y),
-                                     acc[v].z * lrelu_grad(qq.z), acc[v].w * lrelu_grad(qq.w));
-              if (atom) {
-                float* of = reinterpret_cast<float*>(o + c);
-                atomicAdd(of, r.x);
-                atomicAdd(of + 1, r.y);
-                atomicAdd(of + 2, r.z);
-                atomicAdd(of + 3, r.w);
-              } else {
-                o[c] = r;
-              }
+            x[g][v] = (c < h4 && j < n) ? dr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (j0 + g < n) {
+            if (uu[g] != cur) {
+              dq_flush<VEC>(dpq, q, hid, h4, c0, lane, cur, first && cur == u_before, acc);
+              cur = uu[g];
+              first = false;
             }
-            acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-          cur = u;
-          seg_start = j;
-        }
-        const int32_t e = __shfl(my_e, j, 64);
-        const float w = __shfl(my_w, j, 64);
-        const float4* dr = reinterpret_cast<const float4*>(dagg + (int64_t)(e / T) * ld_dagg);
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          const int c = c0 + v * 64 + lane;
-          if (c < h4) {
-            const float4 x = dr[c];
-            acc[v].x = fmaf(w, x.x, acc[v].x);
-            acc[v].y = fmaf(w, x.y, acc[v].y);
-            acc[v].z = fmaf(w, x.z, acc[v].z);
-            acc[v].w = fmaf(w, x.w, acc[v].w);
-          }
-        }
-      }
-      {
-        const bool atom = (seg_start == 0 && cur == u_before) || cur == u_after;
-        const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)cur * hid);
-        float4* o = reinterpret_cast<float4*>(dpq + (int64_t)cur * hid);
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          const int c = c0 + v * 64 + lane;
-          if (c < h4) {
-            const float4 qq = qr[c];
-            float4 r = make_float4(acc[v].x * lrelu_grad(qq.x), acc[v].y * lrelu_grad(qq.y),
-                                   acc[v].z * lrelu_grad(qq.z), acc[v].w * lrelu_grad(qq.w));
-            if (atom) {
-              float* of = reinterpret_cast<float*>(o + c);
-              atomicAdd(of, r.x);
-              atomicAdd(of + 1, r.y);
-              atomicAdd(of + 2, r.z);
-              atomicAdd(of + 3, r.w);
-            } else {
-              o[c] = r;
+            for (int v = 0; v < VEC; ++v) {
+              acc[v].x = fmaf(ww[g], x[g][v].x, acc[v].x);
+              acc[v].y = fmaf(ww[g], x[g][v].y, acc[v].y);
+              acc[v].z = fmaf(ww[g], x[g][v].z, acc[v].z);
+              acc[v].w = fmaf(ww[g], x[g][v].w, acc[v].w);
             }
           }
         }
       }
+      dq_flush<VEC>(dpq, q, hid, h4, c0, lane, cur, (first && cur == u_before) || cur == u_after,
+                    acc);
     }
   }
 }
@@ -719,16 +762,17 @@ int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, co
                      int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int32_t* occ,
                      int32_t* occ_u, hipStream_t st) {
   PS_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)(N_max + 1) * sizeof(int), st));
-  hipLaunchKernelGGL(csr_count_kernel, dim3(grid_for(S_max * T, 256)), dim3(256), 0, st, loc, nS, T,
-                     cnt);
+  const int lds = (int)std::min<int64_t>(N_max, kLdsRows) * 4;
+  const int gb = std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
+  hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt);
   PS_CHECK_LAUNCH();
   const int nb = ceil_div(N_max + 1, kScanChunk);
   hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum);
   PS_CHECK_LAUNCH();
   hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum, off, cursor);
   PS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(csr_fill_kernel, dim3(grid_for(S_max * T, 256)), dim3(256), 0, st, loc, nS, T,
-                     cursor, occ, occ_u);
+  hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cursor, occ,
+                     occ_u);
   PS_CHECK_LAUNCH();
   return kOk;
 }

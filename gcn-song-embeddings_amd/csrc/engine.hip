@@ -27,7 +27,7 @@ int64_t bitset_words(int64_t universe);
 int64_t bitset_blocks(int64_t universe);
 int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
 int launch_mark_table(unsigned long long*, const int32_t*, const int*, int64_t, const int32_t*,
-                      int64_t, int, hipStream_t);
+                      int64_t, int, int64_t, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int launch_rank_list(const unsigned long long*, const uint32_t*, const int64_t*, int64_t, int32_t*,
@@ -155,12 +155,25 @@ static size_t carve(size_t& cur, int64_t bytes) {
 
 constexpr int kColsumBlocks = 32;  // row chunks of the bias-gradient column sums
 
-static int choose_splits(int64_t M, int64_t N, int64_t Kmax) {
-  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int64_t s = std::max<int64_t>(1, 512 / std::max<int64_t>(1, tiles));
-  s = std::min<int64_t>(s, std::max<int64_t>(1, Kmax / 256));
-  return (int)std::min<int64_t>(s, 64);
+// Split-K weight gradients (C[M][N] = A^T B over K data rows): pick the block
+// tile and split count so that tiles x splits fills the 256 CUs with >= 64 rows
+// per split; small outputs (128 x 128 head weights) fall back to 32 x 128 tiles.
+constexpr int kMaxSplits = 64;
+static void choose_wgrad(int64_t M, int64_t N, int64_t Kest, int* cfg, int* splits) {
+  static const int bm[3] = {128, 64, 32};
+  for (int c = 0; c < 3; ++c) {
+    const int64_t tiles = ((M + bm[c] - 1) / bm[c]) * ((N + 127) / 128);
+    int64_t s = std::max<int64_t>(1, 512 / tiles);
+    s = std::min<int64_t>(s, std::max<int64_t>(1, Kest / 64));
+    s = std::min<int64_t>(s, kMaxSplits);
+    if (tiles * s >= 256 || c == 2) {
+      *cfg = c;
+      *splits = (int)s;
+      return;
+    }
+  }
 }
+
 
 static void layout(Engine& E) {
   const EngineConfig& c = E.cfg;
@@ -240,13 +253,12 @@ static void layout(Engine& E) {
   E.scal = carve(cur, 64);
   E.err = carve(cur, 16);
   // split-K slabs: max over the weight-gradient GEMMs
-  int64_t slab = 0;
+  // split-K slabs: any split count up to kMaxSplits (it is chosen from size hints)
+  int64_t slab = kMaxSplits * c.out * c.out;
   for (auto& lb : E.L) {
-    slab = std::max(slab, (int64_t)choose_splits(c.hid, lb.d, lb.N.cap) * c.hid * lb.d);
-    slab = std::max(slab, (int64_t)choose_splits(c.out, lb.d + c.hid, lb.S.cap) * c.out *
-                              (lb.d + c.hid));
+    slab = std::max(slab, (int64_t)kMaxSplits * c.hid * lb.d);
+    slab = std::max(slab, (int64_t)kMaxSplits * c.out * std::max(lb.d, c.hid));
   }
-  slab = std::max(slab, (int64_t)choose_splits(c.out, c.out, top) * c.out * c.out);
   E.slab_floats = slab;
   E.slab = carve(cur, slab * 4);
   E.colpart = carve(cur, kColsumBlocks * std::max(c.hid, c.out) * 4);
@@ -285,7 +297,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
                              cnt(top.S), st));
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
-    PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, E.nb, E.ldT, T, st));
+    PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, E.nb, E.ldT, T, n, st));
     PS_TRY(launch_set_finalize(bits(lb.N), bits(lb.N), nullptr, n, bsum, pref(lb.N), mem(lb.N),
                                cnt(lb.N), st));
     if (l > 0) {
@@ -385,9 +397,11 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
 // weight gradient dst[M][N] (+ column offset) = A^T B over the device row count
 static int weight_grad(Engine& E, void* ws, const float* A, int64_t lda, int M, const float* B,
                        int64_t ldb, const int32_t* b_idx, int N, const int* K_dev, int64_t K_max,
-                       float* dst, int64_t ld_dst, hipStream_t st) {
-  const int S = choose_splits(M, N, K_max);
+                       int64_t K_hint, float* dst, int64_t ld_dst, hipStream_t st) {
+  int cfg = 0, S = 1;
+  choose_wgrad(M, N, K_hint > 0 ? std::min(K_hint, K_max) : K_max, &cfg, &S);
   GemmParams p;
+  p.cfg = cfg;
   p.M = M;
   p.N = N;
   p.K_dev = K_dev;
@@ -427,7 +441,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
   Timed t_hb(E, "bwd.head", st);
   // head: Z = H1 G2^T, H1 = lrelu(y G1^T + b1)
   PS_TRY(weight_grad(E, ws, at<float>(ws, E.dZ), o, o, at<float>(ws, E.H1), o, nullptr, o,
-                     cnt(top.S), top.S.cap, gr + E.pG2w, o, st));
+                     cnt(top.S), top.S.cap, top.S.hint, gr + E.pG2w, o, st));
   {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
@@ -447,7 +461,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     PS_TRY(launch_gemm(p, st));
   }
   PS_TRY(weight_grad(E, ws, at<float>(ws, E.dP1), o, o, at<float>(ws, top.y), o, nullptr, o,
-                     cnt(top.S), top.S.cap, gr + E.pG1w, o, st));
+                     cnt(top.S), top.S.cap, top.S.hint, gr + E.pG1w, o, st));
   PS_TRY(bias_grad(E, ws, at<float>(ws, E.dP1), o, cnt(top.S), gr + E.pG1b, st));
   {
     GemmParams p;  // dY_top = dP1 G1
@@ -477,9 +491,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
                                  o, cnt(lb.S), lb.S.cap, dp, st));
     // dW = dp^T [h_self || agg]
     PS_TRY(weight_grad(E, ws, dp, o, o, h, ldh, at<int32_t>(ws, lb.self_src), d, cnt(lb.S),
-                       lb.S.cap, gr + lb.pWw, d + hd, st));
+                       lb.S.cap, lb.S.hint, gr + lb.pWw, d + hd, st));
     PS_TRY(weight_grad(E, ws, dp, o, o, at<float>(ws, lb.agg), hd, nullptr, hd, cnt(lb.S), lb.S.cap,
-                       gr + lb.pWw + d, d + hd, st));
+                       lb.S.hint, gr + lb.pWw + d, d + hd, st));
     PS_TRY(bias_grad(E, ws, dp, o, cnt(lb.S), gr + lb.pWb, st));
     float* dYprev = l > 0 ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr;
     if (l > 0) {
@@ -527,7 +541,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     // dQ = dpq^T h[q_src]
     Timed tq(E, lname("bwd.q_wgrad", l), st);
     PS_TRY(weight_grad(E, ws, at<float>(ws, lb.dpq), hd, hd, h, ldh, at<int32_t>(ws, lb.q_src), d,
-                       cnt(lb.N), lb.N.cap, gr + lb.pQw, d, st));
+                       cnt(lb.N), lb.N.cap, lb.N.hint, gr + lb.pQw, d, st));
     PS_TRY(bias_grad(E, ws, at<float>(ws, lb.dpq), hd, cnt(lb.N), gr + lb.pQb, st));
     if (l > 0) {
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1

@@ -6,7 +6,11 @@
 // so no sort runs and ranks are O(1) lookups (bitmap + prefix stay in L2).
 #include "common.h"
 
+#include <algorithm>
+
 namespace ps {
+
+int64_t bitset_words(int64_t universe);
 
 constexpr int kScanBlock = 256;
 constexpr int kWordsPerThread = 4;
@@ -41,12 +45,32 @@ __global__ void bits_mark_i64_kernel(unsigned long long* __restrict__ bits,
   }
 }
 
-// mark nb_table[members[f]][t] for f < *count, t < T (table row stride ld)
-__global__ void bits_mark_table_kernel(unsigned long long* __restrict__ bits,
-                                       const int32_t* __restrict__ members,
-                                       const int* __restrict__ count, const int32_t* __restrict__ nb,
-                                       int64_t ld, int T) {
+// mark nb_table[members[f]][t] for f < *count, t < T (table row stride ld).
+// lds_words > 0: each block marks its contiguous slice into an LDS copy of the
+// bitmap and ORs the touched words into HBM once (popular ids repeat thousands
+// of times; global atomics on their words would serialise).
+__global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long long* __restrict__ bits,
+                                                               const int32_t* __restrict__ members,
+                                                               const int* __restrict__ count,
+                                                               const int32_t* __restrict__ nb,
+                                                               int64_t ld, int T, int lds_words) {
+  extern __shared__ unsigned long long lbits[];
   const int64_t n = (int64_t)(*count) * T;
+  if (lds_words > 0) {
+    for (int w = threadIdx.x; w < lds_words; w += blockDim.x) lbits[w] = 0ull;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(n, e0 + per);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      const int64_t f = e / T, t = e - f * T;
+      const int64_t v = nb[(int64_t)members[f] * ld + t];
+      atomicOr(lbits + (v >> 6), 1ull << (v & 63));
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < lds_words; w += blockDim.x)
+      if (lbits[w]) atomicOr(bits + w, lbits[w]);
+    return;
+  }
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = e / T, t = e - f * T;
@@ -180,10 +204,18 @@ int launch_mark_i64(unsigned long long* bits, const int64_t* ids, int64_t n, int
 }
 
 int launch_mark_table(unsigned long long* bits, const int32_t* members, const int* count,
-                      int64_t max_count, const int32_t* nb, int64_t ld, int T, hipStream_t st) {
+                      int64_t max_count, const int32_t* nb, int64_t ld, int T, int64_t universe,
+                      hipStream_t st) {
   if (max_count <= 0) return kOk;
-  hipLaunchKernelGGL(bits_mark_table_kernel, dim3(grid_for(max_count * T, 256)), dim3(256), 0, st,
-                     bits, members, count, nb, ld, T);
+  const int64_t nw = bitset_words(universe);
+  if (nw * 8 <= 64 * 1024) {
+    const int gb = std::max(1, std::min(64, ceil_div(max_count * T, 4096)));
+    hipLaunchKernelGGL(bits_mark_table_kernel, dim3(gb), dim3(1024), (size_t)nw * 8, st, bits,
+                       members, count, nb, ld, T, (int)nw);
+  } else {
+    hipLaunchKernelGGL(bits_mark_table_kernel, dim3(grid_for(max_count * T, 1024)), dim3(1024), 0,
+                       st, bits, members, count, nb, ld, T, 0);
+  }
   PS_CHECK_LAUNCH();
   return kOk;
 }

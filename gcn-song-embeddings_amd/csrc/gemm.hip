@@ -33,7 +33,9 @@ struct Shape {
   static constexpr int MV = R / 4;                // float4 per k-row (MN-major)
   static constexpr int TOT_MN = BK * MV;          // float4 per stage, MN-major
   static constexpr int NV = (TOT_K + 255) / 256;  // float4 per thread (same count both layouts)
-  static constexpr int W = R + PADF;              // floats per staged k-row
+  static constexpr int W = R + PADF;              // MN-major image: [BK][R + 4]
+  static constexpr int WK = BK + 4;               // K-major image:  [R][BK + 4]
+  static constexpr int SZ = (R * WK > BK * W) ? R * WK : BK * W;  // floats per stage
 };
 
 template <int R, int BK>
@@ -75,19 +77,18 @@ __device__ __forceinline__ void kmajor_load(float4 (&v)[(Shape<R, BK>::NV)],
     else v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
+// K-major stage image is row-major [R][BK+4]: one ds_write_b128 per float4, and
+// the fragment reader takes 4 consecutive k of a row with one ds_read_b128.
 template <int R, int BK>
-__device__ __forceinline__ void kmajor_store(float (*Sm)[(Shape<R, BK>::W)],
-                                             const float4 (&v)[(Shape<R, BK>::NV)], int tid) {
+__device__ __forceinline__ void kmajor_store(float* Sm, const float4 (&v)[(Shape<R, BK>::NV)],
+                                             int tid) {
   using S = Shape<R, BK>;
 #pragma unroll
   for (int i = 0; i < S::NV; ++i) {
     const int lin = tid + 256 * i;
     if (lin >= S::TOT_K) continue;
     const int row = lin / S::KV, kc = (lin % S::KV) * 4;
-    Sm[kc + 0][row] = v[i].x;
-    Sm[kc + 1][row] = v[i].y;
-    Sm[kc + 2][row] = v[i].z;
-    Sm[kc + 3][row] = v[i].w;
+    *reinterpret_cast<float4*>(Sm + row * S::WK + kc) = v[i];
   }
 }
 
@@ -112,16 +113,25 @@ __device__ __forceinline__ void mnmajor_load(float4 (&v)[(Shape<R, BK>::NV)], in
   }
 }
 template <int R, int BK>
-__device__ __forceinline__ void mnmajor_store(float (*Sm)[(Shape<R, BK>::W)],
-                                              const float4 (&v)[(Shape<R, BK>::NV)], int tid) {
+__device__ __forceinline__ void mnmajor_store(float* Sm, const float4 (&v)[(Shape<R, BK>::NV)],
+                                              int tid) {
   using S = Shape<R, BK>;
 #pragma unroll
   for (int i = 0; i < S::NV; ++i) {
     const int lin = tid + 256 * i;
     if (lin >= S::TOT_MN) continue;
     const int kr = lin / S::MV, cc = lin % S::MV;
-    *reinterpret_cast<float4*>(&Sm[kr][cc * 4]) = v[i];
+    *reinterpret_cast<float4*>(Sm + kr * S::W + cc * 4) = v[i];
   }
+}
+
+// 4 consecutive k (8s + 4h .. +3) of row `row` from a staged image
+template <bool KM, int R, int BK>
+__device__ __forceinline__ float4 frag4(const float* Sm, int row, int k4) {
+  using S = Shape<R, BK>;
+  if (KM) return *reinterpret_cast<const float4*>(Sm + row * S::WK + k4);
+  return make_float4(Sm[(k4 + 0) * S::W + row], Sm[(k4 + 1) * S::W + row],
+                     Sm[(k4 + 2) * S::W + row], Sm[(k4 + 3) * S::W + row]);
 }
 
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK.
@@ -130,8 +140,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   using SA = Shape<BM, BK>;
   using SB = Shape<BN, BK>;
-  __shared__ __attribute__((aligned(16))) float As[2][BK][SA::W];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][SB::W];
+  __shared__ __attribute__((aligned(16))) float As[2][SA::SZ];
+  __shared__ __attribute__((aligned(16))) float Bs[2][SB::SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int M = p.M_dev ? *p.M_dev : p.M;
@@ -183,43 +193,60 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float4 va[SA::NV], vb[SB::NV];
-    auto load = [&](int k0) {
+    // Two register stages: the global loads of tile t+2 are issued before the
+    // MFMAs of tile t and written to LDS after those of tile t+1, so two k-tiles
+    // of MFMA work cover the HBM latency of the (row-gathered) operand loads.
+    float4 va0[SA::NV], vb0[SB::NV], va1[SA::NV], vb1[SB::NV];
+    auto load = [&](float4 (&va)[SA::NV], float4 (&vb)[SB::NV], int k0) {
       if (AK) kmajor_load<BM, BK>(va, RA, tid, k0, ke, p.K1);
       else mnmajor_load<BM, BK>(va, tid, p.a, p.lda, p.a_idx, m0, M, k0, ke);
       if (BKM) kmajor_load<BN, BK>(vb, RB, tid, k0, ke, -1);
       else mnmajor_load<BN, BK>(vb, tid, p.b, p.ldb, p.b_idx, n0, N, k0, ke);
     };
-    auto store = [&](int buf) {
+    auto store = [&](const float4 (&va)[SA::NV], const float4 (&vb)[SB::NV], int buf) {
       if (AK) kmajor_store<BM, BK>(As[buf], va, tid);
       else mnmajor_store<BM, BK>(As[buf], va, tid);
       if (BKM) kmajor_store<BN, BK>(Bs[buf], vb, tid);
       else mnmajor_store<BN, BK>(Bs[buf], vb, tid);
     };
-    if (nk > 0) {
-      load(kb);
-      store(0);
-    }
-    __syncthreads();
     const int h = lane >> 5, l32 = lane & 31;
-    for (int it = 0; it < nk; ++it) {
-      const int cur = it & 1;
-      if (it + 1 < nk) load(kb + (it + 1) * BK);
+    // MFMA k-assignment: in the r-th MFMA of octet s, lane half h supplies
+    // k = 8s + 4h + r for both operands (any bijection onto the 8 k works).
+    auto compute = [&](int cur) {
 #pragma unroll
-      for (int kk = 0; kk < BK / 2; ++kk) {
-        const int k = 2 * kk + h;
-        float a[TM], b[TN];
+      for (int s8 = 0; s8 < BK / 8; ++s8) {
+        const int k4 = 8 * s8 + 4 * h;
+        float4 a[TM], b[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = As[cur][k][(wm * TM + i) * 32 + l32];
+        for (int i = 0; i < TM; ++i) a[i] = frag4<AK, BM, BK>(As[cur], (wm * TM + i) * 32 + l32, k4);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][k][(wn * TN + j) * 32 + l32];
+        for (int j = 0; j < TN; ++j) b[j] = frag4<BKM, BN, BK>(Bs[cur], (wn * TN + j) * 32 + l32, k4);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+          }
       }
-      if (it + 1 < nk) store(cur ^ 1);
+    };
+    if (nk > 0) {
+      load(va0, vb0, kb);
+      store(va0, vb0, 0);
+    }
+    if (nk > 1) load(va1, vb1, kb + BK);
+    __syncthreads();
+    for (int it = 0; it < nk; it += 2) {
+      if (it + 2 < nk) load(va0, vb0, kb + (it + 2) * BK);
+      compute(0);
+      if (it + 1 < nk) store(va1, vb1, 1);
+      __syncthreads();
+      if (it + 1 >= nk) break;
+      if (it + 3 < nk) load(va1, vb1, kb + (it + 3) * BK);
+      compute(1);
+      if (it + 2 < nk) store(va0, vb0, 0);
       __syncthreads();
     }
 
@@ -240,7 +267,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
           }
         }
     } else if (p.epi == kEpiL2Norm) {
-      float* red = &As[0][0][0];  // [WN][BM] row partial sums (LDS free after the k loop)
+      float* red = &As[0][0];  // [WN][BM] row partial sums (LDS free after the k loop)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
