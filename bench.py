@@ -187,9 +187,15 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
+        t_sample = t_enqueue = 0.0
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            loss = step()[0]
+            ta = time.perf_counter()
+            batch, _ = tr.next_batch()
+            tb = time.perf_counter()
+            loss = tr.train_batch(batch)[0]
+            t_sample += tb - ta
+            t_enqueue += time.perf_counter() - tb
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -258,6 +264,8 @@ def main():
                           "achieved_GBs": agg_bytes / (a_avg * 1e-3) / 1e9 if a_avg > 0 else 0.0,
                           "peak_GBs": PEAK_HBM_GBS, "algorithmic_bytes": agg_bytes},
         "frontier": {"U0_mean": U0, "F0_mean": F0},
+        "host_ms_per_step": {"sample_batch": t_sample / args.steps * 1e3,
+                             "train_batch_enqueue": t_enqueue / args.steps * 1e3},
         "precompute": {"seconds": t_pre, "rng": args.precompute_rng, "hops_per_s": hops / t_pre},
         "kernels": kernels,
         "cpu_baseline": None,

@@ -33,7 +33,7 @@ class EngineConfig(ctypes.Structure):
 
 class EngineOffsets(ctypes.Structure):
     _fields_ = [("ids", i64), ("pos_rank", i64), ("z", i64), ("dz", i64), ("scalars", i64),
-                ("err", i64), ("n_layers", i64), ("count_S", i64 * 8), ("count_N", i64 * 8),
+                ("n_layers", i64), ("count_S", i64 * 8), ("count_N", i64 * 8),
                 ("members_S", i64 * 8), ("members_N", i64 * 8), ("cap_S", i64 * 8),
                 ("cap_N", i64 * 8), ("y", i64 * 8), ("param_offsets", i64 * 8)]
 
@@ -50,7 +50,10 @@ _SIGS = {
     "pinsage_mt_skip": (ctypes.c_int, [vp, i64]),
     "pinsage_mt_draws": (ctypes.c_int, [vp, vp, i64]),
     "pinsage_mt_randperm_prefix": (ctypes.c_int, [vp, i64, i64, vp]),
-    "pinsage_sample_batch_easy": (ctypes.c_int, [vp, vp, i64, i64, i64, vp]),
+    "pinsage_sample_batch_easy": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, vp, vp]),
+    "pinsage_batch_sampler_create": (ctypes.c_int, [vp, i64, i64, i64, vp]),
+    "pinsage_batch_sampler_destroy": (None, [vp]),
+    "pinsage_batch_sampler_next": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp, ctypes.c_int]),
     "pinsage_walk_mt_workspace": (i64, [i64, i64]),
     "pinsage_walk_mt": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, vp, vp, i64, vp, vp]),
     "pinsage_walk_philox": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, u64, u32, i64, vp, vp]),
@@ -64,6 +67,7 @@ _SIGS = {
     "pinsage_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(vp)]),
     "pinsage_engine_destroy": (None, [vp]),
     "pinsage_engine_workspace_bytes": (i64, [vp]),
+    "pinsage_engine_init_workspace": (i32, [vp, vp, vp]),
     "pinsage_engine_num_params": (i64, [vp]),
     "pinsage_engine_offsets": (ctypes.c_int, [vp, ctypes.POINTER(EngineOffsets)]),
     "pinsage_engine_set_tensors": (ctypes.c_int, [vp, vp, i64, vp, vp, i64, vp, vp, vp, vp]),
@@ -150,10 +154,21 @@ class MT:
         check(lib().pinsage_mt_from_torch(g.p, st.ctypes.data_as(vp), st.nbytes), "mt_from_torch")
         return g
 
-    def to_torch(self):
-        st = torch.get_rng_state().numpy().copy()
+    @classmethod
+    def from_state(cls, st):
+        """From a torch.get_rng_state() byte array (numpy uint8)."""
+        g = cls()
+        check(lib().pinsage_mt_from_torch(g.p, st.ctypes.data_as(vp), st.nbytes), "mt_from_torch")
+        return g
+
+    def to_state(self, st):
+        """A copy of the torch state bytes st with this generator written in."""
+        st = st.copy()
         check(lib().pinsage_mt_to_torch(self.p, st.ctypes.data_as(vp), st.nbytes), "mt_to_torch")
-        torch.set_rng_state(torch.from_numpy(st))
+        return st
+
+    def to_torch(self):
+        torch.set_rng_state(torch.from_numpy(self.to_state(torch.get_rng_state().numpy())))
 
     def seed(self, s):
         lib().pinsage_mt_seed(self.p, s)

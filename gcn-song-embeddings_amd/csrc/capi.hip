@@ -4,7 +4,6 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/pinsage_hip.h"
@@ -36,23 +35,91 @@ int launch_agg(const float*, int, const int32_t*, const float*, int, const int*,
                hipStream_t);
 
 // Fisher-Yates prefix of torch.randperm(n): first k entries, all n-1 draws consumed.
+// Only the <= 2k positions the first k swaps touch are stored (open addressing).
 static void randperm_prefix(MTState& g, int64_t n, int64_t k, int64_t* out) {
   k = std::min(k, n);
-  std::unordered_map<int64_t, int64_t> sw;
-  sw.reserve((size_t)(2 * k + 16));
-  auto get = [&](int64_t i) {
-    auto it = sw.find(i);
-    return it == sw.end() ? i : it->second;
-  };
   const int64_t steps = std::min(k, n - 1);
+  int lg = 4;
+  while ((int64_t(1) << lg) < 4 * steps + 16) ++lg;
+  const size_t mask = (size_t(1) << lg) - 1;
+  std::vector<int64_t> keys(mask + 1, -1), vals(mask + 1);
+  auto slot = [&](int64_t i) {
+    size_t h = (size_t)(((uint64_t)i * 0x9E3779B97F4A7C15ull) >> (64 - lg));
+    while (keys[h] != -1 && keys[h] != i) h = (h + 1) & mask;
+    return h;
+  };
+  auto get = [&](int64_t i) {
+    const size_t h = slot(i);
+    return keys[h] == i ? vals[h] : i;
+  };
+  auto put = [&](int64_t i, int64_t v) {
+    const size_t h = slot(i);
+    keys[h] = i;
+    vals[h] = v;
+  };
   for (int64_t i = 0; i < steps; ++i) {
     const int64_t z = (int64_t)(g.draw() % (uint64_t)(n - i));
     const int64_t a = get(i), b = get(i + z);
-    sw[i] = b;
-    sw[i + z] = a;
+    put(i, b);
+    put(i + z, a);
   }
   for (int64_t i = 0; i < k; ++i) out[i] = get(i);
   if (n - 1 > steps) g.skip(n - 1 - steps);
+}
+
+// sample_batch with easy negatives (pinsage_training.py:53-77, 89-97); shared
+// with the batch sampler runtime (loader.hip)
+int sample_batch_easy(MTState& g, const int64_t* positives, int64_t P, int64_t n_items,
+                      int64_t batch_size, int64_t* batch_out, int64_t* nodeset_out,
+                      int64_t* n_nodeset) {
+  const int64_t B = std::min(batch_size, P);
+  std::vector<int64_t> sel((size_t)B);
+  randperm_prefix(g, P, B, sel.data());
+  std::vector<int64_t> mem;
+  mem.reserve((size_t)(2 * B));
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t a = positives[2 * sel[(size_t)b]], p = positives[2 * sel[(size_t)b] + 1];
+    if (a < 0 || a >= n_items || p < 0 || p >= n_items) {
+      set_error("sample_batch: positive pair id out of range");
+      return kErrIndex;
+    }
+    batch_out[3 * b] = a;
+    batch_out[3 * b + 1] = p;
+    mem.push_back(a);
+    mem.push_back(p);
+  }
+  std::sort(mem.begin(), mem.end());
+  mem.erase(std::unique(mem.begin(), mem.end()), mem.end());
+  const int64_t m = n_items - (int64_t)mem.size();
+  std::vector<int64_t> r((size_t)B);
+  randperm_prefix(g, m, B, r.data());
+  const int64_t nneg = std::min(B, m);
+  for (int64_t b = 0; b < B; ++b) {
+    if (b >= nneg) {
+      // the reference's torch.cat fails when fewer negatives than pairs exist
+      set_error("sample_batch: fewer candidate negatives than pairs");
+      return kErrArg;
+    }
+    // r[b]-th smallest id not in mem
+    const int64_t want = r[(size_t)b];
+    int64_t v = want, c = 0;
+    for (;;) {
+      const int64_t c2 = std::upper_bound(mem.begin(), mem.end(), v) - mem.begin();
+      if (c2 == c) break;
+      c = c2;
+      v = want + c;
+    }
+    batch_out[3 * b + 2] = v;
+  }
+  if (nodeset_out) {  // batch.flatten().unique(): sorted union of mem and the negatives
+    std::vector<int64_t> neg((size_t)B);
+    for (int64_t b = 0; b < B; ++b) neg[(size_t)b] = batch_out[3 * b + 2];
+    std::sort(neg.begin(), neg.end());
+    neg.erase(std::unique(neg.begin(), neg.end()), neg.end());
+    int64_t* e = std::set_union(mem.begin(), mem.end(), neg.begin(), neg.end(), nodeset_out);
+    if (n_nodeset) *n_nodeset = (int64_t)(e - nodeset_out);
+  }
+  return kOk;
 }
 
 }  // namespace ps
@@ -109,48 +176,10 @@ int pinsage_mt_randperm_prefix(void* mt, int64_t n, int64_t k, int64_t* out) {
 }
 
 int pinsage_sample_batch_easy(void* mt, const int64_t* positives, int64_t P, int64_t n_items,
-                              int64_t batch_size, int64_t* batch_out) {
-  MTState& g = *reinterpret_cast<MTState*>(mt);
-  const int64_t B = std::min(batch_size, P);
-  std::vector<int64_t> sel((size_t)B);
-  randperm_prefix(g, P, B, sel.data());
-  std::vector<int64_t> mem;
-  mem.reserve((size_t)(2 * B));
-  for (int64_t b = 0; b < B; ++b) {
-    const int64_t a = positives[2 * sel[(size_t)b]], p = positives[2 * sel[(size_t)b] + 1];
-    if (a < 0 || a >= n_items || p < 0 || p >= n_items) {
-      set_error("sample_batch: positive pair id out of range");
-      return kErrIndex;
-    }
-    batch_out[3 * b] = a;
-    batch_out[3 * b + 1] = p;
-    mem.push_back(a);
-    mem.push_back(p);
-  }
-  std::sort(mem.begin(), mem.end());
-  mem.erase(std::unique(mem.begin(), mem.end()), mem.end());
-  const int64_t m = n_items - (int64_t)mem.size();
-  std::vector<int64_t> r((size_t)B);
-  randperm_prefix(g, m, B, r.data());
-  const int64_t nneg = std::min(B, m);
-  for (int64_t b = 0; b < B; ++b) {
-    if (b >= nneg) {
-      // the reference's torch.cat fails when fewer negatives than pairs exist
-      set_error("sample_batch: fewer candidate negatives than pairs");
-      return kErrArg;
-    }
-    // r[b]-th smallest id not in mem
-    const int64_t want = r[(size_t)b];
-    int64_t v = want, c = 0;
-    for (;;) {
-      const int64_t c2 = std::upper_bound(mem.begin(), mem.end(), v) - mem.begin();
-      if (c2 == c) break;
-      c = c2;
-      v = want + c;
-    }
-    batch_out[3 * b + 2] = v;
-  }
-  return kOk;
+                              int64_t batch_size, int64_t* batch_out, int64_t* nodeset_out,
+                              int64_t* n_nodeset) {
+  return sample_batch_easy(*reinterpret_cast<MTState*>(mt), positives, P, n_items, batch_size,
+                           batch_out, nodeset_out, n_nodeset);
 }
 
 // ------------------------------------------------------------------ walks

@@ -37,9 +37,13 @@ __global__ void layer_prep_kernel(const int32_t* __restrict__ S_mem, const int* 
                                   const int32_t* __restrict__ nb, const float* __restrict__ wn,
                                   int64_t ldT, int T, int32_t* __restrict__ self_src,
                                   int32_t* __restrict__ q_src, int32_t* __restrict__ loc,
-                                  float* __restrict__ wloc) {
+                                  float* __restrict__ wloc,
+                                  const unsigned long long* __restrict__ S_bits,
+                                  const uint32_t* __restrict__ S_pref,
+                                  const int64_t* __restrict__ ids, int64_t n_ids,
+                                  int32_t* __restrict__ pos_rank) {
   const int64_t FS = (int64_t)(*nS), FN = (int64_t)(*nN);
-  const int64_t total = FS * T + FS + FN;
+  const int64_t total = FS * T + FS + FN + n_ids;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < FS * T) {
@@ -52,10 +56,14 @@ __global__ void layer_prep_kernel(const int32_t* __restrict__ S_mem, const int* 
       const int64_t f = e - FS * T;
       const int64_t id = S_mem[f];
       self_src[f] = P_bits ? rank_in(P_bits, P_pref, id) : (int32_t)id;
-    } else {
+    } else if (e < FS * T + FS + FN) {
       const int64_t u = e - FS * T - FS;
       const int64_t id = N_mem[u];
       q_src[u] = P_bits ? rank_in(P_bits, P_pref, id) : (int32_t)id;
+    } else {
+      // batch position -> row of the top-layer set (duplicates share a row)
+      const int64_t i = e - FS * T - FS - FN;
+      pos_rank[i] = rank_in(S_bits, S_pref, ids[i]);
     }
   }
 }
@@ -116,10 +124,18 @@ constexpr int kLdsRows = 16384;
 __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restrict__ loc,
                                                          const int* __restrict__ nS, int T,
                                                          const int* __restrict__ nN,
-                                                         int* __restrict__ cnt) {
+                                                         int* __restrict__ cnt,
+                                                         float* __restrict__ zero_rows, int zero_n) {
   extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
   const int U = *nN;
+  if (zero_rows) {  // the dq output receives atomics at chunk boundaries
+    float4* z4 = reinterpret_cast<float4*>(zero_rows);
+    const int64_t tot = (int64_t)U * zero_n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
+         i += (int64_t)gridDim.x * blockDim.x)
+      z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (U <= kLdsRows) {
     for (int u = threadIdx.x; u < U; u += blockDim.x) hist[u] = 0;
     __syncthreads();
@@ -164,7 +180,7 @@ __global__ __launch_bounds__(kScanB) void scan_block_sums_kernel(const int* __re
   __syncthreads();
   if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
-__global__ __launch_bounds__(kScanB) void scan_apply_kernel(const int* __restrict__ cnt,
+__global__ __launch_bounds__(kScanB) void scan_apply_kernel(int* __restrict__ cnt,
                                                             const int* __restrict__ n_dev,
                                                             const int* __restrict__ bsum,
                                                             int* __restrict__ off,
@@ -203,11 +219,48 @@ __global__ __launch_bounds__(kScanB) void scan_apply_kernel(const int* __restric
     if (i0 + q < n) {
       off[i0 + q] = p;
       cursor[i0 + q] = p;
+      ((int*)cnt)[i0 + q] = 0;
     }
     if (i0 + q == n) off[n] = p;
     p += v[q];
   }
 }
+// exclusive scan of cnt[0..U) into off[0..U] and cursor, zeroing cnt behind the
+// read (self-cleaning for the next step); one block, U <= 1024 * 64
+__global__ __launch_bounds__(1024) void scan_small_kernel(int* __restrict__ cnt,
+                                                          const int* __restrict__ n_dev,
+                                                          int* __restrict__ off,
+                                                          int* __restrict__ cursor) {
+  __shared__ int wsum[16];
+  const int U = *n_dev;
+  const int per = (U + 1023) / 1024;
+  const int i0 = threadIdx.x * per;
+  int c = 0;
+  for (int q = 0; q < per; ++q)
+    if (i0 + q < U) c += cnt[i0 + q];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int p = inc - c;
+  for (int i = 0; i < wv; ++i) p += wsum[i];
+  for (int q = 0; q < per; ++q) {
+    const int i = i0 + q;
+    if (i < U) {
+      const int v = cnt[i];
+      off[i] = p;
+      cursor[i] = p;
+      cnt[i] = 0;
+      p += v;
+    }
+  }
+  if (threadIdx.x == 1023) off[U] = p;
+}
+
 __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restrict__ loc,
                                                         const int* __restrict__ nS, int T,
                                                         const int* __restrict__ nN,
@@ -269,14 +322,6 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
 // each partial (it is a per-element factor).
 constexpr int kSegChunk = 32;
 
-// zero rows [0, *nrows) of a [rows][n] buffer (device-side row count)
-__global__ void zero_rows_kernel(float* __restrict__ x, int64_t n, const int* __restrict__ nrows) {
-  const int64_t total = (int64_t)(*nrows) * n / 4;
-  float4* x4 = reinterpret_cast<float4*>(x);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x)
-    x4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
 template <int VEC>
 __device__ __forceinline__ void dq_flush(float* __restrict__ dpq, const float* __restrict__ q, int hid,
                                          int h4, int c0, int lane, int32_t row, bool atom,
@@ -377,11 +422,25 @@ __global__ __launch_bounds__(256) void dq_segment_kernel(
 
 // ---------------------------------------------------------------- L2 norm + lrelu backward
 // y = lrelu(p) / ||lrelu(p)||:  dp = lrelu'(y) * (dy - y (y . dy)) / ||.||
+// Also zeroes (a) rows [0, *z_rows) x z_n of z (the previous layer's dY,
+// about to receive scatter-adds) and (b) zi[0, zi_n) (multiplicity counters of
+// the loss, consumed by now) -- work that would otherwise be memset launches.
 __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __restrict__ y,
                                                              const float* __restrict__ nrm,
                                                              const float* __restrict__ dy, int n,
                                                              const int* __restrict__ nrows,
-                                                             float* __restrict__ dp) {
+                                                             float* __restrict__ dp,
+                                                             float* __restrict__ z, int z_n,
+                                                             const int* __restrict__ z_rows,
+                                                             int* __restrict__ zi, int64_t zi_n) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  if (z) {
+    const int64_t zn = (int64_t)(*z_rows) * z_n;
+    for (int64_t i = gt; i < zn; i += gs) z[i] = 0.f;
+  }
+  if (zi)
+    for (int64_t i = gt; i < zi_n; i += gs) zi[i] = 0;
   const int64_t R = *nrows;
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -398,55 +457,6 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
   }
 }
 
-// ---------------------------------------------------------------- column sums (bias grads)
-// partial[g][c] = sum over row chunk g of X[:, c]: grid (ceil(n/64), G), block
-// 256 = 64 columns x 4 row lanes; reduced later in a fixed order, so the
-// result is deterministic.
-constexpr int kColChunks = 32;
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ X, int n,
-                                                             int64_t ld, const int* __restrict__ nrows_dev,
-                                                             int nrows_host,
-                                                             float* __restrict__ partial) {
-  __shared__ float red[4][64];
-  const int64_t R = nrows_dev ? *nrows_dev : nrows_host;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ty = threadIdx.x >> 6;
-  const int G = gridDim.y;
-  const int64_t rows_per = (R + G - 1) / G;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
-  float s0 = 0.f, s1 = 0.f;
-  if (c < n) {
-    int64_t r = r0 + ty;
-    for (; r + 4 < r1; r += 8) {
-      s0 += X[r * ld + c];
-      s1 += X[(r + 4) * ld + c];
-    }
-    for (; r < r1; r += 4) s0 += X[r * ld + c];
-  }
-  red[ty][threadIdx.x & 63] = s0 + s1;
-  __syncthreads();
-  if (ty == 0 && c < n)
-    partial[(int64_t)blockIdx.y * n + c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
-                                           (red[2][threadIdx.x] + red[3][threadIdx.x]);
-}
-
-// out[i] = sum_s part[s * stride + i]  (fixed order)
-__global__ void reduce_slabs_kernel(const float* __restrict__ part, int S, int64_t stride,
-                                    int64_t len, float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int k = 0;
-    for (; k + 3 < S; k += 4) {
-      s0 += part[k * stride + i];
-      s1 += part[(k + 1) * stride + i];
-      s2 += part[(k + 2) * stride + i];
-      s3 += part[(k + 3) * stride + i];
-    }
-    for (; k < S; ++k) s0 += part[k * stride + i];
-    out[i] = (s0 + s1) + (s2 + s3);
-  }
-}
 
 // ---------------------------------------------------------------- loss
 // One wave per triple b: rows rq, rp, rn of Z (head outputs of the unique top
@@ -563,14 +573,19 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
   }
 }
 
-// dZ[r] = sum_c K[c][r] * G[c][r];  block 0 also reduces the per-block loss
-// partials (fixed order) into scal[0] = loss, scal[1] = node-feature loss.
-__global__ __launch_bounds__(256) void loss_finish_kernel(const float* __restrict__ G,
+// dZ[r] = sum_c K[c][r] * G[c][r], and G is zeroed behind the read so the next
+// step's atomics start from zero without a memset (Kc is zeroed by the first
+// backward kernel).  Block 0 also reduces, in a fixed order, the per-block loss
+// partials into scal[0] = loss, scal[1] = node-feature loss, and the variance
+// monitor (pinsage_training.py:99-103): sum((h - mean)^2)/(B-1) over the B query
+// rows = (sum |h|^2 - B |mean|^2)/(B-1), from per-block column sums.
+__global__ __launch_bounds__(256) void loss_finish_kernel(float* __restrict__ G,
                                                           const int* __restrict__ Kc, int64_t S_max,
                                                           const int* __restrict__ nS, int d,
                                                           float* __restrict__ dZ,
                                                           const float* __restrict__ part, int nparts,
-                                                          int B, float* __restrict__ scal) {
+                                                          const float* __restrict__ colpart, int B,
+                                                          float* __restrict__ scal) {
   const int64_t S = *nS;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -578,39 +593,24 @@ __global__ __launch_bounds__(256) void loss_finish_kernel(const float* __restric
     float v = 0.f;
     for (int c = 0; c < 3; ++c) {
       const int k = Kc[c * S_max + r];
-      if (k) v += (float)k * G[c * S_max * d + e];
+      if (k) {
+        v += (float)k * G[c * S_max * d + e];
+        G[c * S_max * d + e] = 0.f;
+      }
     }
     dZ[e] = v;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float l = 0.f, nf = 0.f, sq = 0.f;
-    for (int i = 0; i < nparts; ++i) {
-      l += part[i * 4 + 0];
-      nf += part[i * 4 + 1];
-      sq += part[i * 4 + 2];
-    }
-    scal[0] = l / (float)B;
-    scal[1] = nf / (float)B;
-    scal[2] = sq;
-  }
-}
-
-// batch_variance of h_q (pinsage_training.py:99-103): sum((h - mean)^2)/(B-1)
-// over the B query rows (duplicates included) = (sum |h|^2 - B |mean|^2)/(B-1),
-// from the loss kernel's per-block column sums and sum of squares (scal[2]).
-__global__ __launch_bounds__(256) void variance_finish_kernel(const float* __restrict__ colpart,
-                                                              int nparts, int d, int B,
-                                                              float* __restrict__ scal) {
+  if (blockIdx.x != 0) return;
   __shared__ float red[4];
-  __shared__ float cs[4][128];
+  __shared__ float cs[4][64];
   float acc = 0.f;
   const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
   for (int c0 = 0; c0 < d; c0 += 64) {
     const int c = c0 + l;
-    float s = 0.f;
+    float sc = 0.f;
     if (c < d)
-      for (int g = q; g < nparts; g += 4) s += colpart[(int64_t)g * d + c];
-    cs[q][l] = s;
+      for (int g = q; g < nparts; g += 4) sc += colpart[(int64_t)g * d + c];
+    cs[q][l] = sc;
     __syncthreads();
     if (q == 0 && c < d) {
       const float m = ((cs[0][l] + cs[1][l]) + (cs[2][l] + cs[3][l])) / (float)B;
@@ -622,8 +622,17 @@ __global__ __launch_bounds__(256) void variance_finish_kernel(const float* __res
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
+    float lsum = 0.f, nf = 0.f, sq = 0.f;
+    for (int i = 0; i < nparts; ++i) {
+      lsum += part[i * 4 + 0];
+      nf += part[i * 4 + 1];
+      sq += part[i * 4 + 2];
+    }
+    scal[0] = lsum / (float)B;
+    scal[1] = nf / (float)B;
+    scal[2] = sq;
     const float msq = red[0] + red[1] + red[2] + red[3];
-    scal[3] = (scal[2] - (float)B * msq) / (float)(B - 1);
+    scal[3] = (sq - (float)B * msq) / (float)(B - 1);
   }
 }
 
@@ -631,13 +640,16 @@ __global__ __launch_bounds__(256) void variance_finish_kernel(const float* __res
 // torch.optim.Adam (single-tensor math, weight_decay 0, amsgrad off):
 //   m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
-// lr comes from device memory (the scheduler updates it), the step counter is
-// bumped by loss_finish, so the whole train step can be graph-replayed.
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
-                            float* __restrict__ m, float* __restrict__ v, int64_t n,
-                            const float* __restrict__ lr_dev, const int* __restrict__ step_dev,
-                            float beta1, float beta2, float eps) {
-  const double step = (double)(*step_dev);
+// lr and the step counter live in device memory, so the step can be
+// graph-replayed: every block computes with step[0] + 1, and the last block to
+// take a ticket (step[1]) stores it -- every block has read step[0] by then.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int64_t n, const float* __restrict__ lr_dev,
+                                                   int* __restrict__ step_dev, float beta1,
+                                                   float beta2, float eps) {
+  const int new_step = step_dev[0] + 1;
+  const double step = (double)new_step;
   const double lr = (double)(*lr_dev);
   const double bc1 = 1.0 - pow((double)beta1, step);
   const double bc2s = sqrt(1.0 - pow((double)beta2, step));
@@ -655,9 +667,15 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
     const float denom = sqrtf(vi) / bc2f + eps;
     p[i] = p[i] - step_size * (mi / denom);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = atomicAdd(step_dev + 1, 1);
+    if (t == (int)gridDim.x - 1) {
+      step_dev[0] = new_step;
+      step_dev[1] = 0;
+    }
+  }
 }
-
-__global__ void step_incr_kernel(int* step) { *step += 1; }
 
 // out[i][:] = Z[pos_rank[i]][:]
 __global__ void gather_out_kernel(const float* __restrict__ Z, int d, const int32_t* __restrict__ pr,
@@ -684,13 +702,29 @@ __global__ void dz_scale_kernel(const float* __restrict__ G, const int* __restri
                                 const int* __restrict__ nS, float* __restrict__ dZ) {
   const int64_t S = *nS;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
-       e += (int64_t)gridDim.x * blockDim.x)
+       e += (int64_t)gridDim.x * blockDim.x) {
     dZ[e] = (float)Kc[e / d] * G[e];
+    ((float*)G)[e] = 0.f;
+  }
 }
 
-// out[m*ld + n] = sum_s part[s*stride + m*N + n]
+// out[m*ld + n] = sum_s part[s*stride + m*N + n]; bias_out[m] = sum_s bpart[s*M + m]
 __global__ void reduce_slabs_2d_kernel(const float* __restrict__ part, int S, int64_t stride, int M,
-                                       int N, float* __restrict__ out, int64_t ld) {
+                                       int N, float* __restrict__ out, int64_t ld,
+                                       const float* __restrict__ bpart, float* __restrict__ bias_out) {
+  if (bias_out) {
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M;
+         m += (int64_t)gridDim.x * blockDim.x) {
+      float s0 = 0.f, s1 = 0.f;
+      int k = 0;
+      for (; k + 1 < S; k += 2) {
+        s0 += bpart[(int64_t)k * M + m];
+        s1 += bpart[(int64_t)(k + 1) * M + m];
+      }
+      if (k < S) s0 += bpart[(int64_t)k * M + m];
+      bias_out[m] = s0 + s1;
+    }
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)M * N;
        i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
@@ -712,8 +746,6 @@ int launch_gather_out(const float* Z, int d, const int32_t* pr, int64_t n, float
 
 int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, const int* nS,
                         int64_t S_max, float* G, int* Kc, float* dZ, hipStream_t st) {
-  PS_CHECK_HIP(hipMemsetAsync(G, 0, (size_t)(S_max * d) * sizeof(float), st));
-  PS_CHECK_HIP(hipMemsetAsync(Kc, 0, (size_t)S_max * sizeof(int), st));
   hipLaunchKernelGGL(dout_accum_kernel, dim3(grid_for(n * d, 256)), dim3(256), 0, st, dout, d, pr, n,
                      G, Kc);
   PS_CHECK_LAUNCH();
@@ -724,9 +756,9 @@ int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, 
 }
 
 int launch_reduce_slabs_2d(const float* part, int S, int64_t stride, int M, int N, float* out,
-                           int64_t ld, hipStream_t st) {
+                           int64_t ld, const float* bpart, float* bias_out, hipStream_t st) {
   hipLaunchKernelGGL(reduce_slabs_2d_kernel, dim3(grid_for((int64_t)M * N, 256, 1024)), dim3(256), 0,
-                     st, part, S, stride, M, N, out, ld);
+                     st, part, S, stride, M, N, out, ld, bpart, bias_out);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -735,10 +767,12 @@ int launch_layer_prep(const int32_t* S_mem, const int* nS, int64_t S_max, const 
                       const uint32_t* N_pref, const unsigned long long* P_bits,
                       const uint32_t* P_pref, const int32_t* nb, const float* wn, int64_t ldT,
                       int T, int32_t* self_src, int32_t* q_src, int32_t* loc, float* wloc,
-                      hipStream_t st) {
-  const int64_t tot = S_max * T + S_max + N_max;
+                      const unsigned long long* S_bits, const uint32_t* S_pref, const int64_t* ids,
+                      int64_t n_ids, int32_t* pos_rank, hipStream_t st) {
+  const int64_t tot = S_max * T + S_max + N_max + n_ids;
   hipLaunchKernelGGL(layer_prep_kernel, dim3(grid_for(tot, 256)), dim3(256), 0, st, S_mem, nS, N_mem,
-                     nN, N_bits, N_pref, P_bits, P_pref, nb, wn, ldT, T, self_src, q_src, loc, wloc);
+                     nN, N_bits, N_pref, P_bits, P_pref, nb, wn, ldT, T, self_src, q_src, loc, wloc,
+                     S_bits, S_pref, ids, n_ids, pos_rank);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -758,19 +792,26 @@ int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, i
   return kOk;
 }
 
+// CSR of the neighbour slots by q row.  cnt must be zero on entry (zeroed once
+// by pinsage_engine_init_workspace, then left zero by the scan).  The count
+// kernel also zeroes dpq's rows (the dq kernel's atomic targets).
 int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, const int* nN,
                      int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int32_t* occ,
-                     int32_t* occ_u, hipStream_t st) {
-  PS_CHECK_HIP(hipMemsetAsync(cnt, 0, (size_t)(N_max + 1) * sizeof(int), st));
+                     int32_t* occ_u, float* dpq, int hid, hipStream_t st) {
   const int lds = (int)std::min<int64_t>(N_max, kLdsRows) * 4;
   const int gb = std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
-  hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt);
+  hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt, dpq, hid);
   PS_CHECK_LAUNCH();
-  const int nb = ceil_div(N_max + 1, kScanChunk);
-  hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum);
-  PS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum, off, cursor);
-  PS_CHECK_LAUNCH();
+  if (N_max <= 1024 * 64) {
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor);
+    PS_CHECK_LAUNCH();
+  } else {
+    const int nb = ceil_div(N_max + 1, kScanChunk);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum);
+    PS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum, off, cursor);
+    PS_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cursor, occ,
                      occ_u);
   PS_CHECK_LAUNCH();
@@ -781,9 +822,6 @@ int launch_dq_segment(const int32_t* occ, const int32_t* occ_u, const float* wlo
                       const float* dagg, int64_t ld_dagg, const float* q, int hid, const int* nS,
                       int64_t S_max, const int* nN, int64_t N_max, float* dpq, hipStream_t st) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq_segment: hidden dim must be a multiple of 4");
-  hipLaunchKernelGGL(zero_rows_kernel, dim3(grid_for(N_max * hid / 4, 256, 2048)), dim3(256), 0, st,
-                     dpq, (int64_t)hid, nN);
-  PS_CHECK_LAUNCH();
   const int64_t chunks = (S_max * T + kSegChunk - 1) / kSegChunk;
   const int grid = grid_for(chunks * 64, 256, 4096);
   if (hid >= 512)
@@ -797,25 +835,10 @@ int launch_dq_segment(const int32_t* occ, const int32_t* occ_u, const float* wlo
 }
 
 int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int n,
-                          const int* nrows, int64_t max_rows, float* dp, hipStream_t st) {
+                          const int* nrows, int64_t max_rows, float* dp, float* z, int z_n,
+                          const int* z_rows, int* zi, int64_t zi_n, hipStream_t st) {
   hipLaunchKernelGGL(norm_lrelu_bwd_kernel, dim3(grid_for(max_rows * 64, 256, 4096)), dim3(256), 0,
-                     st, y, nrm, dy, n, nrows, dp);
-  PS_CHECK_LAUNCH();
-  return kOk;
-}
-
-int launch_colsum_partial(const float* X, int n, int64_t ld, const int* nrows_dev, int nrows_host,
-                          int G, float* partial, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(ceil_div(n, 64), G), dim3(256), 0, st, X, n, ld,
-                     nrows_dev, nrows_host, partial);
-  PS_CHECK_LAUNCH();
-  return kOk;
-}
-
-int launch_reduce_slabs(const float* part, int S, int64_t stride, int64_t len, float* out,
-                        hipStream_t st) {
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(len, 256, 1024)), dim3(256), 0, st, part, S,
-                     stride, len, out);
+                     st, y, nrm, dy, n, nrows, dp, z, z_n, z_rows, zi, zi_n);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -824,24 +847,20 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
                 const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
                 int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
                 hipStream_t st) {
-  PS_CHECK_HIP(hipMemsetAsync(G, 0, (size_t)(3 * S_max * d) * sizeof(float), st));
-  PS_CHECK_HIP(hipMemsetAsync(Kc, 0, (size_t)(3 * S_max) * sizeof(int), st));
+  // G and Kc are zero on entry (init_workspace; then loss_finish / the first
+  // backward kernel leave them zero)
   const int nblk = ceil_div(B, 4);
   hipLaunchKernelGGL(loss_triple_kernel, dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, margin,
                      feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart);
   PS_CHECK_LAUNCH();
   hipLaunchKernelGGL(loss_finish_kernel, dim3(grid_for(S_max * d, 256, 1024)), dim3(256), 0, st, G,
-                     Kc, S_max, nS, d, dZ, part, nblk, B, scal);
-  PS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(variance_finish_kernel, dim3(1), dim3(256), 0, st, colpart, nblk, d, B, scal);
+                     Kc, S_max, nS, d, dZ, part, nblk, colpart, B, scal);
   PS_CHECK_LAUNCH();
   return kOk;
 }
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* lr_dev,
                 int* step_dev, float beta1, float beta2, float eps, hipStream_t st) {
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, st, step_dev);
-  PS_CHECK_LAUNCH();
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, p, g, m, v, n,
                      lr_dev, step_dev, beta1, beta2, eps);
   PS_CHECK_LAUNCH();

@@ -30,29 +30,27 @@ int launch_mark_table(unsigned long long*, const int32_t*, const int*, int64_t, 
                       int64_t, int, int64_t, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
-int launch_rank_list(const unsigned long long*, const uint32_t*, const int64_t*, int64_t, int32_t*,
-                     hipStream_t);
 int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const int*, int64_t,
                       const unsigned long long*, const uint32_t*, const unsigned long long*,
                       const uint32_t*, const int32_t*, const float*, int64_t, int, int32_t*,
-                      int32_t*, int32_t*, float*, hipStream_t);
+                      int32_t*, int32_t*, float*, const unsigned long long*, const uint32_t*,
+                      const int64_t*, int64_t, int32_t*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_csr_build(const int32_t*, const int*, int64_t, int, const int*, int64_t, int*, int*,
-                     int*, int*, int32_t*, int32_t*, hipStream_t);
+                     int*, int*, int32_t*, int32_t*, float*, int, hipStream_t);
 int launch_dq_segment(const int32_t*, const int32_t*, const float*, int, const float*, int64_t,
                       const float*, int, const int*, int64_t, const int*, int64_t, float*,
                       hipStream_t);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
-                          float*, hipStream_t);
-int launch_colsum_partial(const float*, int, int64_t, const int*, int, int, float*, hipStream_t);
-int launch_reduce_slabs(const float*, int, int64_t, int64_t, float*, hipStream_t);
+                          float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
                 hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, int*, float, float,
                 float, hipStream_t);
-int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, hipStream_t);
+int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, const float*,
+                           float*, hipStream_t);
 int launch_gather_out(const float*, int, const int32_t*, int64_t, float*, hipStream_t);
 int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
                         int*, float*, hipStream_t);
@@ -102,7 +100,7 @@ struct Engine {
   // workspace layout
   size_t bits_begin = 0, bits_end = 0;  // all bitmaps contiguous (one memset)
   size_t block_sums = 0, ids = 0, pos_rank = 0, H1 = 0, Z = 0, dZ = 0, dP1 = 0;
-  size_t G = 0, Kc = 0, part = 0, scal = 0, err = 0, slab = 0, colpart = 0, varpart = 0;
+  size_t G = 0, Kc = 0, part = 0, scal = 0, slab = 0, bslab = 0, varpart = 0;
   int64_t slab_floats = 0;
   size_t total = 0;
   int64_t max_bsum_blocks = 0;
@@ -152,8 +150,6 @@ static size_t carve(size_t& cur, int64_t bytes) {
   cur += (size_t)std::max<int64_t>(bytes, 0);
   return at;
 }
-
-constexpr int kColsumBlocks = 32;  // row chunks of the bias-gradient column sums
 
 // Split-K weight gradients (C[M][N] = A^T B over K data rows): pick the block
 // tile and split count so that tiles x splits fills the 256 CUs with >= 64 rows
@@ -251,8 +247,6 @@ static void layout(Engine& E) {
   E.part = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * 4 * 4);
   E.varpart = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * c.out * 4);
   E.scal = carve(cur, 64);
-  E.err = carve(cur, 16);
-  // split-K slabs: max over the weight-gradient GEMMs
   // split-K slabs: any split count up to kMaxSplits (it is chosen from size hints)
   int64_t slab = kMaxSplits * c.out * c.out;
   for (auto& lb : E.L) {
@@ -261,7 +255,7 @@ static void layout(Engine& E) {
   }
   E.slab_floats = slab;
   E.slab = carve(cur, slab * 4);
-  E.colpart = carve(cur, kColsumBlocks * std::max(c.hid, c.out) * 4);
+  E.bslab = carve(cur, kMaxSplits * std::max(c.hid, c.out) * 4);
   E.total = (size_t)align_up((int64_t)cur, 256);
 }
 
@@ -278,7 +272,6 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   const int Lc = (int)c.n_layers, T = (int)c.T;
   const int64_t n = c.n_items;
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.bits_begin), 0, E.bits_end - E.bits_begin, st));
-  PS_CHECK_HIP(hipMemsetAsync(at<int>(ws, E.err), 0, 16, st));
   if (ids_dev != at<int64_t>(ws, E.ids))
     PS_CHECK_HIP(hipMemcpyAsync(at<int64_t>(ws, E.ids), ids_dev, (size_t)n_pos * 8,
                                 hipMemcpyDeviceToDevice, st));
@@ -292,7 +285,8 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   // frontier, top-down
   LayerBuf& top = E.L[(size_t)Lc - 1];
   Timed t_front(E, "fwd.frontier", st);
-  PS_TRY(launch_mark_i64(bits(top.S), ids, n_pos, n, at<int>(ws, E.err), st));
+  // ids were range-checked by the caller (pinsage_model._Engine)
+  PS_TRY(launch_mark_i64(bits(top.S), ids, n_pos, n, nullptr, st));
   PS_TRY(launch_set_finalize(bits(top.S), bits(top.S), nullptr, n, bsum, pref(top.S), mem(top.S),
                              cnt(top.S), st));
   for (int l = Lc - 1; l >= 0; --l) {
@@ -306,18 +300,19 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
                                  cnt(lo.S), st));
     }
   }
-  PS_TRY(launch_rank_list(bits(top.S), pref(top.S), ids, n_pos, at<int32_t>(ws, E.pos_rank), st));
   t_front.stop();
 
   // layers, bottom-up
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
     const SetBuf* prev = l > 0 ? &E.L[(size_t)l - 1].S : nullptr;
+    const bool is_top = l == Lc - 1;  // the top layer also ranks the batch positions
     PS_TRY(launch_layer_prep(mem(lb.S), cnt(lb.S), lb.S.cap, mem(lb.N), cnt(lb.N), lb.N.cap,
                              bits(lb.N), pref(lb.N), prev ? bits(*prev) : nullptr,
                              prev ? pref(*prev) : nullptr, E.nb, E.wn, E.ldT, T,
                              at<int32_t>(ws, lb.self_src), at<int32_t>(ws, lb.q_src),
-                             at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), st));
+                             at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), bits(top.S),
+                             pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank), st));
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
     const int64_t ldh = l == 0 ? E.ld_f : c.out;
     // Q projection of the distinct neighbours: lrelu(h[u] Q^T + b)
@@ -394,38 +389,58 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   return kOk;
 }
 
-// weight gradient dst[M][N] (+ column offset) = A^T B over the device row count
-static int weight_grad(Engine& E, void* ws, const float* A, int64_t lda, int M, const float* B,
-                       int64_t ldb, const int32_t* b_idx, int N, const int* K_dev, int64_t K_max,
-                       int64_t K_hint, float* dst, int64_t ld_dst, hipStream_t st) {
+// Weight gradient dst[M][N] = A^T [B || B2] over the device row count (split-K
+// slabs + one reduction); B2 (columns >= N1) is torch.cat's second operand.  If
+// dst_b is set, the bias gradient dst_b[M] = column sums of A comes out of the
+// same GEMM (bias_part) and the same reduction.
+struct WGrad {
+  const float* A = nullptr;
+  int64_t lda = 0;
+  int M = 0;
+  const float* B = nullptr;
+  int64_t ldb = 0;
+  const int32_t* b_idx = nullptr;
+  int N1 = -1;
+  const float* B2 = nullptr;
+  int64_t ldb2 = 0;
+  int N = 0;
+  const int* K_dev = nullptr;
+  int64_t K_max = 0, K_hint = 0;
+  float* dst = nullptr;
+  int64_t ld_dst = 0;
+  float* dst_b = nullptr;
+};
+
+static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st) {
   int cfg = 0, S = 1;
-  choose_wgrad(M, N, K_hint > 0 ? std::min(K_hint, K_max) : K_max, &cfg, &S);
+  choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
   GemmParams p;
   p.cfg = cfg;
-  p.M = M;
-  p.N = N;
-  p.K_dev = K_dev;
-  p.K_max = (int)K_max;
+  p.M = w.M;
+  p.N = w.N;
+  p.K_dev = w.K_dev;
+  p.K_max = (int)w.K_max;
   p.a_kmajor = false;
-  p.a = A;
-  p.lda = lda;
+  p.a = w.A;
+  p.lda = w.lda;
   p.b_kmajor = false;
-  p.b = B;
-  p.ldb = ldb;
-  p.b_idx = b_idx;
+  p.b = w.B;
+  p.ldb = w.ldb;
+  p.b_idx = w.b_idx;
+  if (w.B2) {
+    p.N1 = w.N1;
+    p.b2 = w.B2;
+    p.ldb2 = w.ldb2;
+  }
   p.c = at<float>(ws, E.slab);
-  p.ldc = N;
+  p.ldc = w.N;
   p.epi = kEpiPartial;
   p.splits = S;
-  PS_REQUIRE((int64_t)S * M * N <= E.slab_floats, kErrWorkspace, "engine: split-K slab too small");
+  p.bias_part = w.dst_b ? at<float>(ws, E.bslab) : nullptr;
+  PS_REQUIRE((int64_t)S * w.M * w.N <= E.slab_floats, kErrWorkspace, "engine: split-K slab too small");
   PS_TRY(launch_gemm(p, st));
-  return launch_reduce_slabs_2d(at<float>(ws, E.slab), S, (int64_t)M * N, M, N, dst, ld_dst, st);
-}
-
-static int bias_grad(Engine& E, void* ws, const float* X, int n, const int* rows_dev, float* dst,
-                     hipStream_t st) {
-  PS_TRY(launch_colsum_partial(X, n, n, rows_dev, 0, kColsumBlocks, at<float>(ws, E.colpart), st));
-  return launch_reduce_slabs(at<float>(ws, E.colpart), kColsumBlocks, n, n, dst, st);
+  return launch_reduce_slabs_2d(at<float>(ws, E.slab), S, (int64_t)w.M * w.N, w.M, w.N, w.dst,
+                                w.ld_dst, p.bias_part, w.dst_b, st);
 }
 
 // ---------------------------------------------------------------- backward
@@ -440,8 +455,21 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
   float* gr = E.grads;
   Timed t_hb(E, "bwd.head", st);
   // head: Z = H1 G2^T, H1 = lrelu(y G1^T + b1)
-  PS_TRY(weight_grad(E, ws, at<float>(ws, E.dZ), o, o, at<float>(ws, E.H1), o, nullptr, o,
-                     cnt(top.S), top.S.cap, top.S.hint, gr + E.pG2w, o, st));
+  {
+    WGrad w;
+    w.A = at<float>(ws, E.dZ);
+    w.lda = o;
+    w.M = o;
+    w.B = at<float>(ws, E.H1);
+    w.ldb = o;
+    w.N = o;
+    w.K_dev = cnt(top.S);
+    w.K_max = top.S.cap;
+    w.K_hint = top.S.hint;
+    w.dst = gr + E.pG2w;
+    w.ld_dst = o;
+    PS_TRY(weight_grad(E, ws, w, st));
+  }
   {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
@@ -460,9 +488,22 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     p.ldm = o;
     PS_TRY(launch_gemm(p, st));
   }
-  PS_TRY(weight_grad(E, ws, at<float>(ws, E.dP1), o, o, at<float>(ws, top.y), o, nullptr, o,
-                     cnt(top.S), top.S.cap, top.S.hint, gr + E.pG1w, o, st));
-  PS_TRY(bias_grad(E, ws, at<float>(ws, E.dP1), o, cnt(top.S), gr + E.pG1b, st));
+  {
+    WGrad w;  // dG1 and db1
+    w.A = at<float>(ws, E.dP1);
+    w.lda = o;
+    w.M = o;
+    w.B = at<float>(ws, top.y);
+    w.ldb = o;
+    w.N = o;
+    w.K_dev = cnt(top.S);
+    w.K_max = top.S.cap;
+    w.K_hint = top.S.hint;
+    w.dst = gr + E.pG1w;
+    w.ld_dst = o;
+    w.dst_b = gr + E.pG1b;
+    PS_TRY(weight_grad(E, ws, w, st));
+  }
   {
     GemmParams p;  // dY_top = dP1 G1
     p.M_dev = cnt(top.S);
@@ -487,62 +528,89 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
     const int64_t ldh = l == 0 ? E.ld_f : c.out;
     float* dp = at<float>(ws, lb.dp);
-    PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
-                                 o, cnt(lb.S), lb.S.cap, dp, st));
-    // dW = dp^T [h_self || agg]
-    PS_TRY(weight_grad(E, ws, dp, o, o, h, ldh, at<int32_t>(ws, lb.self_src), d, cnt(lb.S),
-                       lb.S.cap, lb.S.hint, gr + lb.pWw, d + hd, st));
-    PS_TRY(weight_grad(E, ws, dp, o, o, at<float>(ws, lb.agg), hd, nullptr, hd, cnt(lb.S), lb.S.cap,
-                       lb.S.hint, gr + lb.pWw + d, d + hd, st));
-    PS_TRY(bias_grad(E, ws, dp, o, cnt(lb.S), gr + lb.pWb, st));
     float* dYprev = l > 0 ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr;
-    if (l > 0) {
-      PS_CHECK_HIP(hipMemsetAsync(dYprev, 0, (size_t)E.L[(size_t)l - 1].S.cap * o * 4, st));
-      GemmParams p;  // d_self = dp W[:, :d]  -> scatter-add into the rows of layer l-1
-      p.M_dev = cnt(lb.S);
-      p.M_hint = (int)lb.S.hint;
-      p.M_max = (int)lb.S.cap;
-      p.N = d;
-      p.K = o;
-      p.a = dp;
-      p.lda = o;
-      p.b_kmajor = false;
-      p.b = E.params + lb.pWw;
-      p.ldb = d + hd;
-      p.c = dYprev;
-      p.ldc = o;
-      p.c_idx = at<int32_t>(ws, lb.self_src);
-      p.epi = kEpiAccum;
-      PS_TRY(launch_gemm(p, st));
+    // dp = d(normalize(lrelu(.))); also zeroes dY_{l-1} (scatter-add target
+    // below) and, at the top layer, the loss's multiplicity counters
+    PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
+                                 o, cnt(lb.S), lb.S.cap, dp, dYprev, o,
+                                 l > 0 ? cnt(E.L[(size_t)l - 1].S) : nullptr,
+                                 l == Lc - 1 ? at<int>(ws, E.Kc) : nullptr, 3 * top.S.cap, st));
+    {
+      WGrad w;  // dW = dp^T [h_self || agg], dWb = colsum(dp)
+      w.A = dp;
+      w.lda = o;
+      w.M = o;
+      w.B = h;
+      w.ldb = ldh;
+      w.b_idx = at<int32_t>(ws, lb.self_src);
+      w.N1 = d;
+      w.B2 = at<float>(ws, lb.agg);
+      w.ldb2 = hd;
+      w.N = d + hd;
+      w.K_dev = cnt(lb.S);
+      w.K_max = lb.S.cap;
+      w.K_hint = lb.S.hint;
+      w.dst = gr + lb.pWw;
+      w.ld_dst = d + hd;
+      w.dst_b = gr + lb.pWb;
+      PS_TRY(weight_grad(E, ws, w, st));
     }
     {
-      GemmParams p;  // d_agg = dp W[:, d:]
+      // [d_self || d_agg] = dp W: columns < d scatter-add into the rows of
+      // layer l-1 (l > 0), columns >= d go to dagg
+      GemmParams p;
       p.M_dev = cnt(lb.S);
       p.M_hint = (int)lb.S.hint;
       p.M_max = (int)lb.S.cap;
-      p.N = hd;
       p.K = o;
       p.a = dp;
       p.lda = o;
       p.b_kmajor = false;
-      p.b = E.params + lb.pWw + d;
       p.ldb = d + hd;
-      p.c = at<float>(ws, lb.dagg);
-      p.ldc = hd;
+      if (l > 0) {
+        p.N = d + hd;
+        p.b = E.params + lb.pWw;
+        p.c = dYprev;
+        p.ldc = o;
+        p.c_idx = at<int32_t>(ws, lb.self_src);
+        p.epi = kEpiAccum;
+        p.N1 = d;
+        p.c2 = at<float>(ws, lb.dagg);
+        p.ldc2 = hd;
+      } else {
+        p.N = hd;
+        p.b = E.params + lb.pWw + d;
+        p.c = at<float>(ws, lb.dagg);
+        p.ldc = hd;
+      }
       PS_TRY(launch_gemm(p, st));
     }
     PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
                             at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
                             at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
-                            st));
+                            at<float>(ws, lb.dpq), hd, st));
     PS_TRY(launch_dq_segment(at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u), at<float>(ws, lb.wloc),
                              T, at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, cnt(lb.S),
                              lb.S.cap, cnt(lb.N), lb.N.cap, at<float>(ws, lb.dpq), st));
-    // dQ = dpq^T h[q_src]
-    Timed tq(E, lname("bwd.q_wgrad", l), st);
-    PS_TRY(weight_grad(E, ws, at<float>(ws, lb.dpq), hd, hd, h, ldh, at<int32_t>(ws, lb.q_src), d,
-                       cnt(lb.N), lb.N.cap, lb.N.hint, gr + lb.pQw, d, st));
-    PS_TRY(bias_grad(E, ws, at<float>(ws, lb.dpq), hd, cnt(lb.N), gr + lb.pQb, st));
+    {
+      // dQ = dpq^T h[q_src], dQb = colsum(dpq)
+      Timed tq(E, lname("bwd.q_wgrad", l), st);
+      WGrad w;
+      w.A = at<float>(ws, lb.dpq);
+      w.lda = hd;
+      w.M = hd;
+      w.B = h;
+      w.ldb = ldh;
+      w.b_idx = at<int32_t>(ws, lb.q_src);
+      w.N = d;
+      w.K_dev = cnt(lb.N);
+      w.K_max = lb.N.cap;
+      w.K_hint = lb.N.hint;
+      w.dst = gr + lb.pQw;
+      w.ld_dst = d;
+      w.dst_b = gr + lb.pQb;
+      PS_TRY(weight_grad(E, ws, w, st));
+    }
     if (l > 0) {
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
       p.M_dev = cnt(lb.N);
@@ -562,6 +630,18 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(launch_gemm(p, st));
     }
   }
+  return kOk;
+}
+
+// Zero the regions that kernels keep zero after use (loss G / Kc, CSR counts):
+// once per workspace, before its first step.
+int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
+  const EngineConfig& c = E.cfg;
+  const int64_t top = E.L.back().S.cap;
+  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.G), 0, (size_t)(3 * top * c.out) * 4, st));
+  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.Kc), 0, (size_t)(3 * top) * 4, st));
+  for (auto& lb : E.L)
+    PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, lb.cnt), 0, (size_t)(lb.N.cap + 1) * 4, st));
   return kOk;
 }
 
@@ -642,7 +722,6 @@ int pinsage_engine_offsets(const pinsage_engine* e, pinsage_engine_offsets_t* o)
   o->z = (int64_t)E->Z;
   o->dz = (int64_t)E->dZ;
   o->scalars = (int64_t)E->scal;
-  o->err = (int64_t)E->err;
   o->n_layers = E->cfg.n_layers;
   for (int64_t l = 0; l < E->cfg.n_layers && l < 8; ++l) {
     o->count_S[l] = (int64_t)E->L[(size_t)l].S.count;
@@ -719,6 +798,14 @@ int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t*
     E->L[l].N.hint = N ? N[l] : 0;
   }
   return kOk;
+}
+
+int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream) {
+  if (!e || !ws) {
+    set_error("engine_init_workspace: null argument");
+    return kErrArg;
+  }
+  return engine_init_workspace(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
 }
 
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,

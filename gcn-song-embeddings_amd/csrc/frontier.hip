@@ -38,7 +38,7 @@ __global__ void bits_mark_i64_kernel(unsigned long long* __restrict__ bits,
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t v = ids[i];
     if (v < 0 || v >= limit) {
-      atomicExch(err, 1);
+      if (err) atomicExch(err, 1);
       continue;
     }
     mark(bits, v);
@@ -182,12 +182,57 @@ __global__ __launch_bounds__(kScanBlock) void bits_scan_compact_kernel(
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) *count_out = (int)p;
 }
 
-// ranks of an int64 id list (e.g. batch positions -> rows of the top set)
-__global__ void rank_list_kernel(const unsigned long long* __restrict__ bits,
-                                 const uint32_t* __restrict__ prefix, const int64_t* __restrict__ ids,
-                                 int64_t n, int32_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = rank_of(bits, prefix, ids[i]);
+// Single-block finalisation for bitmaps of <= kSmallWords words (<= 1M ids):
+// OR, popcount, block scan, prefixes, compaction and count in one launch.
+constexpr int kSmallWords = 16384;
+__global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
+    unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ a,
+    const unsigned long long* __restrict__ b, int64_t nwords, uint32_t* __restrict__ prefix,
+    int32_t* __restrict__ members, int* __restrict__ count_out) {
+  __shared__ uint32_t wsum[16];
+  const int per = (int)((nwords + 1023) / 1024);
+  const int64_t w0 = (int64_t)threadIdx.x * per;
+  unsigned long long xs[16];
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    xs[q] = 0ull;
+    const int64_t w = w0 + q;
+    if (q < per && w < nwords) {
+      unsigned long long x = a[w];
+      if (b) x |= b[w];
+      if (dst != a || b) dst[w] = x;
+      xs[q] = x;
+      c += __popcll(x);
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t p = inc - c;
+  for (int i = 0; i < wv; ++i) p += wsum[i];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t w = w0 + q;
+    if (q < per && w < nwords) {
+      prefix[w] = p;
+      unsigned long long m = xs[q];
+      uint32_t j = p;
+      while (m) {
+        const int bit = __ffsll((long long)m) - 1;
+        members[j++] = (int32_t)(w * 64 + bit);
+        m &= m - 1;
+      }
+      p += __popcll(xs[q]);
+    }
+  }
+  if (threadIdx.x == 1023) *count_out = (int)p;
 }
 
 // ---------------------------------------------------------------- host side
@@ -235,21 +280,18 @@ int launch_set_finalize(unsigned long long* dst, const unsigned long long* a,
                         const unsigned long long* b, int64_t universe, uint32_t* block_sums,
                         uint32_t* prefix, int32_t* members, int* count, hipStream_t st) {
   const int64_t nw = bitset_words(universe);
+  if (nw <= kSmallWords) {
+    hipLaunchKernelGGL(bits_finalize_small_kernel, dim3(1), dim3(1024), 0, st, dst, a, b, nw, prefix,
+                       members, count);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
   const int nb = (int)bitset_blocks(universe);
   hipLaunchKernelGGL(bits_or_count_kernel, dim3(nb), dim3(kScanBlock), 0, st, dst, a, b, nw,
                      block_sums);
   PS_CHECK_LAUNCH();
   hipLaunchKernelGGL(bits_scan_compact_kernel, dim3(nb), dim3(kScanBlock), 0, st, dst, nw,
                      block_sums, prefix, members, count);
-  PS_CHECK_LAUNCH();
-  return kOk;
-}
-
-int launch_rank_list(const unsigned long long* bits, const uint32_t* prefix, const int64_t* ids,
-                     int64_t n, int32_t* out, hipStream_t st) {
-  if (n <= 0) return kOk;
-  hipLaunchKernelGGL(rank_list_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, bits, prefix, ids,
-                     n, out);
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -37,9 +37,22 @@ struct GemmParams {
   const float* b = nullptr;
   int64_t ldb = 0;
   const int32_t* b_idx = nullptr;
+  // second N segment of an N-major B (torch.cat along N): columns n >= N1
+  int N1 = -1;
+  const float* b2 = nullptr;
+  int64_t ldb2 = 0;
+  const int32_t* b2_idx = nullptr;
   float* c = nullptr;
   int64_t ldc = 0;
   const int32_t* c_idx = nullptr;  // output row scatter
+  // split output (kEpiStore/kEpiAccum): columns n >= N1 are stored plainly to
+  // c2[m][n - N1] instead of C (so one launch can scatter-add one block of
+  // columns and write the rest)
+  float* c2 = nullptr;
+  int64_t ldc2 = 0;
+  // kEpiPartial: column sums of A over this split's K rows -> bias_part[split][M]
+  // (the bias gradient of a weight gradient dW = A^T B, A M-major)
+  float* bias_part = nullptr;
   int epi = kEpiStore;
   const float* bias = nullptr;
   bool act = false;               // leaky_relu

@@ -92,11 +92,14 @@ __device__ __forceinline__ void kmajor_store(float* Sm, const float4 (&v)[(Shape
   }
 }
 
-// MN-major operand ([k][col] in memory, k rows optionally gathered)
+// MN-major operand ([k][col] in memory, k rows optionally gathered); columns
+// >= c1 (if c1 >= 0) come from a second matrix a2 (torch.cat along columns)
 template <int R, int BK>
 __device__ __forceinline__ void mnmajor_load(float4 (&v)[(Shape<R, BK>::NV)], int tid, const float* a,
                                              int64_t lda, const int32_t* idx, int c0, int cmax,
-                                             int k0, int kend) {
+                                             int k0, int kend, int c1 = -1,
+                                             const float* a2 = nullptr, int64_t lda2 = 0,
+                                             const int32_t* idx2 = nullptr) {
   using S = Shape<R, BK>;
 #pragma unroll
   for (int i = 0; i < S::NV; ++i) {
@@ -105,8 +108,13 @@ __device__ __forceinline__ void mnmajor_load(float4 (&v)[(Shape<R, BK>::NV)], in
     const int k = k0 + kr;
     const int c = c0 + cc * 4;
     if (lin < S::TOT_MN && k < kend && c < cmax) {
-      const int64_t r = idx ? idx[k] : k;
-      v[i] = *reinterpret_cast<const float4*>(a + r * lda + c);
+      if (a2 && c >= c1) {
+        const int64_t r = idx2 ? idx2[k] : k;
+        v[i] = *reinterpret_cast<const float4*>(a2 + r * lda2 + (c - c1));
+      } else {
+        const int64_t r = idx ? idx[k] : k;
+        v[i] = *reinterpret_cast<const float4*>(a + r * lda + c);
+      }
     } else {
       v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -201,7 +209,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
       if (AK) kmajor_load<BM, BK>(va, RA, tid, k0, ke, p.K1);
       else mnmajor_load<BM, BK>(va, tid, p.a, p.lda, p.a_idx, m0, M, k0, ke);
       if (BKM) kmajor_load<BN, BK>(vb, RB, tid, k0, ke, -1);
-      else mnmajor_load<BN, BK>(vb, tid, p.b, p.ldb, p.b_idx, n0, N, k0, ke);
+      else mnmajor_load<BN, BK>(vb, tid, p.b, p.ldb, p.b_idx, n0, N, k0, ke, p.N1, p.b2, p.ldb2,
+                                p.b2_idx);
     };
     auto store = [&](const float4 (&va)[SA::NV], const float4 (&vb)[SB::NV], int buf) {
       if (AK) kmajor_store<BM, BK>(As[buf], va, tid);
@@ -210,9 +219,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
       else mnmajor_store<BN, BK>(Bs[buf], vb, tid);
     };
     const int h = lane >> 5, l32 = lane & 31;
+    const bool do_bias = !AK && p.bias_part && tn == 0 && tid < BM;
+    float bsum = 0.f;
     // MFMA k-assignment: in the r-th MFMA of octet s, lane half h supplies
     // k = 8s + 4h + r for both operands (any bijection onto the 8 k works).
     auto compute = [&](int cur) {
+      if (do_bias) {  // column sums of A^T over this tile's k rows (zero-padded)
+#pragma unroll
+        for (int k = 0; k < BK; ++k) bsum += As[cur][k * SA::W + tid];
+      }
 #pragma unroll
       for (int s8 = 0; s8 < BK / 8; ++s8) {
         const int k4 = 8 * s8 + 4 * h;
@@ -253,6 +268,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     // ------------------------------------------------------------ epilogue
     // acc[i][j][r] -> row m0 + (wm*TM+i)*32 + (r&3) + 8*(r>>2) + 4*h, col n0 + (wn*TN+j)*32 + l32
     if (p.epi == kEpiPartial) {
+      if (do_bias && m0 + tid < M) p.bias_part[(int64_t)split * M + m0 + tid] = bsum;
       float* C = p.c + (int64_t)split * M * p.ldc;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -323,8 +339,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
             if (p.bias) v += p.bias[col];
             if (p.act) v = lrelu(v);
             if (p.mask) v *= lrelu_grad(p.mask[(int64_t)row * p.ldm + col]);
-            float* o = p.c + dst * p.ldc + col;
-            *o = accum ? *o + v : v;
+            if (p.c2 && col >= p.N1) {
+              p.c2[(int64_t)row * p.ldc2 + (col - p.N1)] = v;
+            } else {
+              float* o = p.c + dst * p.ldc + col;
+              *o = accum ? *o + v : v;
+            }
           }
         }
     }
@@ -374,6 +394,10 @@ int launch_gemm(const GemmParams& p, hipStream_t st) {
   PS_REQUIRE(p.a_kmajor || (p.M % 4 == 0 && !p.M_dev), kErrArg,
              "gemm: M-major A needs a static M that is a multiple of 4");
   PS_REQUIRE(p.b_kmajor || p.N % 4 == 0, kErrArg, "gemm: N-major B needs N % 4 == 0");
+  PS_REQUIRE(!p.b2 || (!p.b_kmajor && p.N1 >= 0 && p.N1 % 4 == 0), kErrArg,
+             "gemm: a second B segment needs N-major B and N1 % 4 == 0");
+  PS_REQUIRE(!p.c2 || (p.N1 >= 0 && p.epi != kEpiL2Norm && p.epi != kEpiPartial), kErrArg,
+             "gemm: split output needs N1 and a store/accumulate epilogue");
   PS_REQUIRE(p.epi != kEpiL2Norm || p.N <= 128, kErrArg, "gemm: L2-norm epilogue needs N <= 128");
   PS_REQUIRE(p.epi != kEpiPartial || (!p.M_dev && !p.c_idx), kErrArg,
              "gemm: split-K partials need a static M");

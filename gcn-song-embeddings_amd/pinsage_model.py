@@ -380,7 +380,10 @@ class _Engine:
             pass
 
     def new_workspace(self, dev):
-        return torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+        ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
+        nat.check(nat.lib().pinsage_engine_init_workspace(self.h, nat.ptr(ws), nat.stream_ptr()),
+                  "init_workspace")
+        return ws
 
     def counts(self, ws):
         """Frontier sizes (|S_l|, |N_l|) of the last forward in ws (synchronises)."""
@@ -506,6 +509,9 @@ class _EngineRunner:
         n = int(ids.shape[0])
         if n == 0:
             return torch.empty((0, m.out_dim), device=out_dev)
+        if int(ids.min()) < 0 or int(ids.max()) >= feats.shape[0]:
+            # the reference's features[nodeset] raises the same way
+            raise IndexError(f"node ids out of range for {feats.shape[0]} items")
         self.pack()
         self.ensure_engine(n)
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.params())

@@ -13,6 +13,7 @@ slice; gradients are averaged with one RCCL all-reduce of the flat buffer.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import time
 
@@ -87,25 +88,94 @@ def sample_batch(all_ids, positives, batch_size, nbhds, hard_negatives=True, hn_
     if hard_negatives:
         pos_batch = sample_positives_with_rep(positives, batch_size)
         return sample_hard_negatives(all_ids, pos_batch, nbhds, hn_min, hn_max)
-    pos = positives.to(torch.int64).contiguous()
+    pos = positives if positives.dtype == torch.int64 else positives.to(torch.int64)
+    pos = pos.contiguous()
     n_items = int(all_ids.shape[0])
-    B = min(int(batch_size), int(pos.shape[0]))
-    out = np.empty((B, 3), np.int64)
-    pos_np = pos.numpy() if pos.device.type == "cpu" else pos.cpu().numpy()
     if not _all_ids_is_range(all_ids):
         batch, nodeset = sample_easy_negatives(all_ids, sample_positives_with_rep(positives, batch_size))
         return batch, nodeset
-    with nat.torch_rng() as mt:
-        nat.check(nat.lib().pinsage_sample_batch_easy(
-            mt.p, pos_np.ctypes.data_as(nat.vp), pos_np.shape[0], n_items, int(batch_size),
-            out.ctypes.data_as(nat.vp)), "sample_batch")
-    batch = torch.from_numpy(out)
-    return batch, batch.flatten().unique()
+    return _PREFETCH.sample(pos, n_items, int(batch_size))
+
+
+class _BatchPrefetcher:
+    """Reference-exact easy batches through the native batch sampler
+    (pinsage_batch_sampler_*, csrc/loader.hip).
+
+    The reference draws every batch from torch's global CPU generator; its O(P)
+    part is randperm(P) consuming P-1 draws.  After serving a batch, the native
+    sampler draws the next one on its worker thread from a copy of the generator
+    state it just handed back, and uses that draw only if the next request
+    starts from a byte-identical state (nothing else touched torch's generator);
+    otherwise it draws synchronously.  Batches and generator states are exactly
+    the reference's either way.  PINSAGE_PREFETCH=0 disables the speculation."""
+
+    def __init__(self):
+        self.speculate = os.environ.get("PINSAGE_PREFETCH", "1") != "0"
+        self.h = None
+        self.key = None
+        self.pos_np = None
+        self.hits = 0
+
+    def _sampler(self, pos, n_items, batch_size):
+        key = (pos.data_ptr(), pos._version, tuple(pos.shape), n_items, batch_size)
+        if key != self.key:
+            self.close()
+            self.pos_np = pos.numpy() if pos.device.type == "cpu" else pos.cpu().numpy()
+            h = ctypes.c_void_p()
+            nat.check(nat.lib().pinsage_batch_sampler_create(
+                self.pos_np.ctypes.data_as(nat.vp), self.pos_np.shape[0], n_items, batch_size,
+                ctypes.byref(h)), "batch_sampler_create")
+            self.h, self.key = h, key
+        return self.h
+
+    def close(self):
+        if self.h is not None:
+            nat.lib().pinsage_batch_sampler_destroy(self.h)
+            self.h = None
+            self.key = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sample(self, pos, n_items, batch_size):
+        h = self._sampler(pos, n_items, batch_size)
+        B = min(batch_size, int(pos.shape[0]))
+        state = torch.get_rng_state()
+        st = state.numpy()
+        after = torch.empty_like(state)
+        out = np.empty((B, 3), np.int64)
+        ns = np.empty(3 * B, np.int64)
+        n_ns = ctypes.c_int64(0)
+        rc = nat.lib().pinsage_batch_sampler_next(
+            h, st.ctypes.data_as(nat.vp), st.nbytes, out.ctypes.data_as(nat.vp),
+            ns.ctypes.data_as(nat.vp), ctypes.byref(n_ns), after.numpy().ctypes.data_as(nat.vp),
+            1 if self.speculate else 0)
+        nat.check(min(rc, 0), "sample_batch")
+        self.hits += rc
+        torch.set_rng_state(after)
+        return torch.from_numpy(out), torch.from_numpy(ns[:n_ns.value])
+
+
+_PREFETCH = _BatchPrefetcher()
+
+
+_RANGE_CACHE = {}
 
 
 def _all_ids_is_range(all_ids):
-    n = int(all_ids.shape[0])
-    return torch.equal(all_ids.cpu().to(torch.int64), torch.arange(n, dtype=torch.int64))
+    """all_ids == arange(n) (the reference's PinSage.all_ids); cached per tensor
+    version so the per-batch check is free."""
+    key = (id(all_ids), all_ids.data_ptr(), all_ids._version, tuple(all_ids.shape))
+    hit = _RANGE_CACHE.get(key)
+    if hit is None:
+        n = int(all_ids.shape[0])
+        hit = torch.equal(all_ids.cpu().to(torch.int64), torch.arange(n, dtype=torch.int64))
+        _RANGE_CACHE.clear()
+        _RANGE_CACHE[key] = hit
+    return hit
 
 
 def batch_variance(h):
@@ -141,7 +211,8 @@ class _FusedStep:
         self.m = self.v = None
         self.grads = None
         self.lr_dev = torch.zeros(1, dtype=torch.float32, device=self.dev)
-        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        # [Adam step, completion ticket] (see pinsage_engine_adam)
+        self.step_dev = torch.zeros(2, dtype=torch.int32, device=self.dev)
         self._lr_host = None
         self.host_batch = None
         self._tuned = False
@@ -195,7 +266,7 @@ class _FusedStep:
                             "exp_avg_sq": self.v[off:off + k].view(p.shape)}
             p.grad = self.grads[off:off + k].view(p.shape)
             off += k
-        self.step_dev.fill_(step)
+        self.step_dev.copy_(torch.tensor([step, 0], dtype=torch.int32))
         self.host_step = step
 
     def sync_optimizer_step(self):
@@ -212,6 +283,9 @@ class _FusedStep:
             self.host_ev[k].synchronize()
         hb = self.host_batch[k][:3 * B]
         hb.copy_(batch.reshape(-1).to(torch.int64))
+        n_items = int(self.runner.engine.cfg.n_items)
+        if int(hb.min()) < 0 or int(hb.max()) >= n_items:
+            raise IndexError(f"batch ids out of range for {n_items} items")
         self.ids_view[:3 * B].copy_(hb, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()

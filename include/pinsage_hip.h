@@ -51,9 +51,29 @@ int pinsage_mt_randperm_prefix(void* mt, int64_t n, int64_t k, int64_t* out);
 
 /* sample_batch with easy negatives (pinsage_training.py:53-77, 89-97) on the
  * host: positives is [P][2] int64, batch_out is [B][3] int64 (query, positive,
- * negative).  Consumes exactly the draws the reference does. */
+ * negative).  Consumes exactly the draws the reference does.  nodeset_out
+ * (nullable, capacity 3B) receives batch.flatten().unique() (sorted), its
+ * length in *n_nodeset. */
 int pinsage_sample_batch_easy(void* mt, const int64_t* positives, int64_t n_pos_pairs,
-                              int64_t n_items, int64_t batch_size, int64_t* batch_out);
+                              int64_t n_items, int64_t batch_size, int64_t* batch_out,
+                              int64_t* nodeset_out, int64_t* n_nodeset);
+
+/* Batch sampler runtime (native data loader for PinSage.train's batch loop).
+ * Holds positives [P][2] int64 (must stay alive and unchanged) and draws the
+ * batch that the torch CPU generator state `state` (torch.get_rng_state()
+ * bytes) yields: batch_out [B][3], nodeset_out (nullable, capacity 3B) =
+ * batch.flatten().unique(), state_after = the generator state after the
+ * reference's draws.  With speculate != 0 the batch starting at state_after is
+ * drawn next on a worker thread and used by the next call iff its state is
+ * byte-identical -- results are always exactly pinsage_sample_batch_easy's.
+ * Returns 1 when the speculative draw was used, 0 when drawn synchronously. */
+typedef struct pinsage_batch_sampler pinsage_batch_sampler;
+int pinsage_batch_sampler_create(const int64_t* positives, int64_t n_pos_pairs, int64_t n_items,
+                                 int64_t batch_size, pinsage_batch_sampler** out);
+void pinsage_batch_sampler_destroy(pinsage_batch_sampler* s);
+int pinsage_batch_sampler_next(pinsage_batch_sampler* s, const uint8_t* state, int64_t nbytes,
+                               int64_t* batch_out, int64_t* nodeset_out, int64_t* n_nodeset,
+                               uint8_t* state_after, int speculate);
 
 /* ------------------------------------------------------------------ sampler (device)
  * do_random_walks (pinsage_model.py:32-53).  CSR: indptr int64 [n_all+1],
@@ -133,7 +153,7 @@ typedef struct {
   int64_t max_pos;  /* max ids per forward (3 * batch_size for a train step) */
 } pinsage_engine_config;
 typedef struct {
-  int64_t ids, pos_rank, z, dz, scalars, err, n_layers;
+  int64_t ids, pos_rank, z, dz, scalars, n_layers;
   int64_t count_S[8], count_N[8], members_S[8], members_N[8], cap_S[8], cap_N[8], y[8];
   int64_t param_offsets[8];
 } pinsage_engine_offsets_t;
@@ -151,7 +171,13 @@ int pinsage_engine_offsets(const pinsage_engine* e, pinsage_engine_offsets_t* ou
 int pinsage_engine_set_tensors(pinsage_engine* e, const float* feats, int64_t ld_feats,
                                const int32_t* nb_table, const float* w_table, int64_t ld_table,
                                float* params, float* grads, float* adam_m, float* adam_v);
-/* forward of all ids (a train step passes the [B][3] batch flattened) */
+/* Zero the workspace regions the step kernels keep zero after use (loss
+ * scatter targets, CSR counters).  Call once per new workspace, before its
+ * first forward. */
+int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream);
+/* forward of all ids (a train step passes the [B][3] batch flattened); ids must
+ * lie in [0, n_items) -- the caller validates them (pinsage_model raises
+ * IndexError like the reference's features[nodeset]). */
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                            void* stream);
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
@@ -164,9 +190,10 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
                                    void* stream);
 /* all parameter gradients from dZ into the grad buffer (overwritten) */
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
-/* torch.optim.Adam step over the flat buffers; lr_dev f32 and step_dev int32
- * live in device memory (step is incremented first) so the step can be
- * graph-replayed. */
+/* torch.optim.Adam step over the flat buffers; lr_dev f32 and step_dev int32[2]
+ * live in device memory so the step can be graph-replayed: the update uses
+ * step_dev[0] + 1 and stores it back; step_dev[1] is a completion ticket that
+ * must be 0 on entry (it is left 0). */
 int pinsage_engine_adam(pinsage_engine* e, const float* lr_dev, int32_t* step_dev, float beta1,
                         float beta2, float eps, void* stream);
 

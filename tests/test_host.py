@@ -193,3 +193,40 @@ def test_compute_fails_loudly_without_gpu():
     g = graph.CSRGraph(4, [0, 1, 2, 3], [2, 3, 0, 1])
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         pm.do_random_walks(g, torch.tensor([0]), 3, 0.85)
+
+
+def test_batch_sampler_speculation_is_exact():
+    """The native sampler's speculative next batch is used only when torch's
+    generator is untouched in between; batches, nodesets and the generator
+    state after each call equal the synchronous reference-exact sampler's."""
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(3000, 500, 20000, seed=9)
+    pos = torch.from_numpy(synthetic.make_positives(pg, 8000, seed=3))
+    all_ids = torch.arange(3000)
+
+    def run(speculate):
+        pt._PREFETCH.close()
+        pt._PREFETCH.speculate = speculate
+        pt._PREFETCH.hits = 0
+        torch.manual_seed(21)
+        out = []
+        for i in range(12):
+            b, ns = pt.sample_batch(all_ids, pos, 64 + (i >= 8) * 16, None, hard_negatives=False)
+            out.append((b, ns))
+            if i % 4 == 1:
+                torch.randint(1000, ())   # another generator user: speculation must miss
+            if i == 6:
+                torch.manual_seed(5)      # a reseed as well
+        out.append(int(torch.randint(2 ** 31, ())))
+        return out, pt._PREFETCH.hits
+
+    ref, h0 = run(False)
+    got, h1 = run(True)
+    pt._PREFETCH.close()
+    pt._PREFETCH.speculate = True
+    assert h0 == 0 and h1 >= 4
+    assert ref[-1] == got[-1]
+    for (b1, n1), (b2, n2) in zip(ref[:-1], got[:-1]):
+        assert torch.equal(b1, b2) and torch.equal(n1, n2)
+        assert torch.equal(n2, b2.flatten().unique())
