@@ -30,6 +30,8 @@ int launch_mark_table(unsigned long long*, const int32_t*, const int*, int64_t, 
                       int64_t, int, int64_t, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
+int launch_top_set(unsigned long long*, int64_t, unsigned long long*, const int64_t*, int64_t,
+                   int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const int*, int64_t,
                       const unsigned long long*, const uint32_t*, const unsigned long long*,
                       const uint32_t*, const int32_t*, const float*, int64_t, int, int32_t*,
@@ -271,7 +273,6 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   PS_REQUIRE(n_pos > 0 && n_pos <= c.max_pos, kErrArg, "engine: n_pos out of range");
   const int Lc = (int)c.n_layers, T = (int)c.T;
   const int64_t n = c.n_items;
-  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.bits_begin), 0, E.bits_end - E.bits_begin, st));
   if (ids_dev != at<int64_t>(ws, E.ids))
     PS_CHECK_HIP(hipMemcpyAsync(at<int64_t>(ws, E.ids), ids_dev, (size_t)n_pos * 8,
                                 hipMemcpyDeviceToDevice, st));
@@ -285,10 +286,14 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   // frontier, top-down
   LayerBuf& top = E.L[(size_t)Lc - 1];
   Timed t_front(E, "fwd.frontier", st);
-  // ids were range-checked by the caller (pinsage_model._Engine)
-  PS_TRY(launch_mark_i64(bits(top.S), ids, n_pos, n, nullptr, st));
-  PS_TRY(launch_set_finalize(bits(top.S), bits(top.S), nullptr, n, bsum, pref(top.S), mem(top.S),
-                             cnt(top.S), st));
+  // One kernel zeroes all of the step's bitmaps, marks the ids (range-checked
+  // by the caller) and finalises the top set.  Captured step graphs stay
+  // kernel-only: a memset node at the head of a replayed graph was not ordered
+  // behind the previous replay's kernels on this stack (back-to-back replays
+  // faulted; synchronised ones did not).
+  PS_TRY(launch_top_set(at<unsigned long long>(ws, E.bits_begin),
+                        (int64_t)(E.bits_end - E.bits_begin) / 8, bits(top.S), ids, n_pos, n, bsum,
+                        pref(top.S), mem(top.S), cnt(top.S), st));
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
     PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, E.nb, E.ldT, T, n, st));

@@ -185,10 +185,15 @@ __global__ __launch_bounds__(kScanBlock) void bits_scan_compact_kernel(
 // Single-block finalisation for bitmaps of <= kSmallWords words (<= 1M ids):
 // OR, popcount, block scan, prefixes, compaction and count in one launch.
 constexpr int kSmallWords = 16384;
-__global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
-    unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ a,
-    const unsigned long long* __restrict__ b, int64_t nwords, uint32_t* __restrict__ prefix,
-    int32_t* __restrict__ members, int* __restrict__ count_out) {
+// kCoherent: read the bitmap with device-coherent loads (it was written by
+// atomics of this same kernel, which bypass the CU's L1)
+template <bool kCoherent>
+__device__ __forceinline__ void finalize_block(unsigned long long* __restrict__ dst,
+                                               const unsigned long long* a,
+                                               const unsigned long long* __restrict__ b,
+                                               int64_t nwords, uint32_t* __restrict__ prefix,
+                                               int32_t* __restrict__ members,
+                                               int* __restrict__ count_out) {
   __shared__ uint32_t wsum[16];
   const int per = (int)((nwords + 1023) / 1024);
   const int64_t w0 = (int64_t)threadIdx.x * per;
@@ -199,7 +204,8 @@ __global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
     xs[q] = 0ull;
     const int64_t w = w0 + q;
     if (q < per && w < nwords) {
-      unsigned long long x = a[w];
+      unsigned long long x =
+          kCoherent ? __hip_atomic_load(a + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a[w];
       if (b) x |= b[w];
       if (dst != a || b) dst[w] = x;
       xs[q] = x;
@@ -233,6 +239,41 @@ __global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
     }
   }
   if (threadIdx.x == 1023) *count_out = (int)p;
+}
+
+__global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
+    unsigned long long* __restrict__ dst, const unsigned long long* a,
+    const unsigned long long* __restrict__ b, int64_t nwords, uint32_t* __restrict__ prefix,
+    int32_t* __restrict__ members, int* __restrict__ count_out) {
+  finalize_block<false>(dst, a, b, nwords, prefix, members, count_out);
+}
+
+// The first kernel of a train step: zero every frontier bitmap of the step
+// (zero_words u64 words from zero), mark the batch ids into the top set and
+// finalise it -- one block, replacing a memset, a mark and a finalise launch.
+// Ids outside [0, limit) are skipped (callers validate them).
+__global__ __launch_bounds__(1024) void bits_top_set_kernel(
+    unsigned long long* __restrict__ zero, int64_t zero_words, unsigned long long* bits,
+    const int64_t* __restrict__ ids, int64_t n, int64_t limit, int64_t nwords,
+    uint32_t* __restrict__ prefix, int32_t* __restrict__ members, int* __restrict__ count_out) {
+  for (int64_t w = threadIdx.x; w < zero_words; w += 1024) zero[w] = 0ull;
+  __threadfence();
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const int64_t v = ids[i];
+    if (v >= 0 && v < limit) atomicOr(bits + (v >> 6), 1ull << (v & 63));
+  }
+  __threadfence();
+  __syncthreads();
+  finalize_block<true>(bits, bits, nullptr, nwords, prefix, members, count_out);
+}
+
+// zero n u64 words (a kernel, not a memset: keeps captured step graphs
+// kernel-only)
+__global__ void zero_words_kernel(unsigned long long* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0ull;
 }
 
 // ---------------------------------------------------------------- host side
@@ -276,6 +317,29 @@ int launch_mark_table_i64(unsigned long long* bits, const int64_t* ids, int64_t 
 }
 
 // Finalise a set: dst = a | b, prefix, sorted members, device count.
+int launch_set_finalize(unsigned long long* dst, const unsigned long long* a,
+                        const unsigned long long* b, int64_t universe, uint32_t* block_sums,
+                        uint32_t* prefix, int32_t* members, int* count, hipStream_t st);
+
+// zero the bitmaps region [zero, zero + zero_words), mark ids into bits and
+// finalise that set (the top frontier of a step)
+int launch_top_set(unsigned long long* zero, int64_t zero_words, unsigned long long* bits,
+                   const int64_t* ids, int64_t n, int64_t universe, uint32_t* block_sums,
+                   uint32_t* prefix, int32_t* members, int* count, hipStream_t st) {
+  const int64_t nw = bitset_words(universe);
+  if (nw <= kSmallWords) {
+    hipLaunchKernelGGL(bits_top_set_kernel, dim3(1), dim3(1024), 0, st, zero, zero_words, bits, ids,
+                       n, universe, nw, prefix, members, count);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
+  hipLaunchKernelGGL(zero_words_kernel, dim3(grid_for(zero_words, 256, 2048)), dim3(256), 0, st, zero,
+                     zero_words);
+  PS_CHECK_LAUNCH();
+  PS_TRY(launch_mark_i64(bits, ids, n, universe, nullptr, st));
+  return launch_set_finalize(bits, bits, nullptr, universe, block_sums, prefix, members, count, st);
+}
+
 int launch_set_finalize(unsigned long long* dst, const unsigned long long* a,
                         const unsigned long long* b, int64_t universe, uint32_t* block_sums,
                         uint32_t* prefix, int32_t* members, int* count, hipStream_t st) {
