@@ -579,13 +579,13 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
 // partials into scal[0] = loss, scal[1] = node-feature loss, and the variance
 // monitor (pinsage_training.py:99-103): sum((h - mean)^2)/(B-1) over the B query
 // rows = (sum |h|^2 - B |mean|^2)/(B-1), from per-block column sums.
-__global__ __launch_bounds__(256) void loss_finish_kernel(float* __restrict__ G,
-                                                          const int* __restrict__ Kc, int64_t S_max,
-                                                          const int* __restrict__ nS, int d,
-                                                          float* __restrict__ dZ,
-                                                          const float* __restrict__ part, int nparts,
-                                                          const float* __restrict__ colpart, int B,
-                                                          float* __restrict__ scal) {
+__global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G,
+                                                           const int* __restrict__ Kc, int64_t S_max,
+                                                           const int* __restrict__ nS, int d,
+                                                           float* __restrict__ dZ,
+                                                           const float* __restrict__ part, int nparts,
+                                                           const float* __restrict__ colpart, int B,
+                                                           float* __restrict__ scal) {
   const int64_t S = *nS;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -601,38 +601,59 @@ __global__ __launch_bounds__(256) void loss_finish_kernel(float* __restrict__ G,
     dZ[e] = v;
   }
   if (blockIdx.x != 0) return;
-  __shared__ float red[4];
-  __shared__ float cs[4][64];
-  float acc = 0.f;
-  const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int c0 = 0; c0 < d; c0 += 64) {
-    const int c = c0 + l;
-    float sc = 0.f;
-    if (c < d)
-      for (int g = q; g < nparts; g += 4) sc += colpart[(int64_t)g * d + c];
-    cs[q][l] = sc;
-    __syncthreads();
-    if (q == 0 && c < d) {
-      const float m = ((cs[0][l] + cs[1][l]) + (cs[2][l] + cs[3][l])) / (float)B;
-      acc += m * m;
-    }
-    __syncthreads();
+  // fixed-order reductions with every thread's loads in flight together
+  __shared__ float cs[1024];
+  __shared__ float wred[16][3];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float l = 0.f, nf = 0.f, sq = 0.f;
+  for (int i = t; i < nparts; i += 1024) {
+    l += part[i * 4 + 0];
+    nf += part[i * 4 + 1];
+    sq += part[i * 4 + 2];
   }
-  acc = wave_sum(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  // column sums of the query rows: thread (grp, c) sums parts grp, grp+ng, ...
+  const int ng = 1024 / d, c = t % d, grp = t / d;
+  float cv = 0.f;
+  if (grp < ng) {
+    int g = grp;
+    for (; g + 3 * ng < nparts; g += 4 * ng)
+      cv += (colpart[(int64_t)g * d + c] + colpart[(int64_t)(g + ng) * d + c]) +
+            (colpart[(int64_t)(g + 2 * ng) * d + c] + colpart[(int64_t)(g + 3 * ng) * d + c]);
+    for (; g < nparts; g += ng) cv += colpart[(int64_t)g * d + c];
+  }
+  cs[t] = cv;
+  l = wave_sum(l);
+  nf = wave_sum(nf);
+  sq = wave_sum(sq);
+  if (lane == 0) {
+    wred[wv][0] = l;
+    wred[wv][1] = nf;
+    wred[wv][2] = sq;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float lsum = 0.f, nf = 0.f, sq = 0.f;
-    for (int i = 0; i < nparts; ++i) {
-      lsum += part[i * 4 + 0];
-      nf += part[i * 4 + 1];
-      sq += part[i * 4 + 2];
+  float msq = 0.f;
+  if (t < d) {
+    float tot = 0.f;
+    for (int q = 0; q < ng; ++q) tot += cs[q * d + t];
+    const float m = tot / (float)B;
+    msq = m * m;
+  }
+  msq = wave_sum(msq);
+  __syncthreads();
+  if (lane == 0) cs[wv] = msq;
+  __syncthreads();
+  if (t == 0) {
+    float lsum = 0.f, nfs = 0.f, sqs = 0.f, ms = 0.f;
+    for (int i = 0; i < 16; ++i) {
+      lsum += wred[i][0];
+      nfs += wred[i][1];
+      sqs += wred[i][2];
+      ms += cs[i];
     }
     scal[0] = lsum / (float)B;
-    scal[1] = nf / (float)B;
-    scal[2] = sq;
-    const float msq = red[0] + red[1] + red[2] + red[3];
-    scal[3] = (sq - (float)B * msq) / (float)(B - 1);
+    scal[1] = nfs / (float)B;
+    scal[2] = sqs;
+    scal[3] = (sqs - (float)B * ms) / (float)(B - 1);
   }
 }
 
@@ -708,30 +729,64 @@ __global__ void dz_scale_kernel(const float* __restrict__ G, const int* __restri
   }
 }
 
-// out[m*ld + n] = sum_s part[s*stride + m*N + n]; bias_out[m] = sum_s bpart[s*M + m]
-__global__ void reduce_slabs_2d_kernel(const float* __restrict__ part, int S, int64_t stride, int M,
-                                       int N, float* __restrict__ out, int64_t ld,
-                                       const float* __restrict__ bpart, float* __restrict__ bias_out) {
-  if (bias_out) {
-    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M;
-         m += (int64_t)gridDim.x * blockDim.x) {
-      float s0 = 0.f, s1 = 0.f;
-      int k = 0;
-      for (; k + 1 < S; k += 2) {
-        s0 += bpart[(int64_t)k * M + m];
-        s1 += bpart[(int64_t)(k + 1) * M + m];
+// Split-K reduction: out[m*ld + n] = sum_s part[s*stride + m*N + n] and
+// bias_out[m] = sum_s bpart[s*M + m].  A block is 64 float4 columns x 4 slab
+// groups: each thread issues its S/4 loads together (the reduction is latency-
+// bound otherwise: few outputs, many slabs), then the 4 groups are combined in
+// LDS in a fixed order (deterministic).  Blocks >= nb_main do the bias.
+__global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __restrict__ part, int S,
+                                                              int64_t stride, int M, int N,
+                                                              float* __restrict__ out, int64_t ld,
+                                                              const float* __restrict__ bpart,
+                                                              float* __restrict__ bias_out,
+                                                              int nb_main) {
+  __shared__ float4 red[4][64];
+  const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
+  if ((int)blockIdx.x < nb_main) {
+    const int64_t e4 = (int64_t)blockIdx.x * 64 + j;  // float4 index into [M][N]
+    const bool ok = e4 * 4 < (int64_t)M * N;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+      const float4* p4 = reinterpret_cast<const float4*>(part) + e4;
+      const int64_t st4 = stride / 4;
+      int k = g;
+      for (; k + 12 < S; k += 16) {
+        const float4 x0 = p4[k * st4], x1 = p4[(k + 4) * st4], x2 = p4[(k + 8) * st4],
+                     x3 = p4[(k + 12) * st4];
+        acc.x += (x0.x + x1.x) + (x2.x + x3.x);
+        acc.y += (x0.y + x1.y) + (x2.y + x3.y);
+        acc.z += (x0.z + x1.z) + (x2.z + x3.z);
+        acc.w += (x0.w + x1.w) + (x2.w + x3.w);
       }
-      if (k < S) s0 += bpart[(int64_t)k * M + m];
-      bias_out[m] = s0 + s1;
+      for (; k < S; k += 4) {
+        const float4 x = p4[k * st4];
+        acc.x += x.x;
+        acc.y += x.y;
+        acc.z += x.z;
+        acc.w += x.w;
+      }
     }
+    red[g][j] = acc;
+    __syncthreads();
+    if (g == 0 && ok) {
+      const float4 a = red[0][j], b = red[1][j], c = red[2][j], d = red[3][j];
+      const float4 r = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
+                                   (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
+      const int64_t e = e4 * 4, m = e / N, n = e - m * N;
+      *reinterpret_cast<float4*>(out + m * ld + n) = r;
+    }
+    return;
   }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)M * N;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += part[k * stride + i];
-    const int64_t m = i / N, n = i - m * N;
-    out[m * ld + n] = s;
-  }
+  // bias: 64 rows x 4 slab groups per block
+  float* redf = reinterpret_cast<float*>(&red[0][0]);
+  const int64_t m = (int64_t)(blockIdx.x - nb_main) * 64 + j;
+  float acc = 0.f;
+  if (m < M)
+    for (int k = g; k < S; k += 4) acc += bpart[(int64_t)k * M + m];
+  redf[g * 64 + j] = acc;
+  __syncthreads();
+  if (g == 0 && m < M)
+    bias_out[m] = (redf[j] + redf[64 + j]) + (redf[128 + j] + redf[192 + j]);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -757,8 +812,14 @@ int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, 
 
 int launch_reduce_slabs_2d(const float* part, int S, int64_t stride, int M, int N, float* out,
                            int64_t ld, const float* bpart, float* bias_out, hipStream_t st) {
-  hipLaunchKernelGGL(reduce_slabs_2d_kernel, dim3(grid_for((int64_t)M * N, 256, 1024)), dim3(256), 0,
-                     st, part, S, stride, M, N, out, ld, bpart, bias_out);
+  PS_REQUIRE(N % 4 == 0 && ld % 4 == 0 && stride % 4 == 0 &&
+                 (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                 (reinterpret_cast<uintptr_t>(part) & 15) == 0,
+             kErrArg, "reduce_slabs: needs 16-byte aligned rows");
+  const int nb_main = (int)ceil_div((int64_t)M * N / 4, 64);
+  const int nb_bias = bias_out ? (int)ceil_div(M, 64) : 0;
+  hipLaunchKernelGGL(reduce_slabs_2d_kernel, dim3(nb_main + nb_bias), dim3(256), 0, st, part, S, stride,
+                     M, N, out, ld, bpart, bias_out, nb_main);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -853,7 +914,8 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   hipLaunchKernelGGL(loss_triple_kernel, dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, margin,
                      feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart);
   PS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(loss_finish_kernel, dim3(grid_for(S_max * d, 256, 1024)), dim3(256), 0, st, G,
+  PS_REQUIRE(d <= 1024, kErrArg, "loss: out_dim must be <= 1024");
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(grid_for(S_max * d, 1024, 256)), dim3(1024), 0, st, G,
                      Kc, S_max, nS, d, dZ, part, nblk, colpart, B, scal);
   PS_CHECK_LAUNCH();
   return kOk;

@@ -154,15 +154,16 @@ static size_t carve(size_t& cur, int64_t bytes) {
 }
 
 // Split-K weight gradients (C[M][N] = A^T B over K data rows): pick the block
-// tile and split count so that tiles x splits fills the 256 CUs with >= 64 rows
-// per split; small outputs (128 x 128 head weights) fall back to 32 x 128 tiles.
+// tile and split count so that tiles x splits gives ~2 blocks per CU with >= 128
+// rows per split (the slabs cost S*M*N*8 bytes of traffic, so no more splits than
+// that); small outputs (128 x 128 head weights) fall back to 32 x 128 tiles.
 constexpr int kMaxSplits = 64;
 static void choose_wgrad(int64_t M, int64_t N, int64_t Kest, int* cfg, int* splits) {
   static const int bm[3] = {128, 64, 32};
   for (int c = 0; c < 3; ++c) {
     const int64_t tiles = ((M + bm[c] - 1) / bm[c]) * ((N + 127) / 128);
-    int64_t s = std::max<int64_t>(1, 512 / tiles);
-    s = std::min<int64_t>(s, std::max<int64_t>(1, Kest / 64));
+    int64_t s = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+    s = std::min<int64_t>(s, std::max<int64_t>(1, Kest / 128));
     s = std::min<int64_t>(s, kMaxSplits);
     if (tiles * s >= 256 || c == 2) {
       *cfg = c;
@@ -171,7 +172,6 @@ static void choose_wgrad(int64_t M, int64_t N, int64_t Kest, int* cfg, int* spli
     }
   }
 }
-
 
 static void layout(Engine& E) {
   const EngineConfig& c = E.cfg;
