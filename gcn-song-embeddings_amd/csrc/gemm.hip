@@ -1,155 +1,163 @@
 // fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32: exact fp32 FMA chain, 64 FLOP/clk/SIMD
 // on gfx950; there is no xf32 path, and the reference computes in fp32).
 //
-// Block tile 128x128x16, 256 threads = 4 waves in 2x2, each wave 64x64 =
-// 2x2 MFMA tiles of 32x32 (64 accumulator registers).  Operand tiles are staged
-// global -> registers -> LDS (double-buffered, one barrier per k-tile) in a
-// k-major [BK][128+4] image whatever the global layout, so every MFMA operand
-// fragment is one conflict-free ds_read_b32 (lanes 0-31: 32 consecutive rows of
-// one k; lanes 32-63: the next k).  Persistent grid: tiles are dealt so that
-// the column tiles of one row panel (or the tiles of one split-K slice) share
-// an XCD's L2 (blocks b and b+8 land on one XCD).
+// Block tiles of BM x 128 (BM = 128 / 64 / 32), 256 threads = 4 waves, each
+// wave TM x TN MFMA tiles of 32x32.  Operands are staged HBM -> LDS with
+// global_load_lds (LDS-DMA, 16 B per lane, no staging registers) into a ring of
+// three stage buffers: stage t is computed while t+1 and t+2 are in flight,
+// retired by a counted s_waitcnt vmcnt and a raw s_barrier (a __syncthreads
+// would drain the DMA queue).  K-major images are [R][BK] with 16-B chunks
+// XOR-swizzled by row (conflict-free ds_read_b128 fragments; the swizzle is
+// applied on the per-lane SOURCE address, the DMA writes lane-linearly);
+// MN-major images are linear [BK][R] read with ds_read_b32.  Out-of-range rows,
+// k and columns read clamped in-range addresses; the k-tail is zeroed in LDS
+// after it lands, other garbage only reaches discarded outputs.  Gathered
+// k-row numbers (MN-major operands) are staged in LDS per 1024-row window so
+// that no ordinary VGPR load sits between DMA issue and use.  Persistent grid:
+// the tiles of one row panel (or of one split-K slice) are dealt to blocks
+// b, b+8, ... so they share an XCD's L2.
 #include "gemm.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace ps {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int PADF = 4;  // LDS row padding (floats): conflict-free b32 fragment reads, 16-B aligned rows
+constexpr int kStages = 3;     // LDS ring depth
+constexpr int kIdxWin = 1024;  // gathered k-rows staged in LDS at a time
 
-// Rows of a K-major operand ([row][k] in memory) handled by this thread.
-template <int NV>
-struct KRows {
-  const float* p[NV];
-  const float* p2[NV];
-};
+// One 16-B LDS-DMA per lane (global_load_lds_dwordx4; LDS destination = M0 +
+// 16 * lane).  Issued from inline asm so that hipcc's waitcnt pass, which does
+// not see the counted waits below and drains the whole queue (vmcnt(0)) before
+// LDS reads at control-flow joins, leaves the ring alone; the kernel retires
+// the DMAs itself with s_waitcnt vmcnt(N) before each stage's barrier.
+__device__ __forceinline__ void glds16(const float* g, float* l) {
+  const unsigned lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)l);
+  asm volatile(
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(lds)),
+      "v"(g)
+      : "memory", "m0");
+}
+__device__ __forceinline__ void zero16(float* l) {
+  *reinterpret_cast<float4*>(l) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
 
+// K-major operand: global [row][k] (rows optionally gathered), LDS image
+// [R][BK] with chunk c of row r stored at chunk c ^ swz(r).  Chunk q = j*256 +
+// tid of a stage is this thread's j-th DMA; all of one wave's 64 chunks of an
+// instruction are contiguous in LDS (lane-linear), as the DMA requires.
 template <int R, int BK>
-struct Shape {
-  static constexpr int KV = BK / 4;               // float4 per row per stage (K-major)
-  static constexpr int TOT_K = R * KV;            // float4 per stage, K-major
-  static constexpr int MV = R / 4;                // float4 per k-row (MN-major)
-  static constexpr int TOT_MN = BK * MV;          // float4 per stage, MN-major
-  static constexpr int NV = (TOT_K + 255) / 256;  // float4 per thread (same count both layouts)
-  static constexpr int W = R + PADF;              // MN-major image: [BK][R + 4]
-  static constexpr int WK = BK + 4;               // K-major image:  [R][BK + 4]
-  static constexpr int SZ = (R * WK > BK * W) ? R * WK : BK * W;  // floats per stage
-};
-
-template <int R, int BK>
-__device__ __forceinline__ void kmajor_rows(KRows<(Shape<R, BK>::NV)>& Rw, int tid, int r0, int rmax,
-                                            const float* a, int64_t lda, const int32_t* idx,
-                                            const float* a2, int64_t lda2, const int32_t* idx2) {
-  using S = Shape<R, BK>;
+struct KOp {
+  static constexpr int CPR = BK / 4;
+  static constexpr int NI = R * CPR / 256;
+  static constexpr int SZ = R * BK;  // floats per stage image
+  static_assert(R * CPR % 256 == 0, "whole DMAs per thread");
+  static constexpr int SH = BK == 32 ? 1 : 2;
+  __device__ static __forceinline__ int swz(int row) { return (row >> SH) & (CPR - 1); }
+  __device__ static __forceinline__ float4 frag(const float* img, int row, int k4) {
+    return *reinterpret_cast<const float4*>(img + row * BK + 4 * ((k4 >> 2) ^ swz(row)));
+  }
+  const float* rp[NI];
+  const float* rp2[NI];
+  int lc[NI];
+  __device__ __forceinline__ void init(int tid, int r0, int rmax, const float* a, int64_t lda,
+                                       const int32_t* idx, const float* a2, int64_t lda2,
+                                       const int32_t* idx2) {
 #pragma unroll
-  for (int i = 0; i < S::NV; ++i) {
-    const int lin = tid + 256 * i;
-    const int row = r0 + lin / S::KV;
-    Rw.p[i] = nullptr;
-    Rw.p2[i] = nullptr;
-    if (lin < S::TOT_K && row < rmax) {
-      const int64_t r = idx ? idx[row] : row;
-      Rw.p[i] = a + r * lda;
-      if (a2) {
-        const int64_t r2 = idx2 ? idx2[row] : row;
-        Rw.p2[i] = a2 + r2 * lda2;
-      }
+    for (int j = 0; j < NI; ++j) {
+      const int q = j * 256 + tid, row = q / CPR;
+      lc[j] = 4 * ((q % CPR) ^ swz(row));
+      const int g = r0 + row, rc = g < rmax ? g : rmax - 1;
+      rp[j] = a + (int64_t)(idx ? idx[rc] : rc) * lda;
+      rp2[j] = a2 ? a2 + (int64_t)(idx2 ? idx2[rc] : rc) * lda2 : rp[j];
     }
   }
-}
-
-// K-major operand stage -> registers.  Each float4 chunk picks its K segment
-// on its own (torch.cat along K without a concat buffer), so K1 % 4 == 0 suffices.
-template <int R, int BK>
-__device__ __forceinline__ void kmajor_load(float4 (&v)[(Shape<R, BK>::NV)],
-                                            const KRows<(Shape<R, BK>::NV)>& Rw, int tid, int k0,
-                                            int kend, int K1) {
-  using S = Shape<R, BK>;
+  __device__ __forceinline__ void issue(float* img, int wave, int k0, int kend, int K1) const {
 #pragma unroll
-  for (int i = 0; i < S::NV; ++i) {
-    const int lin = tid + 256 * i;
-    const int k = k0 + (lin % S::KV) * 4;
-    const bool seg2 = K1 >= 0 && k >= K1;
-    const float* base = seg2 ? Rw.p2[i] : Rw.p[i];
-    if (Rw.p[i] && k < kend) v[i] = *reinterpret_cast<const float4*>(base + (seg2 ? k - K1 : k));
-    else v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < NI; ++j) {
+      const int k = min(k0 + lc[j], kend - 4);
+      const float* src = (K1 >= 0 && k >= K1) ? rp2[j] + (k - K1) : rp[j] + k;
+      glds16(src, img + (j * 256 + wave * 64) * 4);
+    }
   }
-}
-// K-major stage image is row-major [R][BK+4]: one ds_write_b128 per float4, and
-// the fragment reader takes 4 consecutive k of a row with one ds_read_b128.
-template <int R, int BK>
-__device__ __forceinline__ void kmajor_store(float* Sm, const float4 (&v)[(Shape<R, BK>::NV)],
-                                             int tid) {
-  using S = Shape<R, BK>;
+  __device__ __forceinline__ void zero_tail(float* img, int tid, int k0, int kend) const {
 #pragma unroll
-  for (int i = 0; i < S::NV; ++i) {
-    const int lin = tid + 256 * i;
-    if (lin >= S::TOT_K) continue;
-    const int row = lin / S::KV, kc = (lin % S::KV) * 4;
-    *reinterpret_cast<float4*>(Sm + row * S::WK + kc) = v[i];
+    for (int j = 0; j < NI; ++j)
+      if (k0 + lc[j] >= kend) zero16(img + (j * 256 + tid) * 4);
   }
-}
+};
 
-// MN-major operand ([k][col] in memory, k rows optionally gathered); columns
-// >= c1 (if c1 >= 0) come from a second matrix a2 (torch.cat along columns)
+// MN-major operand: global [k][col] (k rows optionally gathered; columns >= c1
+// from a second matrix), LDS image linear [BK][R].
 template <int R, int BK>
-__device__ __forceinline__ void mnmajor_load(float4 (&v)[(Shape<R, BK>::NV)], int tid, const float* a,
-                                             int64_t lda, const int32_t* idx, int c0, int cmax,
-                                             int k0, int kend, int c1 = -1,
-                                             const float* a2 = nullptr, int64_t lda2 = 0,
-                                             const int32_t* idx2 = nullptr) {
-  using S = Shape<R, BK>;
-#pragma unroll
-  for (int i = 0; i < S::NV; ++i) {
-    const int lin = tid + 256 * i;
-    const int kr = lin / S::MV, cc = lin % S::MV;
-    const int k = k0 + kr;
-    const int c = c0 + cc * 4;
-    if (lin < S::TOT_MN && k < kend && c < cmax) {
-      if (a2 && c >= c1) {
-        const int64_t r = idx2 ? idx2[k] : k;
-        v[i] = *reinterpret_cast<const float4*>(a2 + r * lda2 + (c - c1));
-      } else {
-        const int64_t r = idx ? idx[k] : k;
-        v[i] = *reinterpret_cast<const float4*>(a + r * lda + c);
-      }
+struct MNOp {
+  static constexpr int CPR = R / 4;
+  static constexpr int NI = BK * CPR / 256;
+  static constexpr int SZ = BK * R;
+  static constexpr int KSTEP = 256 / CPR;  // k-rows between a thread's DMAs
+  static_assert(BK * CPR % 256 == 0 && 256 % CPR == 0, "whole DMAs per thread");
+  __device__ static __forceinline__ float4 frag(const float* img, int col, int k4) {
+    return make_float4(img[(k4 + 0) * R + col], img[(k4 + 1) * R + col], img[(k4 + 2) * R + col],
+                       img[(k4 + 3) * R + col]);
+  }
+  const float* base;
+  int64_t ld;
+  bool gathered;
+  int kr0;
+  __device__ __forceinline__ void init(int tid, int c0, int cmax, const float* a, int64_t lda,
+                                       const int32_t* idx, int c1, const float* a2, int64_t lda2,
+                                       const int32_t* idx2) {
+    kr0 = tid / CPR;
+    const int cc = c0 + 4 * (tid % CPR), cl = cc < cmax ? cc : cmax - 4;
+    if (a2 && cl >= c1) {
+      base = a2 + (cl - c1);
+      ld = lda2;
+      gathered = idx2 != nullptr;
     } else {
-      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      base = a + cl;
+      ld = lda;
+      gathered = idx != nullptr;
     }
   }
-}
-template <int R, int BK>
-__device__ __forceinline__ void mnmajor_store(float* Sm, const float4 (&v)[(Shape<R, BK>::NV)],
-                                              int tid) {
-  using S = Shape<R, BK>;
+  // sidx: LDS window of gathered row numbers starting at k-row wb
+  __device__ __forceinline__ void issue(float* img, int wave, int k0, int kend, const int* sidx,
+                                        int wb) const {
 #pragma unroll
-  for (int i = 0; i < S::NV; ++i) {
-    const int lin = tid + 256 * i;
-    if (lin >= S::TOT_MN) continue;
-    const int kr = lin / S::MV, cc = lin % S::MV;
-    *reinterpret_cast<float4*>(Sm + kr * S::W + cc * 4) = v[i];
+    for (int j = 0; j < NI; ++j) {
+      const int k = min(k0 + kr0 + KSTEP * j, kend - 1);
+      const int64_t r = gathered ? sidx[k - wb] : k;
+      glds16(base + r * ld, img + (j * 256 + wave * 64) * 4);
+    }
   }
-}
-
-// 4 consecutive k (8s + 4h .. +3) of row `row` from a staged image
-template <bool KM, int R, int BK>
-__device__ __forceinline__ float4 frag4(const float* Sm, int row, int k4) {
-  using S = Shape<R, BK>;
-  if (KM) return *reinterpret_cast<const float4*>(Sm + row * S::WK + k4);
-  return make_float4(Sm[(k4 + 0) * S::W + row], Sm[(k4 + 1) * S::W + row],
-                     Sm[(k4 + 2) * S::W + row], Sm[(k4 + 3) * S::W + row]);
-}
+  __device__ __forceinline__ void zero_tail(float* img, int tid, int k0, int kend) const {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      if (k0 + kr0 + KSTEP * j >= kend) zero16(img + (j * 256 + tid) * 4);
+  }
+};
 
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK.
 template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  using SA = Shape<BM, BK>;
-  using SB = Shape<BN, BK>;
-  __shared__ __attribute__((aligned(16))) float As[2][SA::SZ];
-  __shared__ __attribute__((aligned(16))) float Bs[2][SB::SZ];
+  using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
+  using OpB = typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type;
+  constexpr int SZA = OpA::SZ, SZB = OpB::SZ, SZS = SZA + SZB;
+  constexpr int NG = OpA::NI + OpB::NI;  // DMAs per wave per stage
+  constexpr bool GA = !AK, GB = !BKM;    // operands that may need gathered k-rows
+  // ONE __shared__ object: with a second one hipcc emits vmcnt(0) (draining the
+  // DMA ring) before fragment reads that follow a DMA issue.
+  __shared__ __attribute__((aligned(16))) float smem[kStages * SZS + 2 * kIdxWin];
+  float* const sm0 = smem;
+  float* const sm1 = smem + SZS;
+  float* const sm2 = smem + 2 * SZS;
+  int* const sidxA = reinterpret_cast<int*>(smem + kStages * SZS);
+  int* const sidxB = sidxA + kIdxWin;
+
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int M = p.M_dev ? *p.M_dev : p.M;
@@ -166,6 +174,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     G = tiles_m;
     W = tiles_n;
   }
+  const int32_t* idxA = GA ? p.a_idx : nullptr;
+  const int32_t* idxB = GB ? p.b_idx : nullptr;
+  const int32_t* idxB2 = GB ? p.b2_idx : nullptr;
+  const int32_t* idxBw = idxB ? idxB : idxB2;  // one gathered B segment (launch_gemm checks)
+  const bool needA = GA && idxA;
+  const bool needB = GB && (idxB || idxB2);
   // tiles of one row panel (or one split) are dealt to blocks b, b+8, ...:
   // one XCD under round-robin placement, so they share its L2 (speed only)
   const int iters = 8 * ((G + 7) / 8) * W;
@@ -187,11 +201,28 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     const int kb = split * kchunk;
     const int ke = min(K, kb + kchunk);
     const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+    const bool tail = ((ke - kb) % BK) != 0;
 
-    KRows<SA::NV> RA;
-    KRows<SB::NV> RB;
-    if (AK) kmajor_rows<BM, BK>(RA, tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
-    if (BKM) kmajor_rows<BN, BK>(RB, tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
+    OpA opa;
+    OpB opb;
+    if constexpr (AK) opa.init(tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
+    else opa.init(tid, m0, M, p.a, p.lda, idxA, -1, nullptr, 0, nullptr);
+    if constexpr (BKM) opb.init(tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
+    else opb.init(tid, n0, N, p.b, p.ldb, idxB, p.N1, p.b2, p.ldb2, idxB2);
+
+    // gathered k-row numbers of the first window (no DMA is in flight here)
+    int wb = kb;
+    auto fill_idx = [&](int w0) __attribute__((always_inline)) {
+      for (int i = tid; i < kIdxWin; i += 256) {
+        const int k = min(w0 + i, ke - 1);
+        if (needA) sidxA[i] = idxA[k];
+        if (needB) sidxB[i] = idxBw[k];
+      }
+    };
+    if ((needA || needB) && nk > 0) {
+      fill_idx(wb);
+      __syncthreads();
+    }
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -201,69 +232,89 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // Two register stages: the global loads of tile t+2 are issued before the
-    // MFMAs of tile t and written to LDS after those of tile t+1, so two k-tiles
-    // of MFMA work cover the HBM latency of the (row-gathered) operand loads.
-    float4 va0[SA::NV], vb0[SB::NV], va1[SA::NV], vb1[SB::NV];
-    auto load = [&](float4 (&va)[SA::NV], float4 (&vb)[SB::NV], int k0) {
-      if (AK) kmajor_load<BM, BK>(va, RA, tid, k0, ke, p.K1);
-      else mnmajor_load<BM, BK>(va, tid, p.a, p.lda, p.a_idx, m0, M, k0, ke);
-      if (BKM) kmajor_load<BN, BK>(vb, RB, tid, k0, ke, -1);
-      else mnmajor_load<BN, BK>(vb, tid, p.b, p.ldb, p.b_idx, n0, N, k0, ke, p.N1, p.b2, p.ldb2,
-                                p.b2_idx);
-    };
-    auto store = [&](const float4 (&va)[SA::NV], const float4 (&vb)[SB::NV], int buf) {
-      if (AK) kmajor_store<BM, BK>(As[buf], va, tid);
-      else mnmajor_store<BM, BK>(As[buf], va, tid);
-      if (BKM) kmajor_store<BN, BK>(Bs[buf], vb, tid);
-      else mnmajor_store<BN, BK>(Bs[buf], vb, tid);
+    auto issue = [&](int st, float* base) __attribute__((always_inline)) {
+      const int k0 = kb + st * BK;
+      if constexpr (AK) opa.issue(base, wave, k0, ke, p.K1);
+      else opa.issue(base, wave, k0, ke, sidxA, wb);
+      if constexpr (BKM) opb.issue(base + SZA, wave, k0, ke, -1);
+      else opb.issue(base + SZA, wave, k0, ke, sidxB, wb);
     };
     const int h = lane >> 5, l32 = lane & 31;
     const bool do_bias = !AK && p.bias_part && tn == 0 && tid < BM;
     float bsum = 0.f;
     // MFMA k-assignment: in the r-th MFMA of octet s, lane half h supplies
     // k = 8s + 4h + r for both operands (any bijection onto the 8 k works).
-    auto compute = [&](int cur) {
-      if (do_bias) {  // column sums of A^T over this tile's k rows (zero-padded)
+    // Fragments of octet s+1 are read from LDS while octet s's MFMAs run.
+    auto compute = [&](const float* As, const float* Bs) __attribute__((always_inline)) {
+      if (do_bias) {  // column sums of A^T over this tile's k rows (tail zeroed)
 #pragma unroll
-        for (int k = 0; k < BK; ++k) bsum += As[cur][k * SA::W + tid];
+        for (int k = 0; k < BK; ++k) bsum += As[k * BM + tid];
       }
-#pragma unroll
-      for (int s8 = 0; s8 < BK / 8; ++s8) {
+      auto rd = [&](float4 (&fa)[TM], float4 (&fb)[TN], int s8) __attribute__((always_inline)) {
         const int k4 = 8 * s8 + 4 * h;
-        float4 a[TM], b[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = frag4<AK, BM, BK>(As[cur], (wm * TM + i) * 32 + l32, k4);
+        for (int i = 0; i < TM; ++i) fa[i] = OpA::frag(As, (wm * TM + i) * 32 + l32, k4);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = frag4<BKM, BN, BK>(Bs[cur], (wn * TN + j) * 32 + l32, k4);
+        for (int j = 0; j < TN; ++j) fb[j] = OpB::frag(Bs, (wn * TN + j) * 32 + l32, k4);
+      };
+      auto mm = [&](const float4 (&fa)[TM], const float4 (&fb)[TN]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
           }
+      };
+      static_assert((BK / 8) % 2 == 0, "octets are processed in pairs");
+      float4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+      rd(fa0, fb0, 0);
+#pragma unroll
+      for (int s8 = 0; s8 < BK / 8; s8 += 2) {
+        rd(fa1, fb1, s8 + 1);
+        mm(fa0, fb0);
+        if (s8 + 2 < BK / 8) rd(fa0, fb0, s8 + 2);
+        mm(fa1, fb1);
       }
     };
-    if (nk > 0) {
-      load(va0, vb0, kb);
-      store(va0, vb0, 0);
-    }
-    if (nk > 1) load(va1, vb1, kb + BK);
-    __syncthreads();
-    for (int it = 0; it < nk; it += 2) {
-      if (it + 2 < nk) load(va0, vb0, kb + (it + 2) * BK);
-      compute(0);
-      if (it + 1 < nk) store(va1, vb1, 1);
-      __syncthreads();
+
+    // ring: stage t is computed from its slot while t+1 and t+2 are in flight
+    auto step = [&](int it, float* cur, float* nxt2) __attribute__((always_inline)) {
+      // retire this wave's DMAs of stage it (stage it+1's NG may stay in flight)
+      if (it + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tail && it == nk - 1) {  // zero the k-tail this thread's DMAs brought in
+        const int k0 = kb + it * BK;
+        opa.zero_tail(cur, tid, k0, ke);
+        opb.zero_tail(cur + SZA, tid, k0, ke);
+      }
+      // publish stage it; every wave is done reading stage it-1's slot (= nxt2)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (it + 2 < nk) {
+        const int k2 = kb + (it + 2) * BK;
+        if ((needA || needB) && k2 >= wb + kIdxWin) {  // next window of row numbers
+          wb += kIdxWin;
+          fill_idx(wb);
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        issue(it + 2, nxt2);
+      }
+      compute(cur, cur + SZA);
+    };
+    if (nk > 0) issue(0, sm0);
+    if (nk > 1) issue(1, sm1);
+    for (int it = 0; it < nk; it += 3) {
+      step(it, sm0, sm2);
       if (it + 1 >= nk) break;
-      if (it + 3 < nk) load(va1, vb1, kb + (it + 3) * BK);
-      compute(1);
-      if (it + 2 < nk) store(va0, vb0, 0);
-      __syncthreads();
+      step(it + 1, sm1, sm0);
+      if (it + 2 >= nk) break;
+      step(it + 2, sm2, sm1);
     }
+    __syncthreads();  // stage buffers are reused by the epilogue / next tile
 
     // ------------------------------------------------------------ epilogue
     // acc[i][j][r] -> row m0 + (wm*TM+i)*32 + (r&3) + 8*(r>>2) + 4*h, col n0 + (wn*TN+j)*32 + l32
@@ -283,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
           }
         }
     } else if (p.epi == kEpiL2Norm) {
-      float* red = &As[0][0];  // [WN][BM] row partial sums (LDS free after the k loop)
+      float* red = smem;  // [WN][BM] row partial sums (LDS free after the k loop)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -389,6 +440,10 @@ int launch_gemm(const GemmParams& p, hipStream_t st) {
   PS_REQUIRE(p.N > 0 && Mmax >= 0 && Kmax >= 0, kErrArg, "gemm: bad sizes");
   if (Mmax == 0) return kOk;
   PS_REQUIRE(p.K % 4 == 0 || p.K_dev, kErrArg, "gemm: K must be a multiple of 4");
+  PS_REQUIRE(!p.K_dev || (!p.a_kmajor && !p.b_kmajor), kErrArg,
+             "gemm: a device-side K needs M-major A and N-major B");
+  PS_REQUIRE(!(p.b_idx && p.b2_idx) || p.b_idx == p.b2_idx, kErrArg,
+             "gemm: at most one gathered B segment");
   PS_REQUIRE(p.K1 < 0 || (p.K1 % 4 == 0 && p.a_kmajor && p.a2), kErrArg,
              "gemm: second K segment must start on a multiple of 4");
   PS_REQUIRE(p.a_kmajor || (p.M % 4 == 0 && !p.M_dev), kErrArg,
