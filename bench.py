@@ -103,6 +103,21 @@ def kernel_table(engine):
     return out
 
 
+def pmc_traffic(config, site):
+    """HBM bytes per launch of `site` from the newest committed rocprofv3 --pmc
+    summary (profiles/rNN/pmc_<config>_*.json, written by the PMC passes that
+    tools/pmc_summary.py documents); None when there is none for this config."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"pmc_{config}_*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("site") == site and d.get("config") == config:
+            return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
     """The oracle's restatement of the reference train step (dense clone
     put_embeddings, f64 aggregation, torch CPU) on the same workload."""
@@ -238,6 +253,7 @@ def main():
     a_avg = a_ms / max(a_calls, 1)
     agg_bytes = F0 * T * hid * 4 + F0 * T * 8 + F0 * hid * 4
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "calls": v[1]} for k, v in sorted(kt.items())}
+    traffic, traffic_src = pmc_traffic(args.config, "fwd.q_gemm.l0")
     result = {
         "metric": "PinSAGE train-step nodes/sec (2-hop, batch 512) at 1/2/4/8 MI355X",
         "value": value,
@@ -258,8 +274,10 @@ def main():
                    "batch_rng": "mt19937 (reference-exact)"},
         "roofline": {"bound": "mfma", "kernel": "fwd.q_gemm.l0 (gather + fp32 MFMA Q projection)",
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
-                     "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg},
+                     "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg,
+                     "algorithmic_bytes_per_launch": 4.0 * (U0 * d + d * hid + U0 * hid)},
         "gather_kernel": {"kernel": "fwd.agg.l0", "bound": "hbm", "avg_launch_ms": a_avg,
                           "achieved_GBs": agg_bytes / (a_avg * 1e-3) / 1e9 if a_avg > 0 else 0.0,
                           "peak_GBs": PEAK_HBM_GBS, "algorithmic_bytes": agg_bytes},
