@@ -125,10 +125,12 @@ __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restri
                                                          const int* __restrict__ nS, int T,
                                                          const int* __restrict__ nN,
                                                          int* __restrict__ cnt,
-                                                         float* __restrict__ zero_rows, int zero_n) {
+                                                         float* __restrict__ zero_rows, int zero_n,
+                                                         int* __restrict__ nsplit) {
   extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
   const int U = *nN;
+  if (nsplit && blockIdx.x == 0 && threadIdx.x == 0) *nsplit = 0;  // the scan appends to it
   if (zero_rows) {  // the dq output receives atomics at chunk boundaries
     float4* z4 = reinterpret_cast<float4*>(zero_rows);
     const int64_t tot = (int64_t)U * zero_n / 4;
@@ -163,102 +165,164 @@ __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restri
   }
 }
 
-// exclusive scan of cnt[0..*n) into off[0..*n] (off[n] = total); one block per
-// 1024 entries, each block sums its predecessors' totals itself.
+// Exclusive scans of cnt[0..*n) into off[0..*n] (off[n] = total) and of the
+// per-row chunk counts ceil(cnt/kDqChunk), emitting the chunk list the dq
+// kernel walks: chunk = {row u, first occurrence}, at most kDqChunk
+// occurrences, never spanning two rows.  cnt is zeroed behind the read (kept
+// zero for the next step).  Multi-block form: one block per 1024 rows, each
+// block sums its predecessors' totals itself.
+constexpr int kDqChunk = 16;
 constexpr int kScanB = 256, kScanPer = 4, kScanChunk = kScanB * kScanPer;
-__global__ __launch_bounds__(kScanB) void scan_block_sums_kernel(const int* __restrict__ cnt,
-                                                                 const int* __restrict__ n_dev,
-                                                                 int* __restrict__ bsum) {
-  __shared__ int red[kScanB / 64];
-  const int64_t n = *n_dev;
-  const int64_t i0 = (int64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
-  int c = 0;
-  for (int q = 0; q < kScanPer; ++q)
-    if (i0 + q < n) c += cnt[i0 + q];
-  c = wave_sum_i(c);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-__global__ __launch_bounds__(kScanB) void scan_apply_kernel(int* __restrict__ cnt,
-                                                            const int* __restrict__ n_dev,
-                                                            const int* __restrict__ bsum,
-                                                            int* __restrict__ off,
-                                                            int* __restrict__ cursor) {
-  __shared__ int ws[kScanB / 64];
-  __shared__ int base_sh;
-  const int64_t n = *n_dev;
-  if ((int64_t)blockIdx.x * kScanChunk > n) return;
-  int o = 0;
-  for (int i = threadIdx.x; i < (int)blockIdx.x; i += kScanB) o += bsum[i];
-  o = wave_sum_i(o);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = o;
-  __syncthreads();
-  if (threadIdx.x == 0) base_sh = ws[0] + ws[1] + ws[2] + ws[3];
-  __syncthreads();
-  const int base = base_sh;
-  __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
-  int v[kScanPer], c = 0;
-  for (int q = 0; q < kScanPer; ++q) {
-    v[q] = (i0 + q < n) ? cnt[i0 + q] : 0;
-    c += v[q];
-  }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int inc = c;
-  for (int s = 1; s < 64; s <<= 1) {
-    int y = __shfl_up(inc, s, 64);
-    if (lane >= s) inc += y;
-  }
-  if (lane == 63) ws[wv] = inc;
-  __syncthreads();
-  int wo = 0;
-  for (int i = 0; i < wv; ++i) wo += ws[i];
-  int p = base + wo + inc - c;
-  for (int q = 0; q < kScanPer; ++q) {
-    if (i0 + q < n) {
-      off[i0 + q] = p;
-      cursor[i0 + q] = p;
-      ((int*)cnt)[i0 + q] = 0;
-    }
-    if (i0 + q == n) off[n] = p;
-    p += v[q];
-  }
-}
-// exclusive scan of cnt[0..U) into off[0..U] and cursor, zeroing cnt behind the
-// read (self-cleaning for the next step); one block, U <= 1024 * 64
-__global__ __launch_bounds__(1024) void scan_small_kernel(int* __restrict__ cnt,
-                                                          const int* __restrict__ n_dev,
-                                                          int* __restrict__ off,
-                                                          int* __restrict__ cursor) {
-  __shared__ int wsum[16];
-  const int U = *n_dev;
-  const int per = (U + 1023) / 1024;
-  const int i0 = threadIdx.x * per;
-  int c = 0;
-  for (int q = 0; q < per; ++q)
-    if (i0 + q < U) c += cnt[i0 + q];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int inc = c;
+__device__ __forceinline__ int n_chunks(int c) { return (c + kDqChunk - 1) / kDqChunk; }
+__device__ __forceinline__ void wave_scan2(int& a, int& b, int lane) {
   for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
+    const int ya = __shfl_up(a, o, 64), yb = __shfl_up(b, o, 64);
+    if (lane >= o) {
+      a += ya;
+      b += yb;
+    }
   }
-  if (lane == 63) wsum[wv] = inc;
-  __syncthreads();
-  int p = inc - c;
-  for (int i = 0; i < wv; ++i) p += wsum[i];
+}
+// off/cursor/chunks for rows i0 .. i0+per-1 from running totals (p, pc); the
+// thread whose range holds index n also writes off[n] and the chunk count
+__device__ __forceinline__ void scan_emit(int* __restrict__ cnt, int64_t i0, int per, int64_t n,
+                                          int& p, int& pc, int* __restrict__ off,
+                                          int* __restrict__ cursor, int2* __restrict__ chunks,
+                                          int* __restrict__ nchunks, int2* __restrict__ split,
+                                          int* __restrict__ nsplit) {
   for (int q = 0; q < per; ++q) {
-    const int i = i0 + q;
-    if (i < U) {
+    const int64_t i = i0 + q;
+    if (i < n) {
       const int v = cnt[i];
       off[i] = p;
       cursor[i] = p;
       cnt[i] = 0;
+      const int nc = n_chunks(v);
+      for (int j = 0; j < nc; ++j) chunks[pc + j] = make_int2((int)i, p + j * kDqChunk);
+      if (nc > 1) split[atomicAdd(nsplit, 1)] = make_int2((int)i, pc);  // order is irrelevant
       p += v;
+      pc += nc;
+    }
+    if (i == n) {
+      off[n] = p;
+      *nchunks = pc;
     }
   }
-  if (threadIdx.x == 1023) off[U] = p;
+}
+__global__ __launch_bounds__(kScanB) void scan_block_sums_kernel(const int* __restrict__ cnt,
+                                                                 const int* __restrict__ n_dev,
+                                                                 int2* __restrict__ bsum) {
+  __shared__ int red[2][kScanB / 64];
+  const int64_t n = *n_dev;
+  const int64_t i0 = (int64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  int c = 0, h = 0;
+  for (int q = 0; q < kScanPer; ++q)
+    if (i0 + q < n) {
+      const int v = cnt[i0 + q];
+      c += v;
+      h += n_chunks(v);
+    }
+  c = wave_sum_i(c);
+  h = wave_sum_i(h);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = c;
+    red[1][threadIdx.x >> 6] = h;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    bsum[blockIdx.x] = make_int2(red[0][0] + red[0][1] + red[0][2] + red[0][3],
+                                 red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+}
+__global__ __launch_bounds__(kScanB) void scan_apply_kernel(int* __restrict__ cnt,
+                                                            const int* __restrict__ n_dev,
+                                                            const int2* __restrict__ bsum,
+                                                            int* __restrict__ off,
+                                                            int* __restrict__ cursor,
+                                                            int2* __restrict__ chunks,
+                                                            int* __restrict__ nchunks,
+                                                            int2* __restrict__ split,
+                                                            int* __restrict__ nsplit) {
+  __shared__ int ws[2][kScanB / 64];
+  const int64_t n = *n_dev;
+  if ((int64_t)blockIdx.x * kScanChunk > n) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int o = 0, oc = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += kScanB) {
+    const int2 b = bsum[i];
+    o += b.x;
+    oc += b.y;
+  }
+  o = wave_sum_i(o);
+  oc = wave_sum_i(oc);
+  if (lane == 0) {
+    ws[0][wv] = o;
+    ws[1][wv] = oc;
+  }
+  __syncthreads();
+  const int base = ws[0][0] + ws[0][1] + ws[0][2] + ws[0][3];
+  const int basec = ws[1][0] + ws[1][1] + ws[1][2] + ws[1][3];
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  int c = 0, h = 0;
+  for (int q = 0; q < kScanPer; ++q)
+    if (i0 + q < n) {
+      const int v = cnt[i0 + q];
+      c += v;
+      h += n_chunks(v);
+    }
+  int inc = c, incc = h;
+  wave_scan2(inc, incc, lane);
+  if (lane == 63) {
+    ws[0][wv] = inc;
+    ws[1][wv] = incc;
+  }
+  __syncthreads();
+  int p = base + inc - c, pc = basec + incc - h;
+  for (int i = 0; i < wv; ++i) {
+    p += ws[0][i];
+    pc += ws[1][i];
+  }
+  scan_emit(cnt, i0, kScanPer, n, p, pc, off, cursor, chunks, nchunks, split, nsplit);
+}
+// single-block form, U <= 1024 * 64
+__global__ __launch_bounds__(1024) void scan_small_kernel(int* __restrict__ cnt,
+                                                          const int* __restrict__ n_dev,
+                                                          int* __restrict__ off,
+                                                          int* __restrict__ cursor,
+                                                          int2* __restrict__ chunks,
+                                                          int* __restrict__ nchunks,
+                                                          int2* __restrict__ split,
+                                                          int* __restrict__ nsplit) {
+  __shared__ int wsum[2][16];
+  const int U = *n_dev;
+  const int per = (U + 1023) / 1024;
+  const int i0 = threadIdx.x * per;
+  int c = 0, h = 0;
+  for (int q = 0; q < per; ++q)
+    if (i0 + q < U) {
+      const int v = cnt[i0 + q];
+      c += v;
+      h += n_chunks(v);
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = c, incc = h;
+  wave_scan2(inc, incc, lane);
+  if (lane == 63) {
+    wsum[0][wv] = inc;
+    wsum[1][wv] = incc;
+  }
+  __syncthreads();
+  int p = inc - c, pc = incc - h;
+  for (int i = 0; i < wv; ++i) {
+    p += wsum[0][i];
+    pc += wsum[1][i];
+  }
+  scan_emit(cnt, i0, per, U, p, pc, off, cursor, chunks, nchunks, split, nsplit);
+  // no range holds index U when U == 1024 * per: thread 1023 ends on the totals
+  if (threadIdx.x == 1023 && U == 1024 * per) {
+    off[U] = p;
+    *nchunks = pc;
+  }
 }
 
 __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restrict__ loc,
@@ -313,109 +377,161 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
   }
 }
 
-// dp_q[u][:] = lrelu'(q[u][:]) * sum_{e in occ(u)} wloc[e] * dagg[e / T][:]
-// Load-balanced segmented reduction over the occurrence list grouped by u:
-// every wave takes a fixed chunk of kSegChunk positions (popular tracks sit in
-// thousands of neighbour lists, so one-wave-per-u would serialise them).  A
-// segment wholly inside a chunk is stored; a segment cut by a chunk boundary
-// is added with f32 atomics into the pre-zeroed output.  lrelu' is applied to
-// each partial (it is a per-element factor).
-constexpr int kSegChunk = 32;
-
+// dpq[u] = lrelu'(q[u]) * sum over the occurrences (f, t) of u in the slot
+// table of w[f][t] * dagg[f]   (the transpose of agg, pinsage_model.py:202).
+// One wave per chunk of <= kDqChunk occurrences of ONE row u (chunk list from
+// the CSR scan; popular tracks, in thousands of neighbour lists, span many
+// chunks): the wave issues its q row and all of its dagg rows at once, so a
+// chunk costs one memory round trip.  A row with one chunk is finished here;
+// a row split over several chunks leaves one raw partial per chunk in `part`
+// and dq_combine_kernel sums them in chunk order (deterministic, and no
+// device-scope float atomics: with per-XCD L2s those run at the memory side
+// and serialise on popular rows).
 template <int VEC>
-__device__ __forceinline__ void dq_flush(float* __restrict__ dpq, const float* __restrict__ q, int hid,
-                                         int h4, int c0, int lane, int32_t row, bool atom,
-                                         float4 (&acc)[VEC]) {
-  const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)row * hid);
-  float4* o = reinterpret_cast<float4*>(dpq + (int64_t)row * hid);
-#pragma unroll
-  for (int v = 0; v < VEC; ++v) {
-    const int c = c0 + v * 64 + lane;
-    if (c < h4) {
-      const float4 qq = qr[c];
-      const float4 r = make_float4(acc[v].x * lrelu_grad(qq.x), acc[v].y * lrelu_grad(qq.y),
-                                   acc[v].z * lrelu_grad(qq.z), acc[v].w * lrelu_grad(qq.w));
-      if (atom) {
-        float* of = reinterpret_cast<float*>(o + c);
-        atomicAdd(of, r.x);
-        atomicAdd(of + 1, r.y);
-        atomicAdd(of + 2, r.z);
-        atomicAdd(of + 3, r.w);
-      } else {
-        o[c] = r;
-      }
-    }
-    acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-template <int VEC>
-__global__ __launch_bounds__(256) void dq_segment_kernel(
-    const int32_t* __restrict__ occ, const int32_t* __restrict__ occ_u,
-    const float* __restrict__ wloc, int T, const float* __restrict__ dagg, int64_t ld_dagg,
-    const float* __restrict__ q, int hid, const int* __restrict__ nS, float* __restrict__ dpq) {
-  constexpr int G = 4;  // occurrences whose rows are loaded together
-  const int64_t total = (int64_t)(*nS) * T;
+__global__ __launch_bounds__(256) void dq_chunk_kernel(
+    const int2* __restrict__ chunks, const int* __restrict__ nchunks, const int* __restrict__ off,
+    const int32_t* __restrict__ occ, const float* __restrict__ wloc, int T,
+    const float* __restrict__ dagg, int64_t ld_dagg, const float* __restrict__ q, int hid,
+    float* __restrict__ dpq, float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int h4 = hid >> 2;
-  for (int64_t ch = wid; ch * kSegChunk < total; ch += nw) {
-    const int64_t p0 = ch * kSegChunk;
-    const int n = (int)min((int64_t)kSegChunk, total - p0);
-    int32_t my_u = -1, my_e = 0;
+  const int nch = *nchunks;
+  for (int64_t ci = wid; ci < nch; ci += nw) {
+    const int2 ch = chunks[ci];
+    const int u = ch.x, p0 = ch.y;
+    const int s0 = off[u], s1 = off[u + 1];
+    const int n = min(kDqChunk, s1 - p0);
+    const bool split = s1 - s0 > kDqChunk;
+    int32_t my_row = 0;
     float my_w = 0.f;
     if (lane < n) {
-      my_u = occ_u[p0 + lane];
-      my_e = occ[p0 + lane];
-      my_w = wloc[my_e];
+      const int32_t e = occ[p0 + lane];
+      my_row = e / T;
+      my_w = wloc[e];
     }
-    const int32_t u_before = p0 > 0 ? occ_u[p0 - 1] : -1;
-    const int32_t u_after = p0 + n < total ? occ_u[p0 + n] : -1;
     for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
+      float4 qv[VEC], x[kDqChunk][VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const int c = min(c0 + v * 64 + lane, h4 - 1);
+        qv[v] = reinterpret_cast<const float4*>(q + (int64_t)u * hid)[c];
+      }
+      // rows in groups of 4 (n is wave-uniform, so the group tests are scalar
+      // branches); every load is issued before the first use, and a partial
+      // group repeats its last row (a cache hit) instead of branching per row
+      const int ng = (n + 3) >> 2;
+#pragma unroll
+      for (int g = 0; g < kDqChunk / 4; ++g) {
+        if (g < ng) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * g + jj;
+            const int32_t row = __shfl(my_row, min(j, n - 1), 64);
+            const float4* dr = reinterpret_cast<const float4*>(dagg + (int64_t)row * ld_dagg);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) x[j][v] = dr[min(c0 + v * 64 + lane, h4 - 1)];
+          }
+        }
+      }
       float4 acc[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-      int32_t cur = __shfl(my_u, 0, 64);
-      bool first = true;  // the current segment started at this chunk's first position
-      for (int j0 = 0; j0 < n; j0 += G) {
-        float4 x[G][VEC];
-        int32_t uu[G];
-        float ww[G];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const int j = j0 + g;
-          const int jj = j < n ? j : n - 1;
-          uu[g] = __shfl(my_u, jj, 64);
-          ww[g] = __shfl(my_w, jj, 64);
-          const int32_t e = __shfl(my_e, jj, 64);
-          const float4* dr = reinterpret_cast<const float4*>(dagg + (int64_t)(e / T) * ld_dagg);
+      for (int g = 0; g < kDqChunk / 4; ++g) {
+        if (g < ng) {
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) {
-            const int c = c0 + v * 64 + lane;
-            x[g][v] = (c < h4 && j < n) ? dr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          if (j0 + g < n) {
-            if (uu[g] != cur) {
-              dq_flush<VEC>(dpq, q, hid, h4, c0, lane, cur, first && cur == u_before, acc);
-              cur = uu[g];
-              first = false;
-            }
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * g + jj;
+            const float w = j < n ? __shfl(my_w, j, 64) : 0.f;
 #pragma unroll
             for (int v = 0; v < VEC; ++v) {
-              acc[v].x = fmaf(ww[g], x[g][v].x, acc[v].x);
-              acc[v].y = fmaf(ww[g], x[g][v].y, acc[v].y);
-              acc[v].z = fmaf(ww[g], x[g][v].z, acc[v].z);
-              acc[v].w = fmaf(ww[g], x[g][v].w, acc[v].w);
+              acc[v].x = fmaf(w, x[j][v].x, acc[v].x);
+              acc[v].y = fmaf(w, x[j][v].y, acc[v].y);
+              acc[v].z = fmaf(w, x[j][v].z, acc[v].z);
+              acc[v].w = fmaf(w, x[j][v].w, acc[v].w);
             }
           }
         }
       }
-      dq_flush<VEC>(dpq, q, hid, h4, c0, lane, cur, (first && cur == u_before) || cur == u_after,
-                    acc);
+      float4* o = reinterpret_cast<float4*>(split ? part + ci * hid : dpq + (int64_t)u * hid);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const int c = c0 + v * 64 + lane;
+        if (c < h4)
+          o[c] = split ? acc[v]
+                       : make_float4(acc[v].x * lrelu_grad(qv[v].x), acc[v].y * lrelu_grad(qv[v].y),
+                                     acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
+      }
+    }
+  }
+}
+
+// dpq[u] = lrelu'(q[u]) * (sum of u's chunk partials) for the rows
+// dq_chunk_kernel split (the scan's split list: {u, first chunk}).  One
+// 1024-thread block per row: wave w sums partials j = w, w + 16, ... with 8
+// loads in flight per lane, then the 16 wave sums are added in a fixed order in
+// LDS (deterministic).  Popular rows have hundreds of partials, so a row's sum
+// is spread over a block rather than one wave.
+constexpr int kCombWaves = 16;
+__global__ __launch_bounds__(1024) void dq_combine_kernel(const int2* __restrict__ split,
+                                                          const int* __restrict__ nsplit,
+                                                          const int* __restrict__ off,
+                                                          const float* __restrict__ part,
+                                                          const float* __restrict__ q, int hid,
+                                                          float* __restrict__ dpq) {
+  __shared__ float4 red[kCombWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h4 = hid >> 2;
+  const int ns = *nsplit;
+  for (int si = blockIdx.x; si < ns; si += gridDim.x) {
+    const int2 sp = split[si];
+    const int u = sp.x;
+    const int64_t ci = sp.y;
+    const int k = (off[u + 1] - off[u] + kDqChunk - 1) / kDqChunk;
+    for (int c0 = 0; c0 < h4; c0 += 64) {
+      const int c = c0 + lane;
+      const int cc = min(c, h4 - 1);
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      int j = wv;
+      for (; j + 7 * kCombWaves < k; j += 8 * kCombWaves) {
+        float4 x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          x[i] = reinterpret_cast<const float4*>(part + (ci + j + i * kCombWaves) * hid)[cc];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc.x += x[i].x;
+          acc.y += x[i].y;
+          acc.z += x[i].z;
+          acc.w += x[i].w;
+        }
+      }
+      for (; j < k; j += kCombWaves) {
+        const float4 x = reinterpret_cast<const float4*>(part + (ci + j) * hid)[cc];
+        acc.x += x.x;
+        acc.y += x.y;
+        acc.z += x.z;
+        acc.w += x.w;
+      }
+      red[wv][lane] = acc;
+      __syncthreads();
+      if (wv == 0 && c < h4) {
+        float4 t = red[0][lane];
+        for (int i = 1; i < kCombWaves; ++i) {
+          const float4 x = red[i][lane];
+          t.x += x.x;
+          t.y += x.y;
+          t.z += x.z;
+          t.w += x.w;
+        }
+        const float4 qq = reinterpret_cast<const float4*>(q + (int64_t)u * hid)[c];
+        reinterpret_cast<float4*>(dpq + (int64_t)u * hid)[c] =
+            make_float4(t.x * lrelu_grad(qq.x), t.y * lrelu_grad(qq.y), t.z * lrelu_grad(qq.z),
+                        t.w * lrelu_grad(qq.w));
+      }
+      __syncthreads();
     }
   }
 }
@@ -856,21 +972,31 @@ int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, i
 // CSR of the neighbour slots by q row.  cnt must be zero on entry (zeroed once
 // by pinsage_engine_init_workspace, then left zero by the scan).  The count
 // kernel also zeroes dpq's rows (the dq kernel's atomic targets).
+// CSR of the neighbour slots by q row, plus the dq chunk list.  cnt must be
+// zero on entry (zeroed once by pinsage_engine_init_workspace, then left zero
+// by the scan).
 int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, const int* nN,
                      int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int32_t* occ,
-                     int32_t* occ_u, float* dpq, int hid, hipStream_t st) {
+                     int32_t* occ_u, int2* chunks, int* nchunks, int2* split, int* nsplit,
+                     float* dpq, int hid, hipStream_t st) {
   const int lds = (int)std::min<int64_t>(N_max, kLdsRows) * 4;
   const int gb = std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
-  hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt, dpq, hid);
+  // dq writes every row it owns (no atomics), so dpq needs no zeroing
+  (void)dpq;
+  hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt,
+                     (float*)nullptr, hid, nsplit);
   PS_CHECK_LAUNCH();
   if (N_max <= 1024 * 64) {
-    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor);
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor, chunks,
+                       nchunks, split, nsplit);
     PS_CHECK_LAUNCH();
   } else {
     const int nb = ceil_div(N_max + 1, kScanChunk);
-    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum);
+    int2* bs = reinterpret_cast<int2*>(bsum);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bs);
     PS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bsum, off, cursor);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bs, off, cursor,
+                       chunks, nchunks, split, nsplit);
     PS_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cursor, occ,
@@ -879,18 +1005,28 @@ int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, co
   return kOk;
 }
 
-int launch_dq_segment(const int32_t* occ, const int32_t* occ_u, const float* wloc, int T,
-                      const float* dagg, int64_t ld_dagg, const float* q, int hid, const int* nS,
-                      int64_t S_max, const int* nN, int64_t N_max, float* dpq, hipStream_t st) {
-  PS_REQUIRE(hid % 4 == 0, kErrArg, "dq_segment: hidden dim must be a multiple of 4");
-  const int64_t chunks = (S_max * T + kSegChunk - 1) / kSegChunk;
-  const int grid = grid_for(chunks * 64, 256, 4096);
+// upper bound of the dq chunk list: one partial chunk per row plus full ones
+int64_t dq_chunk_capacity(int64_t S_max, int T, int64_t N_max) {
+  return N_max + (S_max * T + kDqChunk - 1) / kDqChunk + 1;
+}
+// upper bound of the split-row list: a split row holds more than kDqChunk slots
+int64_t dq_split_capacity(int64_t S_max, int T) { return S_max * T / (kDqChunk + 1) + 1; }
+
+int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks, const int2* split,
+                     const int* nsplit, int64_t max_split, const int* off, const int32_t* occ,
+                     const float* wloc, int T, const float* dagg, int64_t ld_dagg, const float* q,
+                     int hid, float* dpq, float* part, hipStream_t st) {
+  PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
+  const int grid = grid_for(max_chunks * 64, 256, 8192);
   if (hid >= 512)
-    hipLaunchKernelGGL((dq_segment_kernel<2>), dim3(grid), dim3(256), 0, st, occ, occ_u, wloc, T, dagg,
-                       ld_dagg, q, hid, nS, dpq);
+    hipLaunchKernelGGL((dq_chunk_kernel<2>), dim3(grid), dim3(256), 0, st, chunks, nchunks, off, occ,
+                       wloc, T, dagg, ld_dagg, q, hid, dpq, part);
   else
-    hipLaunchKernelGGL((dq_segment_kernel<1>), dim3(grid), dim3(256), 0, st, occ, occ_u, wloc, T, dagg,
-                       ld_dagg, q, hid, nS, dpq);
+    hipLaunchKernelGGL((dq_chunk_kernel<1>), dim3(grid), dim3(256), 0, st, chunks, nchunks, off, occ,
+                       wloc, T, dagg, ld_dagg, q, hid, dpq, part);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dq_combine_kernel, dim3((int)std::max<int64_t>(1, std::min<int64_t>(max_split, 512))),
+                     dim3(1024), 0, st, split, nsplit, off, part, q, hid, dpq);
   PS_CHECK_LAUNCH();
   return kOk;
 }

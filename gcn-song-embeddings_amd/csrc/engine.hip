@@ -40,10 +40,13 @@ int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_csr_build(const int32_t*, const int*, int64_t, int, const int*, int64_t, int*, int*,
-                     int*, int*, int32_t*, int32_t*, float*, int, hipStream_t);
-int launch_dq_segment(const int32_t*, const int32_t*, const float*, int, const float*, int64_t,
-                      const float*, int, const int*, int64_t, const int*, int64_t, float*,
-                      hipStream_t);
+                     int*, int*, int32_t*, int32_t*, int2*, int*, int2*, int*, float*, int,
+                     hipStream_t);
+int64_t dq_chunk_capacity(int64_t, int, int64_t);
+int64_t dq_split_capacity(int64_t, int);
+int launch_dq_chunks(const int2*, const int*, int64_t, const int2*, const int*, int64_t, const int*,
+                     const int32_t*, const float*, int, const float*, int64_t, const float*, int,
+                     float*, float*, hipStream_t);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
@@ -80,7 +83,8 @@ struct LayerBuf {
   size_t q = 0, agg = 0, y = 0, nrm = 0;
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, occ = 0,
-         occ_u = 0;
+         occ_u = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
+  int64_t max_chunks = 0, max_split = 0;
   // parameter offsets (floats) into the flat param / grad buffers
   int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
 };
@@ -116,7 +120,35 @@ struct Engine {
   float* grads = nullptr;
   float* adam_m = nullptr;
   float* adam_v = nullptr;
+  // backward side streams: [0] transposes (CSR) of the neighbour slots, [1]
+  // weight gradients; forked from / joined to the caller's stream with events
+  hipStream_t side[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev;
+  int ev_next = 0;
+  ~Engine() {
+    for (auto& s : side)
+      if (s) (void)hipStreamDestroy(s);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+  }
 };
+
+// An event from the engine's pool (round-robin; a step records well under
+// kEvents, and a wait binds to the record that precedes it on the host).
+constexpr int kEvents = 32;
+static int ensure_streams(Engine& E) {
+  if (E.side[0]) return kOk;
+  for (auto& s : E.side) PS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  E.ev.resize(kEvents);
+  for (auto& e : E.ev) PS_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return kOk;
+}
+// `to` waits for everything enqueued so far on `from`
+static int dep(Engine& E, hipStream_t from, hipStream_t to) {
+  hipEvent_t e = E.ev[(size_t)(E.ev_next++ % kEvents)];
+  PS_CHECK_HIP(hipEventRecord(e, from));
+  PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+  return kOk;
+}
 
 struct Timed {
   Engine& E;
@@ -231,11 +263,18 @@ static void layout(Engine& E) {
     lb.dagg = carve(cur, FS * c.hid * 4);
     lb.dpq = carve(cur, FN * c.hid * 4);
     lb.cnt = carve(cur, (FN + 1) * 4);
-    lb.bsum = carve(cur, (int64_t)ceil_div(FN + 1, 1024) * 4 + 16);
+    lb.bsum = carve(cur, (int64_t)ceil_div(FN + 1, 1024) * 8 + 16);
     lb.off = carve(cur, (FN + 1) * 4);
     lb.cursor = carve(cur, (FN + 1) * 4);
     lb.occ = carve(cur, FS * T * 4);
     lb.occ_u = carve(cur, FS * T * 4);
+    lb.max_chunks = dq_chunk_capacity(FS, (int)T, FN);
+    lb.chunks = carve(cur, lb.max_chunks * 8);
+    lb.nchunks = carve(cur, 16);
+    lb.dqpart = carve(cur, lb.max_chunks * c.hid * 4);  // partials of split dq rows
+    lb.max_split = dq_split_capacity(FS, (int)T);
+    lb.split = carve(cur, lb.max_split * 8);
+    lb.nsplit = carve(cur, 16);
   }
   const int64_t top = E.L.back().S.cap;
   E.ids = carve(cur, c.max_pos * 8);
@@ -458,9 +497,29 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
   LayerBuf& top = E.L[(size_t)Lc - 1];
   const int o = (int)c.out, hd = (int)c.hid;
   float* gr = E.grads;
+  PS_TRY(ensure_streams(E));
+  hipStream_t s_csr = E.side[0], s_wg = E.side[1];
+  // the transposes of the neighbour slots depend only on the forward: build
+  // them beside the head backward; events mark each layer's CSR done
+  PS_TRY(dep(E, st, s_csr));
+  std::vector<hipEvent_t> csr_done((size_t)Lc);
+  for (int l = Lc - 1; l >= 0; --l) {
+    LayerBuf& lb = E.L[(size_t)l];
+    Timed tc(E, lname("bwd.csr", l), s_csr);
+    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
+                            at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
+                            at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
+                            at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), at<int2>(ws, lb.split),
+                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), hd, s_csr));
+    tc.stop();
+    csr_done[(size_t)l] = E.ev[(size_t)(E.ev_next++ % kEvents)];
+    PS_CHECK_HIP(hipEventRecord(csr_done[(size_t)l], s_csr));
+  }
+  // weight gradients run on s_wg, each forked once its inputs exist on st
   Timed t_hb(E, "bwd.head", st);
-  // head: Z = H1 G2^T, H1 = lrelu(y G1^T + b1)
+  PS_TRY(dep(E, st, s_wg));
   {
+    Timed tw(E, "bwd.wgrad.head", s_wg);
     WGrad w;
     w.A = at<float>(ws, E.dZ);
     w.lda = o;
@@ -473,7 +532,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     w.K_hint = top.S.hint;
     w.dst = gr + E.pG2w;
     w.ld_dst = o;
-    PS_TRY(weight_grad(E, ws, w, st));
+    PS_TRY(weight_grad(E, ws, w, s_wg));
   }
   {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
@@ -493,7 +552,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     p.ldm = o;
     PS_TRY(launch_gemm(p, st));
   }
+  PS_TRY(dep(E, st, s_wg));
   {
+    Timed tw(E, "bwd.wgrad.head", s_wg);
     WGrad w;  // dG1 and db1
     w.A = at<float>(ws, E.dP1);
     w.lda = o;
@@ -507,7 +568,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     w.dst = gr + E.pG1w;
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
-    PS_TRY(weight_grad(E, ws, w, st));
+    PS_TRY(weight_grad(E, ws, w, s_wg));
   }
   {
     GemmParams p;  // dY_top = dP1 G1
@@ -540,7 +601,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
                                  o, cnt(lb.S), lb.S.cap, dp, dYprev, o,
                                  l > 0 ? cnt(E.L[(size_t)l - 1].S) : nullptr,
                                  l == Lc - 1 ? at<int>(ws, E.Kc) : nullptr, 3 * top.S.cap, st));
+    PS_TRY(dep(E, st, s_wg));
     {
+      Timed tw(E, lname("bwd.w_wgrad", l), s_wg);
       WGrad w;  // dW = dp^T [h_self || agg], dWb = colsum(dp)
       w.A = dp;
       w.lda = o;
@@ -558,7 +621,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       w.dst = gr + lb.pWw;
       w.ld_dst = d + hd;
       w.dst_b = gr + lb.pWb;
-      PS_TRY(weight_grad(E, ws, w, st));
+      PS_TRY(weight_grad(E, ws, w, s_wg));
     }
     {
       // [d_self || d_agg] = dp W: columns < d scatter-add into the rows of
@@ -590,16 +653,16 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       }
       PS_TRY(launch_gemm(p, st));
     }
-    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
-                            at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
-                            at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
-                            at<float>(ws, lb.dpq), hd, st));
-    PS_TRY(launch_dq_segment(at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u), at<float>(ws, lb.wloc),
-                             T, at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, cnt(lb.S),
-                             lb.S.cap, cnt(lb.N), lb.N.cap, at<float>(ws, lb.dpq), st));
+    PS_CHECK_HIP(hipStreamWaitEvent(st, csr_done[(size_t)l], 0));
+    PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
+                            at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
+                            at<int>(ws, lb.off), at<int32_t>(ws, lb.occ), at<float>(ws, lb.wloc), T,
+                            at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
+                            at<float>(ws, lb.dqpart), st));
+    PS_TRY(dep(E, st, s_wg));
     {
       // dQ = dpq^T h[q_src], dQb = colsum(dpq)
-      Timed tq(E, lname("bwd.q_wgrad", l), st);
+      Timed tq(E, lname("bwd.q_wgrad", l), s_wg);
       WGrad w;
       w.A = at<float>(ws, lb.dpq);
       w.lda = hd;
@@ -614,7 +677,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       w.dst = gr + lb.pQw;
       w.ld_dst = d;
       w.dst_b = gr + lb.pQb;
-      PS_TRY(weight_grad(E, ws, w, st));
+      PS_TRY(weight_grad(E, ws, w, s_wg));
     }
     if (l > 0) {
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
@@ -635,6 +698,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(launch_gemm(p, st));
     }
   }
+  // every gradient is written once the side streams drain into st
+  PS_TRY(dep(E, s_csr, st));
+  PS_TRY(dep(E, s_wg, st));
   return kOk;
 }
 
