@@ -61,12 +61,17 @@ def build_problem(cfg, seed=0):
     import graph
     import synthetic
     t0 = time.time()
+    log(f"[bench] building synthetic graph: {cfg['n_tracks']} tracks, {cfg['n_cols']} collections, "
+        f"{cfg['memberships']} memberships")
     pg = synthetic.make_playlist_graph(cfg["n_tracks"], cfg["n_cols"], cfg["memberships"], seed=seed)
+    log(f"[bench]   memberships drawn in {time.time()-t0:.1f}s")
     indptr, indices = pg.csr()
     g = graph.CSRGraph.from_csr(indptr, indices)
+    log(f"[bench]   CSR built ({time.time()-t0:.1f}s)")
     rng = np.random.default_rng(seed + 1)
     feats = torch.from_numpy(rng.standard_normal((cfg["n_tracks"], cfg["d_in"]), dtype=np.float32))
-    pos = torch.from_numpy(synthetic.make_positives(pg, 5 * cfg["n_tracks"], seed=seed + 2))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 5 * cfg["n_tracks"], seed=seed + 2,
+                                                    csr=(indptr, indices)))
     log(f"[bench] graph n_all={pg.n_all} edges={pg.n_edges} built in {time.time()-t0:.1f}s")
     return pg, g, feats, pos
 

@@ -163,13 +163,13 @@ struct Timed {
       E.sites.push_back(TimingSite{name, {}, 0.0, 0});
       site = &E.sites.back();
     }
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    hipEventRecord(a, st);
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, st);
   }
   void stop() {
     if (!site) return;
-    hipEventRecord(b, st);
+    (void)hipEventRecord(b, st);
     site->pending.emplace_back(a, b);
     site = nullptr;
   }
@@ -292,7 +292,7 @@ static void layout(Engine& E) {
   int64_t slab = kMaxSplits * c.out * c.out;
   for (auto& lb : E.L) {
     slab = std::max(slab, (int64_t)kMaxSplits * c.hid * lb.d);
-    slab = std::max(slab, (int64_t)kMaxSplits * c.out * std::max(lb.d, c.hid));
+    slab = std::max(slab, (int64_t)kMaxSplits * c.out * (lb.d + c.hid));  // merged [self || agg]
   }
   E.slab_floats = slab;
   E.slab = carve(cur, slab * 4);
@@ -811,8 +811,8 @@ int pinsage_engine_timing(pinsage_engine* e, int enable) {
   Engine* E = reinterpret_cast<Engine*>(e);
   for (auto& t : E->sites)
     for (auto& pr : t.pending) {
-      hipEventDestroy(pr.first);
-      hipEventDestroy(pr.second);
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
     }
   E->sites.clear();
   E->timing = enable != 0;
@@ -828,8 +828,8 @@ int pinsage_engine_timing_collect(pinsage_engine* e) {
       PS_CHECK_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
       t.ms += ms;
       t.calls += 1;
-      hipEventDestroy(pr.first);
-      hipEventDestroy(pr.second);
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
     }
     t.pending.clear();
   }

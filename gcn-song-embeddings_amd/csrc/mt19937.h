@@ -9,6 +9,8 @@
 #include <cstdint>
 #include <cstring>
 
+#include "mt_jump.h"
+
 namespace ps {
 
 struct MTState {
@@ -53,8 +55,22 @@ struct MTState {
   }
   // words available without a twist
   inline int64_t avail() const { return (int64_t)left - 1; }
-  // Advance by n draws without tempering (twist-only); same end state as n draw()s.
+  // Advance by n draws without tempering; same end state as n draw()s.  Long
+  // skips jump over GF(2) (mt_jump.h); short ones twist through.
+  static constexpr int64_t kJumpMin = int64_t(1) << 21;
   void skip(int64_t n) {
+    if (n >= kJumpMin && mtjump::available()) {
+      // the array s holds outputs x_b .. x_{b+623}, of which c are consumed;
+      // jump the window to start at the last skipped output, then resume at
+      // its second word (next = 1, the first is consumed)
+      const int64_t c = 625 - left;
+      uint32_t out[N];
+      mtjump::jump_window(s, c + n - 1, out);
+      std::memcpy(s, out, sizeof(s));
+      next = 1;
+      left = N;
+      return;
+    }
     while (n > 0) {
       int64_t a = avail();
       if (a == 0) {

@@ -105,8 +105,10 @@ def make_playlist_graph(n_tracks: int, n_cols: int, n_memberships: int,
     fix = np.nonzero(cnt < 2)[0]
     if fix.size:
         add_c, add_t = [], []
-        for c in fix:
-            have = set(tracks[cols == c].tolist())
+        lo = np.searchsorted(cols, fix, side="left")   # key is sorted: cols ascending
+        hi = np.searchsorted(cols, fix, side="right")
+        for c, a, b in zip(fix.tolist(), lo.tolist(), hi.tolist()):
+            have = set(tracks[a:b].tolist())
             while len(have) < 2:
                 t = int(rng.integers(n_tracks))
                 if t not in have:
@@ -128,12 +130,12 @@ def make_features(n: int, d: int, seed: int = 1) -> np.ndarray:
     return ((f - mean) / std).astype(np.float32)
 
 
-def make_positives(g: PlaylistGraph, n_pairs: int, seed: int = 3) -> np.ndarray:
+def make_positives(g: PlaylistGraph, n_pairs: int, seed: int = 3, csr=None) -> np.ndarray:
     """Positive pairs (a, b) of distinct tracks sharing a collection ([P, 2] int64).
 
     Stands in for ``generate_positives.py:50`` ("auto" = 5 pairs per track)."""
     rng = np.random.default_rng(seed)
-    indptr, indices = g.csr()
+    indptr, indices = g.csr() if csr is None else csr
     n = g.n_tracks
     a = rng.integers(0, n, size=n_pairs)
     # pick one of a's collections, then one member of it

@@ -230,3 +230,37 @@ def test_batch_sampler_speculation_is_exact():
     for (b1, n1), (b2, n2) in zip(ref[:-1], got[:-1]):
         assert torch.equal(b1, b2) and torch.equal(n1, n2)
         assert torch.equal(n2, b2.flatten().unique())
+
+
+@pytest.mark.parametrize("n", [(1 << 21) + 7, 3_000_017, 12_345_678])
+def test_mt_long_skip_jumps_exactly(n):
+    """Skips of >= 2^21 draws use the GF(2) jump-ahead (mt_jump.h); the state
+    must equal n sequential draws, from any position inside a block."""
+    import _native as nat
+    for pre in (0, 1, 311, 623, 624, 1000):
+        a = nat.MT().seed(1234 + pre)
+        b = nat.MT().seed(1234 + pre)
+        a.draws(pre)
+        b.draws(pre)
+        a.skip(n)
+        # reference: sequential twisting in bounded pieces (below the jump threshold)
+        left = n
+        while left:
+            k = min(left, (1 << 21) - 1)
+            b.skip(k)
+            left -= k
+        assert (a.draws(2000) == b.draws(2000)).all(), (n, pre)
+
+
+def test_randperm_prefix_long_matches_torch():
+    """torch.randperm(5M)[:512] and the generator state after it (jump path)."""
+    import _native as nat
+    n, k = 5_000_000, 512
+    torch.manual_seed(99)
+    with nat.torch_rng() as mt:
+        got = mt.randperm_prefix(n, k)
+    after = int(torch.randint(1000, ()))
+    torch.manual_seed(99)
+    ref = torch.randperm(n)[:k].numpy()
+    assert (got == ref).all()
+    assert int(torch.randint(1000, ())) == after
