@@ -35,12 +35,17 @@ constexpr int kIdxWin = 1024;  // gathered k-rows staged in LDS at a time
 // the DMAs itself with s_waitcnt vmcnt(N) before each stage's barrier.
 __device__ __forceinline__ void glds16(const float* g, float* l) {
   const unsigned lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)l);
+  unsigned saved;
+  // M0 is reserved to the compiler: save and restore it around the DMA
   asm volatile(
-      "s_mov_b32 m0, %0\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(lds)),
-      "v"(g)
-      : "memory", "m0");
+      "global_load_lds_dwordx4 %2, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(g)
+      : "memory");
 }
 __device__ __forceinline__ void zero16(float* l) {
   *reinterpret_cast<float4*>(l) = make_float4(0.f, 0.f, 0.f, 0.f);
