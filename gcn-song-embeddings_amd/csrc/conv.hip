@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
 // block counts its contiguous slice of occurrences in an LDS histogram and
 // flushes one global atomic per row it touched; otherwise lanes of a wave with
 // the same row combine into one global atomic.
-constexpr int kLdsRows = 16384;
+constexpr int kLdsRows = 40960;  // 160 KiB: a workgroup may take all of a CU's LDS
 __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restrict__ loc,
                                                          const int* __restrict__ nS, int T,
                                                          const int* __restrict__ nN,
@@ -774,44 +774,44 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
 }
 
 // ---------------------------------------------------------------- Adam
-// torch.optim.Adam (single-tensor math, weight_decay 0, amsgrad off):
-//   m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2
-//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
-// lr and the step counter live in device memory, so the step can be
-// graph-replayed: every block computes with step[0] + 1, and the last block to
-// take a ticket (step[1]) stores it -- every block has read step[0] by then.
+// torch.optim.Adam step (pinsage_training.py:147,191; torch _single_tensor_adam):
+//   m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2
+//   p -= step_size * m / (sqrt(v) / bc2_sqrt + eps)
+// coef = {step_size = lr / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t)} comes from
+// device memory, written by the host beside the batch ids each step (the host
+// computes them in double exactly as torch does), so the replayed graph needs
+// no step counter on the device.
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float ss, float bc2,
+                                      float beta2, float omb1, float omb2, float eps) {
+  m = m + omb1 * (g - m);
+  v = v * beta2 + omb2 * g * g;
+  const float denom = sqrtf(v) / bc2 + eps;
+  p = p - ss * (m / denom);
+}
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   int64_t n, const float* __restrict__ lr_dev,
-                                                   int* __restrict__ step_dev, float beta1,
-                                                   float beta2, float eps) {
-  const int new_step = step_dev[0] + 1;
-  const double step = (double)new_step;
-  const double lr = (double)(*lr_dev);
-  const double bc1 = 1.0 - pow((double)beta1, step);
-  const double bc2s = sqrt(1.0 - pow((double)beta2, step));
-  const float step_size = (float)(lr / bc1);
-  const float bc2f = (float)bc2s;
+                                                   int64_t n, const float* __restrict__ coef,
+                                                   float beta1, float beta2, float eps) {
+  const float ss = coef[0], bc2 = coef[1];
   const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    float mi = m[i];
-    mi = mi + omb1 * (gi - mi);
-    float vi = v[i] * beta2 + omb2 * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2f + eps;
-    p[i] = p[i] - step_size * (mi / denom);
+  const int64_t n4 = n >> 2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, ts = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = t0; i < n4; i += ts) {
+    float4 pp = p4[i], mm = m4[i], vv = v4[i];
+    const float4 gg = g4[i];
+    adam1(pp.x, gg.x, mm.x, vv.x, ss, bc2, beta2, omb1, omb2, eps);
+    adam1(pp.y, gg.y, mm.y, vv.y, ss, bc2, beta2, omb1, omb2, eps);
+    adam1(pp.z, gg.z, mm.z, vv.z, ss, bc2, beta2, omb1, omb2, eps);
+    adam1(pp.w, gg.w, mm.w, vv.w, ss, bc2, beta2, omb1, omb2, eps);
+    p4[i] = pp;
+    m4[i] = mm;
+    v4[i] = vv;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int t = atomicAdd(step_dev + 1, 1);
-    if (t == (int)gridDim.x - 1) {
-      step_dev[0] = new_step;
-      step_dev[1] = 0;
-    }
-  }
+  for (int64_t i = 4 * n4 + t0; i < n; i += ts) adam1(p[i], g[i], m[i], v[i], ss, bc2, beta2, omb1, omb2, eps);
 }
 
 // out[i][:] = Z[pos_rank[i]][:]
@@ -975,6 +975,21 @@ int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, i
 // CSR of the neighbour slots by q row, plus the dq chunk list.  cnt must be
 // zero on entry (zeroed once by pinsage_engine_init_workspace, then left zero
 // by the scan).
+// dynamic LDS above 64 KiB must be allowed per kernel (once, outside capture)
+int csr_prepare() {
+  static int rc = [] {
+    if (hipFuncSetAttribute((const void*)csr_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kLdsRows * 4) != hipSuccess)
+      return (int)kErrHip;
+    if (hipFuncSetAttribute((const void*)csr_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kLdsRows * 4) != hipSuccess)
+      return (int)kErrHip;
+    return (int)kOk;
+  }();
+  if (rc != kOk) set_error("csr: cannot raise the dynamic LDS limit");
+  return rc;
+}
+
 int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, const int* nN,
                      int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int32_t* occ,
                      int32_t* occ_u, int2* chunks, int* nchunks, int2* split, int* nsplit,
@@ -1057,10 +1072,13 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   return kOk;
 }
 
-int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* lr_dev,
-                int* step_dev, float beta1, float beta2, float eps, hipStream_t st) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, p, g, m, v, n,
-                     lr_dev, step_dev, beta1, beta2, eps);
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* coef,
+                float beta1, float beta2, float eps, hipStream_t st) {
+  PS_REQUIRE(((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+               reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0,
+             kErrArg, "adam: buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4, 256, 2048)), dim3(256), 0, st, p, g, m,
+                     v, n, coef, beta1, beta2, eps);
   PS_CHECK_LAUNCH();
   return kOk;
 }

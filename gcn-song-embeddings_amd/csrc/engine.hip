@@ -52,8 +52,9 @@ int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const i
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
                 hipStream_t);
-int launch_adam(float*, const float*, float*, float*, int64_t, const float*, int*, float, float,
-                float, hipStream_t);
+int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
+                hipStream_t);
+int csr_prepare();
 int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, const float*,
                            float*, hipStream_t);
 int launch_gather_out(const float*, int, const int32_t*, int64_t, float*, hipStream_t);
@@ -137,6 +138,7 @@ struct Engine {
 constexpr int kEvents = 32;
 static int ensure_streams(Engine& E) {
   if (E.side[0]) return kOk;
+  PS_TRY(csr_prepare());
   for (auto& s : E.side) PS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   E.ev.resize(kEvents);
   for (auto& e : E.ev) PS_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -277,7 +279,7 @@ static void layout(Engine& E) {
     lb.nsplit = carve(cur, 16);
   }
   const int64_t top = E.L.back().S.cap;
-  E.ids = carve(cur, c.max_pos * 8);
+  E.ids = carve(cur, c.max_pos * 8 + 16);  // + Adam coefficients staged behind the ids
   E.pos_rank = carve(cur, c.max_pos * 4);
   E.H1 = carve(cur, top * c.out * 4);
   E.Z = carve(cur, top * c.out * 4);
@@ -921,16 +923,16 @@ int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream) {
   return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
 }
 
-int pinsage_engine_adam(pinsage_engine* e, const float* lr_dev, int32_t* step_dev, float beta1,
-                        float beta2, float eps, void* stream) {
+int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,
+                        void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
   Timed t(*E, "adam", (hipStream_t)stream);
   if (!E->adam_m || !E->adam_v) {
     set_error("engine_adam: optimizer state not set");
     return kErrArg;
   }
-  return launch_adam(E->params, E->grads, E->adam_m, E->adam_v, E->n_params, lr_dev, step_dev, beta1,
-                     beta2, eps, (hipStream_t)stream);
+  return launch_adam(E->params, E->grads, E->adam_m, E->adam_v, E->n_params, coef, beta1, beta2, eps,
+                     (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -25,7 +25,7 @@ namespace ps {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kStages = 3;     // LDS ring depth
+constexpr int kLdsBudget = 81920;  // bytes per workgroup: two workgroups per CU
 constexpr int kIdxWin = 1024;  // gathered k-rows staged in LDS at a time
 
 // One 16-B LDS-DMA per lane (global_load_lds_dwordx4; LDS destination = M0 +
@@ -33,8 +33,7 @@ constexpr int kIdxWin = 1024;  // gathered k-rows staged in LDS at a time
 // not see the counted waits below and drains the whole queue (vmcnt(0)) before
 // LDS reads at control-flow joins, leaves the ring alone; the kernel retires
 // the DMAs itself with s_waitcnt vmcnt(N) before each stage's barrier.
-__device__ __forceinline__ void glds16(const float* g, float* l) {
-  const unsigned lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)l);
+__device__ __forceinline__ void glds16(const float* g, unsigned lds) {  // lds: LDS byte address
   unsigned saved;
   // M0 is reserved to the compiler: save and restore it around the DMA
   asm volatile(
@@ -81,12 +80,12 @@ struct KOp {
       rp2[j] = a2 ? a2 + (int64_t)(idx2 ? idx2[rc] : rc) * lda2 : rp[j];
     }
   }
-  __device__ __forceinline__ void issue(float* img, int wave, int k0, int kend, int K1) const {
+  __device__ __forceinline__ void issue(unsigned img, int wave, int k0, int kend, int K1) const {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int k = min(k0 + lc[j], kend - 4);
       const float* src = (K1 >= 0 && k >= K1) ? rp2[j] + (k - K1) : rp[j] + k;
-      glds16(src, img + (j * 256 + wave * 64) * 4);
+      glds16(src, img + (unsigned)(j * 256 + wave * 64) * 16u);
     }
   }
   __device__ __forceinline__ void zero_tail(float* img, int tid, int k0, int kend) const {
@@ -129,13 +128,13 @@ struct MNOp {
     }
   }
   // sidx: LDS window of gathered row numbers starting at k-row wb
-  __device__ __forceinline__ void issue(float* img, int wave, int k0, int kend, const int* sidx,
+  __device__ __forceinline__ void issue(unsigned img, int wave, int k0, int kend, const int* sidx,
                                         int wb) const {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int k = min(k0 + kr0 + KSTEP * j, kend - 1);
       const int64_t r = gathered ? sidx[k - wb] : k;
-      glds16(base + r * ld, img + (j * 256 + wave * 64) * 4);
+      glds16(base + r * ld, img + (unsigned)(j * 256 + wave * 64) * 16u);
     }
   }
   __device__ __forceinline__ void zero_tail(float* img, int tid, int k0, int kend) const {
@@ -154,14 +153,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   constexpr int SZA = OpA::SZ, SZB = OpB::SZ, SZS = SZA + SZB;
   constexpr int NG = OpA::NI + OpB::NI;  // DMAs per wave per stage
   constexpr bool GA = !AK, GB = !BKM;    // operands that may need gathered k-rows
-  // ONE __shared__ object: with a second one hipcc emits vmcnt(0) (draining the
-  // DMA ring) before fragment reads that follow a DMA issue.
-  __shared__ __attribute__((aligned(16))) float smem[kStages * SZS + 2 * kIdxWin];
-  float* const sm0 = smem;
-  float* const sm1 = smem + SZS;
-  float* const sm2 = smem + 2 * SZS;
-  int* const sidxA = reinterpret_cast<int*>(smem + kStages * SZS);
-  int* const sidxB = sidxA + kIdxWin;
+  // ring depth: as many stage buffers as fit two workgroups per CU (3 or 4);
+  // the k-row windows exist only for MN-major (possibly gathered) operands
+  constexpr int IDXF = (GA ? kIdxWin : 0) + (GB ? kIdxWin : 0);
+  constexpr int NSA = (kLdsBudget / 4 - IDXF) / SZS;
+  constexpr int NS = NSA > 4 ? 4 : NSA;
+  static_assert(NS >= 3, "stage buffers do not fit");
+  __shared__ __attribute__((aligned(16))) float smem[NS * SZS + IDXF];
+  int* const sidxA = reinterpret_cast<int*>(smem + NS * SZS);
+  int* const sidxB = sidxA + (GA ? kIdxWin : 0);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -237,12 +237,16 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto issue = [&](int st, float* base) __attribute__((always_inline)) {
+    // LDS byte address of the ring (a constant: the cast of the __shared__
+    // array itself, not of a computed generic pointer)
+    const unsigned smem_lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)smem);
+    auto issue = [&](int st) __attribute__((always_inline)) {
       const int k0 = kb + st * BK;
+      const unsigned base = smem_lds + (unsigned)((st % NS) * SZS) * 4u;
       if constexpr (AK) opa.issue(base, wave, k0, ke, p.K1);
       else opa.issue(base, wave, k0, ke, sidxA, wb);
-      if constexpr (BKM) opb.issue(base + SZA, wave, k0, ke, -1);
-      else opb.issue(base + SZA, wave, k0, ke, sidxB, wb);
+      if constexpr (BKM) opb.issue(base + SZA * 4u, wave, k0, ke, -1);
+      else opb.issue(base + SZA * 4u, wave, k0, ke, sidxB, wb);
     };
     const int h = lane >> 5, l32 = lane & 31;
     const bool do_bias = !AK && p.bias_part && tn == 0 && tid < BM;
@@ -285,39 +289,42 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
       }
     };
 
-    // ring: stage t is computed from its slot while t+1 and t+2 are in flight
-    auto step = [&](int it, float* cur, float* nxt2) __attribute__((always_inline)) {
-      // retire this wave's DMAs of stage it (stage it+1's NG may stay in flight)
-      if (it + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ring: stage t is computed from slot t % NS while stages t+1 .. t+NS-2 are
+    // in flight; stage t+NS-1 is issued into the slot stage t-1 used
+    auto slot = [&](int st) __attribute__((always_inline)) { return smem + (st % NS) * SZS; };
+    for (int st = 0; st < NS - 1 && st < nk; ++st) issue(st);
+    for (int it = 0; it < nk; ++it) {
+      // retire this wave's DMAs of stage it; the younger stages stay in flight
+      const int younger = min(NS - 2, nk - 1 - it);
+      if constexpr (NS == 4) {
+        if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      float* cur = slot(it);
       if (tail && it == nk - 1) {  // zero the k-tail this thread's DMAs brought in
         const int k0 = kb + it * BK;
         opa.zero_tail(cur, tid, k0, ke);
         opb.zero_tail(cur + SZA, tid, k0, ke);
       }
-      // publish stage it; every wave is done reading stage it-1's slot (= nxt2)
+      // publish stage it; every wave is done reading stage it-1's slot
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (it + 2 < nk) {
-        const int k2 = kb + (it + 2) * BK;
+      const int nx = it + NS - 1;
+      if (nx < nk) {
+        const int k2 = kb + nx * BK;
         if ((needA || needB) && k2 >= wb + kIdxWin) {  // next window of row numbers
           wb += kIdxWin;
           fill_idx(wb);
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
         }
-        issue(it + 2, nxt2);
+        issue(nx);
       }
       compute(cur, cur + SZA);
-    };
-    if (nk > 0) issue(0, sm0);
-    if (nk > 1) issue(1, sm1);
-    for (int it = 0; it < nk; it += 3) {
-      step(it, sm0, sm2);
-      if (it + 1 >= nk) break;
-      step(it + 1, sm1, sm0);
-      if (it + 2 >= nk) break;
-      step(it + 2, sm2, sm1);
     }
     __syncthreads();  // stage buffers are reused by the epilogue / next tile
 

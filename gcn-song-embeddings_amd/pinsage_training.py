@@ -210,10 +210,6 @@ class _FusedStep:
         self.ws = None
         self.m = self.v = None
         self.grads = None
-        self.lr_dev = torch.zeros(1, dtype=torch.float32, device=self.dev)
-        # [Adam step, completion ticket] (see pinsage_engine_adam)
-        self.step_dev = torch.zeros(2, dtype=torch.int32, device=self.dev)
-        self._lr_host = None
         self.host_batch = None
         self._tuned = False
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
@@ -237,11 +233,15 @@ class _FusedStep:
             self.ws = r.engine.new_workspace(self.dev)
             self.B = B
             off = r.engine.off
-            self.ids_view = r.engine.view(self.ws, int(off.ids), torch.int64, r.engine.cfg.max_pos)
+            mp = r.engine.cfg.max_pos
+            self.ids_view = r.engine.view(self.ws, int(off.ids), torch.int64, mp)
+            # ids and, behind them, this step's Adam coefficients travel in ONE
+            # host-to-device copy (pinsage_engine_adam)
+            self.stage_view = self.ws[int(off.ids):int(off.ids) + mp * 8 + 16]
             self.scal = r.engine.view(self.ws, int(off.scalars), torch.float32, 4)
             # two pinned staging buffers: the host fills one while the previous
             # step's H2D copy from the other may still be queued
-            self.host_batch = [torch.empty(r.engine.cfg.max_pos, dtype=torch.int64).pin_memory()
+            self.host_batch = [torch.empty(mp * 8 + 16, dtype=torch.uint8).pin_memory()
                                for _ in range(2)]
             self.host_ev = [None, None]
             self.slot = 0
@@ -266,7 +266,6 @@ class _FusedStep:
                             "exp_avg_sq": self.v[off:off + k].view(p.shape)}
             p.grad = self.grads[off:off + k].view(p.shape)
             off += k
-        self.step_dev.copy_(torch.tensor([step, 0], dtype=torch.int32))
         self.host_step = step
 
     def sync_optimizer_step(self):
@@ -275,18 +274,31 @@ class _FusedStep:
             if st is not None:
                 st["step"] = torch.tensor(float(self.host_step))
 
+    def _adam_coef(self, step):
+        """torch.optim.Adam's per-step scalars (_single_tensor_adam, computed in
+        double as there): lr / (1 - beta1^t) and sqrt(1 - beta2^t)."""
+        g = self.tr.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        lr = float(g["lr"])
+        return lr / (1 - b1 ** step), (1 - b2 ** step) ** 0.5
+
     def _stage(self, batch, B):
-        """Copy the [B, 3] batch into the engine's device id buffer."""
+        """Copy the [B, 3] batch, and the Adam coefficients of the step about to
+        run, into the engine's device id buffer (one host-to-device copy)."""
         k = self.slot
         self.slot ^= 1
         if self.host_ev[k] is not None:
             self.host_ev[k].synchronize()
-        hb = self.host_batch[k][:3 * B]
-        hb.copy_(batch.reshape(-1).to(torch.int64))
+        n = 3 * B * 8
+        hb = self.host_batch[k]
+        ids = hb[:n].view(torch.int64)
+        ids.copy_(batch.reshape(-1).to(torch.int64))
         n_items = int(self.runner.engine.cfg.n_items)
-        if int(hb.min()) < 0 or int(hb.max()) >= n_items:
+        if int(ids.min()) < 0 or int(ids.max()) >= n_items:
             raise IndexError(f"batch ids out of range for {n_items} items")
-        self.ids_view[:3 * B].copy_(hb, non_blocking=True)
+        hb[n:n + 8].view(torch.float32).copy_(torch.tensor(self._adam_coef(self.host_step + 1),
+                                                           dtype=torch.float32))
+        self.stage_view[:n + 8].copy_(hb[:n + 8], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.host_ev[k] = ev
@@ -306,8 +318,8 @@ class _FusedStep:
     def _adam(self):
         g = self.tr.optimizer.param_groups[0]
         b1, b2 = g["betas"]
-        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, nat.ptr(self.lr_dev),
-                                                nat.ptr(self.step_dev), float(b1), float(b2),
+        coef = ctypes.c_void_p(self.stage_view.data_ptr() + 3 * self.B_cur * 8)
+        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, coef, float(b1), float(b2),
                                                 float(g["eps"]), nat.stream_ptr()), "adam")
 
     def _signature(self, feats, table):
@@ -332,10 +344,7 @@ class _FusedStep:
         feats = r.features(tr.features)
         table = r.table(tr.nbhds)
         r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)
-        lr = float(tr.optimizer.param_groups[0]["lr"])
-        if lr != self._lr_host:
-            self.lr_dev.fill_(lr)
-            self._lr_host = lr
+        self.B_cur = B
         self._stage(batch, B)
         sig = self._signature(feats, table)
         if self.graph is not None and (self.graph_B != B or self.graph_sig != sig or not self.use_graph):

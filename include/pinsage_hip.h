@@ -190,12 +190,12 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
                                    void* stream);
 /* all parameter gradients from dZ into the grad buffer (overwritten) */
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
-/* torch.optim.Adam step over the flat buffers; lr_dev f32 and step_dev int32[2]
- * live in device memory so the step can be graph-replayed: the update uses
- * step_dev[0] + 1 and stores it back; step_dev[1] is a completion ticket that
- * must be 0 on entry (it is left 0). */
-int pinsage_engine_adam(pinsage_engine* e, const float* lr_dev, int32_t* step_dev, float beta1,
-                        float beta2, float eps, void* stream);
+/* torch.optim.Adam step over the flat buffers (pinsage_training.py:147,191).
+ * coef: device f32[2] = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} for this step
+ * t, computed by the caller in double as torch does (kept in device memory so
+ * a captured step graph picks up each step's values). */
+int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,
+                        void* stream);
 
 /* Frontier sizes of the last forward in ws (synchronises the stream): S[l] =
  * |S_l| (nodes convolved at layer l), N[l] = |N_l| (distinct neighbours). */
