@@ -63,6 +63,9 @@ _SIGS = {
     "pinsage_frontier_workspace": (i64, [i64]),
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),
     "pinsage_linear": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, ctypes.c_int, vp, i64, vp]),
+    "pinsage_gemm_ex": (ctypes.c_int, [i64, i64, i64, ctypes.c_int, ctypes.c_int, vp, i64, vp, vp, i64,
+                                       vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, vp]),
     "pinsage_weighted_agg": (ctypes.c_int, [vp, i64, vp, vp, i64, i64, vp, vp]),
     "pinsage_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(vp)]),
     "pinsage_engine_destroy": (None, [vp]),
@@ -77,6 +80,7 @@ _SIGS = {
     "pinsage_engine_set_output_grad": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_backward": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_adam": (ctypes.c_int, [vp, vp, f32, f32, f32, vp]),
+    "pinsage_engine_backward_adam": (ctypes.c_int, [vp, vp, vp, f32, f32, f32, vp]),
     "pinsage_engine_read_counts": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "pinsage_engine_set_hints": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_timing": (ctypes.c_int, [vp, ctypes.c_int]),

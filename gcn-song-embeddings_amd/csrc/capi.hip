@@ -338,6 +338,55 @@ int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M,
   return launch_gemm(p, (hipStream_t)stream);
 }
 
+int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor, const float* A,
+                    int64_t lda, const int32_t* a_idx, const float* B, int64_t ldb,
+                    const int32_t* b_idx, float* C, int64_t ldc, const float* bias, int act,
+                    int epi, int splits, int cfg, int stream_k, void* stream) {
+  if (M < 0 || N <= 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX ||
+      (epi != kEpiStore && epi != kEpiAccum && epi != kEpiPartial) || splits < 1 || cfg < -1 ||
+      cfg > 2) {
+    set_error("gemm_ex: bad argument");
+    return kErrArg;
+  }
+  GemmParams p;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.a_kmajor = a_kmajor != 0;
+  p.b_kmajor = b_kmajor != 0;
+  p.a = A;
+  p.lda = lda;
+  p.a_idx = a_idx;
+  p.b = B;
+  p.ldb = ldb;
+  p.b_idx = b_idx;
+  p.c = C;
+  p.ldc = ldc;
+  p.bias = bias;
+  p.act = act != 0;
+  p.epi = epi;
+  p.splits = splits;
+  p.cfg = cfg;
+  p.stream_k = stream_k;
+  if (stream_k != 0) {  // library-owned stream-K scratch (tests and microbenchmarks)
+    static float* slab = nullptr;
+    static int* cnt = nullptr;
+    constexpr int64_t kCnt = 1 << 20;
+    if (!slab) {
+      if (hipMalloc(&slab, (size_t)gemm_sk_slab_floats() * sizeof(float)) != hipSuccess ||
+          hipMalloc(&cnt, (size_t)kCnt * sizeof(int)) != hipSuccess ||
+          hipMemset(cnt, 0, (size_t)kCnt * sizeof(int)) != hipSuccess) {
+        set_error("gemm_ex: stream-K scratch allocation failed");
+        return kErrHip;
+      }
+    }
+    p.sk_slab = slab;
+    p.sk_cnt = cnt;
+    p.sk_cnt_len = kCnt;
+  }
+  return launch_gemm(p, (hipStream_t)stream);
+}
+
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
                          int64_t n_rows, int64_t T, float* agg, void* stream) {
   return launch_agg(q, (int)hid, loc, w, (int)T, nullptr, n_rows, agg, (hipStream_t)stream);

@@ -49,6 +49,20 @@ const char* last_error();
     if (_rc != 0) return _rc;   \
   } while (0)
 
+// Adam state of one parameter slice (weight [M][N] and optional bias [M]) for
+// kernels that apply torch.optim.Adam as they produce the slice's gradient.
+// coef = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} on the device (staged per step).
+struct AdamSlice {
+  float* p = nullptr;   // weight rows (same row stride as the gradient)
+  float* m = nullptr;
+  float* v = nullptr;
+  float* pb = nullptr;  // bias (nullable)
+  float* mb = nullptr;
+  float* vb = nullptr;
+  const float* coef = nullptr;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+};
+
 // ---------------------------------------------------------------- device helpers
 constexpr int kWave = 64;
 constexpr float kSlope = 0.01f;  // nn.functional.leaky_relu default

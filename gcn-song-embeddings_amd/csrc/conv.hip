@@ -855,9 +855,16 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
                                                               float* __restrict__ out, int64_t ld,
                                                               const float* __restrict__ bpart,
                                                               float* __restrict__ bias_out,
-                                                              int nb_main) {
+                                                              int nb_main, AdamSlice ad) {
   __shared__ float4 red[4][64];
   const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
+  float ss = 0.f, bc2 = 1.f, omb1 = 0.f, omb2 = 0.f;
+  if (ad.coef) {
+    ss = ad.coef[0];
+    bc2 = ad.coef[1];
+    omb1 = (float)(1.0 - (double)ad.beta1);
+    omb2 = (float)(1.0 - (double)ad.beta2);
+  }
   if ((int)blockIdx.x < nb_main) {
     const int64_t e4 = (int64_t)blockIdx.x * 64 + j;  // float4 index into [M][N]
     const bool ok = e4 * 4 < (int64_t)M * N;
@@ -888,8 +895,20 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
       const float4 a = red[0][j], b = red[1][j], c = red[2][j], d = red[3][j];
       const float4 r = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y),
                                    (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
-      const int64_t e = e4 * 4, m = e / N, n = e - m * N;
-      *reinterpret_cast<float4*>(out + m * ld + n) = r;
+      const int64_t e = e4 * 4, m = e / N, n = e - m * N, o = m * ld + n;
+      *reinterpret_cast<float4*>(out + o) = r;
+      if (ad.p) {  // the slice's Adam step, as adam_kernel would apply it
+        float4 pp = *reinterpret_cast<const float4*>(ad.p + o);
+        float4 mm = *reinterpret_cast<const float4*>(ad.m + o);
+        float4 vv = *reinterpret_cast<const float4*>(ad.v + o);
+        adam1(pp.x, r.x, mm.x, vv.x, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.y, r.y, mm.y, vv.y, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.z, r.z, mm.z, vv.z, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.w, r.w, mm.w, vv.w, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+        *reinterpret_cast<float4*>(ad.p + o) = pp;
+        *reinterpret_cast<float4*>(ad.m + o) = mm;
+        *reinterpret_cast<float4*>(ad.v + o) = vv;
+      }
     }
     return;
   }
@@ -901,8 +920,11 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
     for (int k = g; k < S; k += 4) acc += bpart[(int64_t)k * M + m];
   redf[g * 64 + j] = acc;
   __syncthreads();
-  if (g == 0 && m < M)
-    bias_out[m] = (redf[j] + redf[64 + j]) + (redf[128 + j] + redf[192 + j]);
+  if (g == 0 && m < M) {
+    const float r = (redf[j] + redf[64 + j]) + (redf[128 + j] + redf[192 + j]);
+    bias_out[m] = r;
+    if (ad.pb) adam1(ad.pb[m], r, ad.mb[m], ad.vb[m], ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+  }
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -927,15 +949,24 @@ int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, 
 }
 
 int launch_reduce_slabs_2d(const float* part, int S, int64_t stride, int M, int N, float* out,
-                           int64_t ld, const float* bpart, float* bias_out, hipStream_t st) {
+                           int64_t ld, const float* bpart, float* bias_out, const AdamSlice* adam,
+                           hipStream_t st) {
   PS_REQUIRE(N % 4 == 0 && ld % 4 == 0 && stride % 4 == 0 &&
                  (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
                  (reinterpret_cast<uintptr_t>(part) & 15) == 0,
              kErrArg, "reduce_slabs: needs 16-byte aligned rows");
+  AdamSlice ad;
+  if (adam) {
+    ad = *adam;
+    PS_REQUIRE(ad.p && ad.m && ad.v && ad.coef && (!bias_out || (ad.pb && ad.mb && ad.vb)) &&
+                   ((reinterpret_cast<uintptr_t>(ad.p) | reinterpret_cast<uintptr_t>(ad.m) |
+                     reinterpret_cast<uintptr_t>(ad.v)) & 15) == 0,
+               kErrArg, "reduce_slabs: Adam slice needs 16-byte aligned state for every output");
+  }
   const int nb_main = (int)ceil_div((int64_t)M * N / 4, 64);
   const int nb_bias = bias_out ? (int)ceil_div(M, 64) : 0;
   hipLaunchKernelGGL(reduce_slabs_2d_kernel, dim3(nb_main + nb_bias), dim3(256), 0, st, part, S, stride,
-                     M, N, out, ld, bpart, bias_out, nb_main);
+                     M, N, out, ld, bpart, bias_out, nb_main, ad);
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -56,7 +56,7 @@ int launch_adam(float*, const float*, float*, float*, int64_t, const float*, flo
                 hipStream_t);
 int csr_prepare();
 int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, const float*,
-                           float*, hipStream_t);
+                           float*, const AdamSlice*, hipStream_t);
 int launch_gather_out(const float*, int, const int32_t*, int64_t, float*, hipStream_t);
 int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
                         int*, float*, hipStream_t);
@@ -457,7 +457,34 @@ struct WGrad {
   float* dst_b = nullptr;
 };
 
-static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st) {
+// Adam applied by the gradient reductions (pinsage_engine_backward_adam)
+struct AdamStep {
+  const float* coef;
+  float beta1, beta2, eps;
+};
+
+// Adam slice of the parameter at flat offsets (w_off, b_off); b_off < 0: none
+static AdamSlice adam_slice(const Engine& E, const AdamStep& a, int64_t w_off, int64_t b_off) {
+  AdamSlice s;
+  s.p = E.params + w_off;
+  s.m = E.adam_m + w_off;
+  s.v = E.adam_v + w_off;
+  if (b_off >= 0) {
+    s.pb = E.params + b_off;
+    s.mb = E.adam_m + b_off;
+    s.vb = E.adam_v + b_off;
+  }
+  s.coef = a.coef;
+  s.beta1 = a.beta1;
+  s.beta2 = a.beta2;
+  s.eps = a.eps;
+  return s;
+}
+
+// after_use: with Adam fused, the reduction (which updates the parameter)
+// waits for this event, recorded behind the main stream's last read of it
+static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st,
+                       const AdamSlice* adam = nullptr, hipEvent_t after_use = nullptr) {
   int cfg = 0, S = 1;
   choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
   GemmParams p;
@@ -485,15 +512,27 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st) {
   p.bias_part = w.dst_b ? at<float>(ws, E.bslab) : nullptr;
   PS_REQUIRE((int64_t)S * w.M * w.N <= E.slab_floats, kErrWorkspace, "engine: split-K slab too small");
   PS_TRY(launch_gemm(p, st));
+  if (adam && after_use) PS_CHECK_HIP(hipStreamWaitEvent(st, after_use, 0));
   return launch_reduce_slabs_2d(at<float>(ws, E.slab), S, (int64_t)w.M * w.N, w.M, w.N, w.dst,
-                                w.ld_dst, p.bias_part, w.dst_b, st);
+                                w.ld_dst, p.bias_part, w.dst_b, adam, st);
 }
 
 // ---------------------------------------------------------------- backward
 // Starts from dZ (gradient of the head output rows of the unique top nodes).
-int engine_backward(Engine& E, void* ws, hipStream_t st) {
+// adam != nullptr: the step ends with torch.optim.Adam.  The last gradient,
+// dQ of layer 0, is the step's tail on the weight-gradient stream: its
+// reduction applies Q0's Adam itself, while the main stream (its own chain
+// done) applies Adam to every other parameter (contiguous behind Q0 in the
+// flat layout) once their gradients exist -- the optimizer pass is off the
+// critical path.  No other reduction waits on the main stream.
+int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   const EngineConfig& c = E.cfg;
   PS_REQUIRE(E.grads, kErrArg, "engine: grad buffer not set");
+  PS_REQUIRE(!adam || (E.adam_m && E.adam_v), kErrArg, "engine: optimizer state not set");
+  const LayerBuf& l0 = E.L[0];
+  PS_REQUIRE(!adam || (l0.pQw == 0 && l0.pQb == l0.pQw + c.hid * l0.d && l0.pWw == l0.pQb + c.hid),
+             kErrArg, "engine: Q0 must lead the flat parameter layout");
+  hipEvent_t others_ready = nullptr;  // s_wg: every gradient but Q0's is written
   const int Lc = (int)c.n_layers, T = (int)c.T;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
@@ -519,23 +558,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
   }
   // weight gradients run on s_wg, each forked once its inputs exist on st
   Timed t_hb(E, "bwd.head", st);
-  PS_TRY(dep(E, st, s_wg));
-  {
-    Timed tw(E, "bwd.wgrad.head", s_wg);
-    WGrad w;
-    w.A = at<float>(ws, E.dZ);
-    w.lda = o;
-    w.M = o;
-    w.B = at<float>(ws, E.H1);
-    w.ldb = o;
-    w.N = o;
-    w.K_dev = cnt(top.S);
-    w.K_max = top.S.cap;
-    w.K_hint = top.S.hint;
-    w.dst = gr + E.pG2w;
-    w.ld_dst = o;
-    PS_TRY(weight_grad(E, ws, w, s_wg));
-  }
+  PS_TRY(dep(E, st, s_wg));  // dZ, H1 ready: dG2 (its reduction also waits for dP1)
   {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
@@ -554,9 +577,25 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     p.ldm = o;
     PS_TRY(launch_gemm(p, st));
   }
-  PS_TRY(dep(E, st, s_wg));
   {
     Timed tw(E, "bwd.wgrad.head", s_wg);
+    WGrad w;
+    w.A = at<float>(ws, E.dZ);
+    w.lda = o;
+    w.M = o;
+    w.B = at<float>(ws, E.H1);
+    w.ldb = o;
+    w.N = o;
+    w.K_dev = cnt(top.S);
+    w.K_max = top.S.cap;
+    w.K_hint = top.S.hint;
+    w.dst = gr + E.pG2w;
+    w.ld_dst = o;
+    PS_TRY(weight_grad(E, ws, w, s_wg));
+  }
+  PS_TRY(dep(E, st, s_wg));
+  WGrad g1_wgrad;
+  {
     WGrad w;  // dG1 and db1
     w.A = at<float>(ws, E.dP1);
     w.lda = o;
@@ -570,7 +609,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     w.dst = gr + E.pG1w;
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
-    PS_TRY(weight_grad(E, ws, w, s_wg));
+    g1_wgrad = w;
   }
   {
     GemmParams p;  // dY_top = dP1 G1
@@ -588,6 +627,10 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
     p.ldc = o;
     PS_TRY(launch_gemm(p, st));
   }
+  {
+    Timed tw(E, "bwd.wgrad.head", s_wg);
+    PS_TRY(weight_grad(E, ws, g1_wgrad, s_wg));
+  }
   t_hb.stop();
   for (int l = Lc - 1; l >= 0; --l) {
     Timed tb(E, lname("bwd.layer", l), st);
@@ -604,8 +647,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
                                  l > 0 ? cnt(E.L[(size_t)l - 1].S) : nullptr,
                                  l == Lc - 1 ? at<int>(ws, E.Kc) : nullptr, 3 * top.S.cap, st));
     PS_TRY(dep(E, st, s_wg));
+    WGrad w_wgrad;
     {
-      Timed tw(E, lname("bwd.w_wgrad", l), s_wg);
       WGrad w;  // dW = dp^T [h_self || agg], dWb = colsum(dp)
       w.A = dp;
       w.lda = o;
@@ -623,7 +666,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       w.dst = gr + lb.pWw;
       w.ld_dst = d + hd;
       w.dst_b = gr + lb.pWb;
-      PS_TRY(weight_grad(E, ws, w, s_wg));
+      w_wgrad = w;
     }
     {
       // [d_self || d_agg] = dp W: columns < d scatter-add into the rows of
@@ -655,6 +698,10 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       }
       PS_TRY(launch_gemm(p, st));
     }
+    {
+      Timed tw(E, lname("bwd.w_wgrad", l), s_wg);
+      PS_TRY(weight_grad(E, ws, w_wgrad, s_wg));
+    }
     PS_CHECK_HIP(hipStreamWaitEvent(st, csr_done[(size_t)l], 0));
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
                             at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
@@ -662,9 +709,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
                             at<float>(ws, lb.dqpart), st));
     PS_TRY(dep(E, st, s_wg));
+    WGrad q_wgrad;
     {
       // dQ = dpq^T h[q_src], dQb = colsum(dpq)
-      Timed tq(E, lname("bwd.q_wgrad", l), s_wg);
       WGrad w;
       w.A = at<float>(ws, lb.dpq);
       w.lda = hd;
@@ -679,7 +726,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       w.dst = gr + lb.pQw;
       w.ld_dst = d;
       w.dst_b = gr + lb.pQb;
-      PS_TRY(weight_grad(E, ws, w, s_wg));
+      q_wgrad = w;
     }
     if (l > 0) {
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
@@ -699,6 +746,22 @@ int engine_backward(Engine& E, void* ws, hipStream_t st) {
       p.epi = kEpiAccum;
       PS_TRY(launch_gemm(p, st));
     }
+    {
+      AdamSlice q0;
+      if (adam && l == 0) {
+        others_ready = E.ev[(size_t)(E.ev_next++ % kEvents)];
+        PS_CHECK_HIP(hipEventRecord(others_ready, s_wg));
+        q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
+      }
+      Timed tq(E, lname("bwd.q_wgrad", l), s_wg);
+      PS_TRY(weight_grad(E, ws, q_wgrad, s_wg, adam && l == 0 ? &q0 : nullptr));
+    }
+  }
+  if (adam) {  // Adam on everything behind Q0, beside Q0's weight gradient
+    PS_CHECK_HIP(hipStreamWaitEvent(st, others_ready, 0));
+    Timed ta(E, "adam", st);
+    PS_TRY(launch_adam(E.params + l0.pWw, E.grads + l0.pWw, E.adam_m + l0.pWw, E.adam_v + l0.pWw,
+                       E.n_params - l0.pWw, adam->coef, adam->beta1, adam->beta2, adam->eps, st));
   }
   // every gradient is written once the side streams drain into st
   PS_TRY(dep(E, s_csr, st));
@@ -920,7 +983,17 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
 }
 
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream) {
-  return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
+  return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream, nullptr);
+}
+
+int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, float beta1,
+                                 float beta2, float eps, void* stream) {
+  if (!coef) {
+    set_error("engine_backward_adam: null coefficients");
+    return kErrArg;
+  }
+  const AdamStep a{coef, beta1, beta2, eps};
+  return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream, &a);
 }
 
 int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,

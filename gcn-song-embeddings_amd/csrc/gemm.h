@@ -62,7 +62,22 @@ struct GemmParams {
   int splits = 1;                 // kEpiPartial: split-K count
   int M_hint = 0;                 // expected M (device-side M): picks the block tile
   int cfg = -1;                   // force a tile config (tests); -1 = choose by size
+  // stream-K (kEpiStore / kEpiAccum / kEpiL2Norm, static K > 0, K-major or
+  // ungathered MN-major operands): the launch's k-steps are cut into equal runs
+  // over a full grid, and tiles cut between blocks are combined in-launch.
+  // Scratch: gemm_sk_slab_floats() floats and sk_cnt_len zeroed ints (the
+  // tickets reset themselves), one set per stream.
+  float* sk_slab = nullptr;
+  int* sk_cnt = nullptr;
+  int64_t sk_cnt_len = 0;
+  int stream_k = -1;              // -1 choose by size, 0 off, 1 on (when allowed)
+  int sk_min_units = 4;           // k-steps per block at least
 };
+
+// slab floats a stream-K launch may use (two partial tiles per resident block)
+int64_t gemm_sk_slab_floats();
+// resident workgroups of one GEMM launch (two per CU)
+int gemm_slots();
 
 // Block-tile configurations (4 waves each): rows x cols, k-depth per stage.
 //   0: 128 x 128 x 16  (2x2 waves of 64x64)      large M

@@ -144,6 +144,20 @@ struct MNOp {
   }
 };
 
+// Stream-K arrival ticket and slab addressing (work units = (tile, k-step)).
+// Block b of the Ga active blocks owns units [b*U/Ga, (b+1)*U/Ga); a tile cut
+// by a block boundary is finished by the last of its blocks to arrive.  Every
+// block keeps at most two partial tiles (its first and its last), in slab
+// slots 2b and 2b+1.
+struct SkPlan {
+  int64_t U;
+  int I, Ga;
+  __device__ __forceinline__ int64_t start(int b) const { return (int64_t)b * U / Ga; }
+  __device__ __forceinline__ int block_of(int64_t u) const {  // the block owning unit u
+    return (int)(((u + 1) * Ga - 1) / U);
+  }
+};
+
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK.
 template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
@@ -171,40 +185,23 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int kchunk = (((K + splits - 1) / splits) + BK - 1) / BK * BK;
-  int G, W;
-  if (splits > 1) {
-    G = splits;
-    W = tiles_m * tiles_n;
-  } else {
-    G = tiles_m;
-    W = tiles_n;
-  }
   const int32_t* idxA = GA ? p.a_idx : nullptr;
   const int32_t* idxB = GB ? p.b_idx : nullptr;
   const int32_t* idxB2 = GB ? p.b2_idx : nullptr;
   const int32_t* idxBw = idxB ? idxB : idxB2;  // one gathered B segment (launch_gemm checks)
   const bool needA = GA && idxA;
   const bool needB = GB && (idxB || idxB2);
-  // tiles of one row panel (or one split) are dealt to blocks b, b+8, ...:
-  // one XCD under round-robin placement, so they share its L2 (speed only)
-  const int iters = 8 * ((G + 7) / 8) * W;
-  for (int t = blockIdx.x; t < iters; t += gridDim.x) {
-    const int xcd = t & 7, s = t >> 3;
-    const int g = (s / W) * 8 + xcd, w = s % W;
-    if (g >= G) continue;
-    int split, tm, tn;
-    if (splits > 1) {
-      split = g;
-      tm = w / tiles_n;
-      tn = w % tiles_n;
-    } else {
-      split = 0;
-      tm = g;
-      tn = w;
-    }
+  const int h = lane >> 5, l32 = lane & 31;
+  // LDS byte address of the ring (a constant: the cast of the __shared__
+  // array itself, not of a computed generic pointer)
+  const unsigned smem_lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)smem);
+
+  // one tile (tm, tn) over k in [kb, ke): k loop, then the epilogue.  sk_t >= 0:
+  // a stream-K segment of tile sk_t that does not cover all of k (publish the
+  // partial sum; the last segment to arrive adds them up and runs the epilogue)
+  auto run_item = [&](int tm, int tn, int split, int kb, int ke, int sk_t, int sk_slot,
+                      const SkPlan& sk) __attribute__((always_inline)) {
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kb = split * kchunk;
-    const int ke = min(K, kb + kchunk);
     const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
     const bool tail = ((ke - kb) % BK) != 0;
 
@@ -237,9 +234,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // LDS byte address of the ring (a constant: the cast of the __shared__
-    // array itself, not of a computed generic pointer)
-    const unsigned smem_lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)smem);
     auto issue = [&](int st) __attribute__((always_inline)) {
       const int k0 = kb + st * BK;
       const unsigned base = smem_lds + (unsigned)((st % NS) * SZS) * 4u;
@@ -248,7 +242,6 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
       if constexpr (BKM) opb.issue(base + SZA * 4u, wave, k0, ke, -1);
       else opb.issue(base + SZA * 4u, wave, k0, ke, sidxB, wb);
     };
-    const int h = lane >> 5, l32 = lane & 31;
     const bool do_bias = !AK && p.bias_part && tn == 0 && tid < BM;
     float bsum = 0.f;
     // MFMA k-assignment: in the r-th MFMA of octet s, lane half h supplies
@@ -278,14 +271,20 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
           }
       };
       static_assert((BK / 8) % 2 == 0, "octets are processed in pairs");
+      // sched_barrier pins the prefetch distance (the scheduler otherwise
+      // sinks each read next to its MFMAs and exposes the LDS latency)
       float4 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
       rd(fa0, fb0, 0);
 #pragma unroll
       for (int s8 = 0; s8 < BK / 8; s8 += 2) {
         rd(fa1, fb1, s8 + 1);
+        __builtin_amdgcn_sched_barrier(0);
         mm(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
         if (s8 + 2 < BK / 8) rd(fa0, fb0, s8 + 2);
+        __builtin_amdgcn_sched_barrier(0);
         mm(fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
       }
     };
 
@@ -327,6 +326,67 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
       compute(cur, cur + SZA);
     }
     __syncthreads();  // stage buffers are reused by the epilogue / next tile
+
+    // ------------------------------------------------------------ stream-K
+    // Publish (write-through sc1 slab stores, every wave drains, one ticket
+    // add per block); the block drawing the last ticket reads every segment's
+    // slab with sc1 loads in block order (a fixed summation order: the result
+    // does not depend on which block arrives last) and runs the epilogue.
+    if (sk_t >= 0) {
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(p.sk_slab, 0, 0x7fffffff, 0x00020000);
+      constexpr int SLAB = BM * BN * 4;  // bytes per slot
+      const unsigned lo = (unsigned)tid * 16u;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                                         acc[i][j][4 * q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4i*>(&v), rs,
+                                                   lo + (unsigned)(((i * TN + j) * 4 + q) * 4096),
+                                                   sk_slot * SLAB, 16);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* const flag = reinterpret_cast<int*>(smem);
+      const int tile = sk_t;
+      const int bf = sk.block_of((int64_t)tile * sk.I), bl = sk.block_of((int64_t)(tile + 1) * sk.I - 1);
+      if (tid == 0)
+        flag[0] = __hip_atomic_fetch_add(p.sk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const bool last = flag[0] == bl - bf;
+      __syncthreads();
+      if (!last) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int bb = bf; bb <= bl; ++bb) {
+        const int sl = 2 * bb + ((int)(sk.start(bb) / sk.I) == tile ? 0 : 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const v4i x = __builtin_amdgcn_raw_buffer_load_b128(
+                  rs, lo + (unsigned)(((i * TN + j) * 4 + q) * 4096), sl * SLAB, 16);
+              const float4 v = *reinterpret_cast<const float4*>(&x);
+              acc[i][j][4 * q] += v.x;
+              acc[i][j][4 * q + 1] += v.y;
+              acc[i][j][4 * q + 2] += v.z;
+              acc[i][j][4 * q + 3] += v.w;
+            }
+      }
+      if (tid == 0) __hip_atomic_store(p.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 
     // ------------------------------------------------------------ epilogue
     // acc[i][j][r] -> row m0 + (wm*TM+i)*32 + (r&3) + 8*(r>>2) + 4*h, col n0 + (wn*TN+j)*32 + l32
@@ -412,10 +472,84 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
         }
     }
     __syncthreads();
+  };
+
+  if (p.sk_cnt) {
+    // stream-K: the tiles' k-steps laid end to end and cut into equal runs,
+    // at least sk_min_units k-steps each (launch_gemm: K-major or ungathered
+    // operands, K > 0, no split-K partials)
+    SkPlan sk;
+    sk.I = (K + BK - 1) / BK;
+    sk.U = (int64_t)tiles_m * tiles_n * sk.I;
+    if (sk.U == 0) return;
+    const int64_t ga = sk.U / p.sk_min_units;
+    sk.Ga = (int)(ga < 1 ? 1 : (ga < (int64_t)gridDim.x ? ga : (int64_t)gridDim.x));
+    if (sk.Ga >= 8) sk.Ga &= ~7;
+    // runs are numbered so that consecutive runs go to blocks b, b+8, ...
+    // (one XCD under round-robin placement: a tile's pieces and neighbouring
+    // tiles' shared A rows stay in one L2; speed only)
+    const int per = sk.Ga >= 8 ? sk.Ga / 8 : sk.Ga;
+    const int b = sk.Ga >= 8 ? (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    if ((int)blockIdx.x >= sk.Ga) return;
+    const int64_t u0 = sk.start(b), u1 = sk.start(b + 1);
+    const int t_first = (int)(u0 / sk.I);
+    for (int64_t u = u0; u < u1;) {
+      const int t = (int)(u / sk.I), i0 = (int)(u - (int64_t)t * sk.I);
+      const int i1 = (int)min((int64_t)sk.I, i0 + (u1 - u));
+      const bool part = !(i0 == 0 && i1 == sk.I);
+      run_item(t / tiles_n, t % tiles_n, 0, i0 * BK, min(K, i1 * BK), part ? t : -1,
+               2 * b + (t == t_first ? 0 : 1), sk);
+      u += i1 - i0;
+    }
+    return;
+  }
+
+  int G, W;
+  if (splits > 1) {
+    G = splits;
+    W = tiles_m * tiles_n;
+  } else {
+    G = tiles_m;
+    W = tiles_n;
+  }
+  // tiles of one row panel (or one split) are dealt to blocks b, b+8, ...:
+  // one XCD under round-robin placement, so they share its L2 (speed only)
+  const SkPlan none{};
+  const int iters = 8 * ((G + 7) / 8) * W;
+  for (int t = blockIdx.x; t < iters; t += gridDim.x) {
+    const int xcd = t & 7, s = t >> 3;
+    const int g = (s / W) * 8 + xcd, w = s % W;
+    if (g >= G) continue;
+    int split, tm, tn;
+    if (splits > 1) {
+      split = g;
+      tm = w / tiles_n;
+      tn = w % tiles_n;
+    } else {
+      split = 0;
+      tm = g;
+      tn = w;
+    }
+    const int kb = split * kchunk;
+    run_item(tm, tn, split, kb, min(K, kb + kchunk), -1, 0, none);
   }
 }
 
 constexpr int kCfgBM[3] = {128, 64, 32};
+
+int gemm_slots() {
+  static const int slots = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    return 2 * cus;
+  }();
+  return slots;
+}
+
+int64_t gemm_sk_slab_floats() { return (int64_t)gemm_slots() * 2 * 64 * 128; }
 
 // Cost model: tiles are dealt round-robin over 256 CUs, so a launch takes
 // ~ceil(tiles / 256) tile-times and a tile-time is ~ BM (fixed BN, same K).
@@ -446,7 +580,8 @@ static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32>), g, dim3(256), 0, st, p);
 }
 
-int launch_gemm(const GemmParams& p, hipStream_t st) {
+int launch_gemm(const GemmParams& p_in, hipStream_t st) {
+  GemmParams p = p_in;
   const int Mmax = p.M_dev ? p.M_max : p.M;
   const int Kmax = p.K_dev ? p.K_max : p.K;
   PS_REQUIRE(p.N > 0 && Mmax >= 0 && Kmax >= 0, kErrArg, "gemm: bad sizes");
@@ -468,15 +603,49 @@ int launch_gemm(const GemmParams& p, hipStream_t st) {
   PS_REQUIRE(p.epi != kEpiL2Norm || p.N <= 128, kErrArg, "gemm: L2-norm epilogue needs N <= 128");
   PS_REQUIRE(p.epi != kEpiPartial || (!p.M_dev && !p.c_idx), kErrArg,
              "gemm: split-K partials need a static M");
+  PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
-  const int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, splits);
+  int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, splits);
+  const int tiles_n = (p.N + 127) / 128;
+  const int slots = gemm_slots();
+
+  // stream-K: allowed for whole-tile epilogues with no per-window gathered
+  // k-rows; chosen when the tiles do not fill the resident slots evenly
+  const bool sk_allowed =
+      p.sk_slab && p.sk_cnt && p.stream_k != 0 && p.epi != kEpiPartial && !p.K_dev && p.K > 0 &&
+      (p.a_kmajor || !p.a_idx) && (p.b_kmajor || (!p.b_idx && !p.b2_idx));
+  bool sk = false;
+  if (sk_allowed) {
+    const int skc = p.cfg >= 0 ? p.cfg : 1;  // 64 x 128 tiles: the best k-step rate
+    const int64_t tiles_max = (int64_t)((Mmax + kCfgBM[skc] - 1) / kCfgBM[skc]) * tiles_n;
+    if (skc != 0 && tiles_max <= p.sk_cnt_len) {
+      if (p.stream_k == 1) {
+        sk = true;
+      } else {
+        const int64_t tiles = (int64_t)((Mest + kCfgBM[skc] - 1) / kCfgBM[skc]) * tiles_n;
+        const int64_t units = tiles * ((p.K + 31) / 32);
+        // uneven last round, or too few tiles to cover the slots
+        sk = tiles < 4LL * slots && tiles % slots != 0 && units >= 2LL * p.sk_min_units;
+      }
+      if (sk) cfg = skc;
+    }
+  }
+  if (!sk) {
+    p.sk_cnt = nullptr;
+    p.sk_slab = nullptr;
+  }
   const int BMc = kCfgBM[cfg];
-  const int tiles_m = (Mmax + BMc - 1) / BMc, tiles_n = (p.N + 127) / 128;
-  int G = splits > 1 ? splits : tiles_m, W = splits > 1 ? tiles_m * tiles_n : tiles_n;
-  int64_t iters = 8LL * ((G + 7) / 8) * W;
-  int grid = (int)(iters < 1024 ? iters : 1024);
-  grid = (grid + 7) / 8 * 8;
+  const int tiles_m = (Mmax + BMc - 1) / BMc;
+  int grid;
+  if (sk) {
+    grid = slots;
+  } else {
+    const int G = splits > 1 ? splits : tiles_m, W = splits > 1 ? tiles_m * tiles_n : tiles_n;
+    const int64_t iters = 8LL * ((G + 7) / 8) * W;
+    grid = (int)(iters < 1024 ? iters : 1024);
+    grid = (grid + 7) / 8 * 8;
+  }
   dim3 g(grid);
   if (p.a_kmajor && p.b_kmajor) launch_cfg<true, true>(cfg, g, st, p);
   else if (p.a_kmajor && !p.b_kmajor) launch_cfg<true, false>(cfg, g, st, p);

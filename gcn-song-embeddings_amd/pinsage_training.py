@@ -216,6 +216,8 @@ class _FusedStep:
         # the device step (forward, loss, backward, Adam) is captured once into a
         # hipGraph and replayed: one launch instead of ~90 per step
         self.use_graph = os.environ.get("PINSAGE_HIPGRAPH", "1") != "0"
+        # Adam fused into the gradient reductions (0: separate optimizer pass)
+        self.fuse_adam = os.environ.get("PINSAGE_FUSED_ADAM", "1") != "0"
         self.graph = None
         self.graph_B = None
 
@@ -311,16 +313,32 @@ class _FusedStep:
         nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
                   "forward")
         nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
-        nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.ws), st), "backward")
+        self._backward(with_adam)
+
+    def _backward(self, with_adam):
+        """Backward; with_adam: Adam fused into the gradient reductions
+        (pinsage_engine_backward_adam, bitwise equal to backward + adam)."""
+        e = self.runner.engine
+        if with_adam and self.fuse_adam:
+            g = self.tr.optimizer.param_groups[0]
+            b1, b2 = g["betas"]
+            nat.check(nat.lib().pinsage_engine_backward_adam(
+                e.h, nat.ptr(self.ws), self._coef_ptr(), float(b1), float(b2), float(g["eps"]),
+                nat.stream_ptr()), "backward_adam")
+            return
+        nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(self.ws), nat.stream_ptr()),
+                  "backward")
         if with_adam:
             self._adam()
+
+    def _coef_ptr(self):
+        return ctypes.c_void_p(self.stage_view.data_ptr() + 3 * self.B_cur * 8)
 
     def _adam(self):
         g = self.tr.optimizer.param_groups[0]
         b1, b2 = g["betas"]
-        coef = ctypes.c_void_p(self.stage_view.data_ptr() + 3 * self.B_cur * 8)
-        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, coef, float(b1), float(b2),
-                                                float(g["eps"]), nat.stream_ptr()), "adam")
+        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, self._coef_ptr(), float(b1),
+                                                float(b2), float(g["eps"]), nat.stream_ptr()), "adam")
 
     def _signature(self, feats, table):
         return (self.runner.flat.data_ptr(), self.grads.data_ptr(), self.m.data_ptr(),
@@ -361,9 +379,7 @@ class _FusedStep:
             if not self._tuned:  # once: frontier sizes of a real batch pick the GEMM tiles
                 e.tune(self.ws)
                 self._tuned = True
-            nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.ws), st), "backward")
-            if not self.dist:
-                self._adam()
+            self._backward(with_adam=not self.dist)
             if self.use_graph and self._tuned and self.graph is None:
                 self._capture(B, sig)
         if self.dist:

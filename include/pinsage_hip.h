@@ -131,6 +131,18 @@ int pinsage_frontier_step(const int64_t* nodeset, int64_t n, const int32_t* nb_t
 int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
                    const float* W, const float* bias, int64_t N, int act, float* C, int64_t ldc,
                    void* stream);
+/* General form of the same GEMM, for per-configuration tests and
+ * microbenchmarks: C = op(A) op(B) with A K-major ([M][K], rows gathered by
+ * a_idx) or M-major ([K][M], k-rows gathered), B K-major ([N][K]) or N-major
+ * ([K][N], k-rows gathered by b_idx); epi 0 store, 1 accumulate, 3 split-K
+ * slabs C[splits][M][N]; cfg -1 picks the tile by size, 0..2 forces one;
+ * stream_k -1 chooses by size, 0 disables, 1 forces the stream-K schedule
+ * (in-launch combine of tiles cut between workgroups; scratch is owned by
+ * the library). */
+int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor, const float* A,
+                    int64_t lda, const int32_t* a_idx, const float* B, int64_t ldb,
+                    const int32_t* b_idx, float* C, int64_t ldc, const float* bias, int act,
+                    int epi, int splits, int cfg, int stream_k, void* stream);
 /* agg[f] = sum_t w[f][t] * q[loc[f][t]]  (weights already normalised;
  * pinsage_model.py:202). */
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
@@ -196,6 +208,13 @@ int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
  * a captured step graph picks up each step's values). */
 int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,
                         void* stream);
+/* backward followed by that Adam step, scheduled off the critical path: the
+ * last gradient (layer 0's Q) applies its own Adam step in the reduction that
+ * produces it, and every other parameter is updated beside that reduction.
+ * Gradients are still written to the grad buffer; the arithmetic is that of
+ * pinsage_engine_backward + pinsage_engine_adam. */
+int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, float beta1,
+                                 float beta2, float eps, void* stream);
 
 /* Frontier sizes of the last forward in ws (synchronises the stream): S[l] =
  * |S_l| (nodes convolved at layer l), N[l] = |N_l| (distinct neighbours). */

@@ -1,0 +1,129 @@
+"""The fp32 MFMA GEMM behind every projection (pinsage_model.py:196,201,208,
+211,223-224 forward; their autograd products backward) through the C-ABI
+entry pinsage_gemm_ex: every operand layout x tile configuration x schedule
+(data-parallel tiles / stream-K), ragged shapes, gathered rows, epilogues,
+against an fp64 product of the same fp32 operands.  Tolerance: the north
+star's 1e-4 relative (Frobenius), and stream-K results must be bitwise
+repeatable (its combine order is fixed, whichever workgroup arrives last).
+"""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-4
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _gemm(M, N, K, ak, bk, A, a_idx, B, C, bias=None, act=0, epi=0, splits=1, cfg=-1, sk=0):
+    import _native as nat
+    lib = nat.lib()
+    rc = lib.pinsage_gemm_ex(M, N, K, ak, bk, _vp(A), A.shape[1], _vp(a_idx), _vp(B), B.shape[1],
+                             None, _vp(C), C.shape[-1], _vp(bias), act, epi, splits, cfg, sk,
+                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    nat.check(rc, "gemm_ex")
+
+
+def _ref(M, N, K, ak, bk, A, a_idx, B, bias, act):
+    A64, B64 = A.double(), B.double()
+    if ak:
+        a = A64[a_idx.long()] if a_idx is not None else A64[:M]
+    else:
+        a = A64[:K, :M].t()
+    b = B64[:N, :K].t() if bk else B64[:K, :N]
+    r = a @ b
+    if bias is not None:
+        r = r + bias.double()
+    if act:
+        r = torch.nn.functional.leaky_relu(r, 0.01)
+    return r
+
+
+def _rel(x, r):
+    return ((x.double() - r).norm() / r.norm().clamp_min(1e-30)).item()
+
+
+SHAPES = [  # M, N, K: ragged M / K tails, N = 128 and multi-tile N, long K
+    (1, 128, 4),
+    (37, 128, 132),
+    (200, 256, 516),
+    (1000, 384, 128),
+    (64 * 9 + 5, 128, 2048),
+    (3000, 512, 512),
+]
+
+
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("sk", [0, 1])
+def test_gemm_layouts_configs_schedules(ak, bk, cfg, sk):
+    if sk and cfg == 0:
+        pytest.skip("stream-K runs the 64- and 32-row tiles")
+    g = torch.Generator(device="cuda").manual_seed(1234 + 10 * cfg + sk)
+    for M, N, K in SHAPES:
+        if not ak and M % 4:
+            M += 4 - M % 4  # M-major A needs M % 4 == 0 (launch_gemm)
+        A = torch.randn((M, K) if ak else (K, M), device="cuda", generator=g)
+        B = torch.randn((N, K) if bk else (K, N), device="cuda", generator=g)
+        a_idx = None
+        if ak and M > 1:
+            a_idx = torch.randint(0, M, (M,), device="cuda", generator=g, dtype=torch.int32)
+        bias = torch.randn(N, device="cuda", generator=g)
+        C = torch.full((M, N), float("nan"), device="cuda")
+        _gemm(M, N, K, ak, bk, A, a_idx, B, C, bias=bias, act=1, cfg=cfg, sk=sk)
+        torch.cuda.synchronize()
+        r = _ref(M, N, K, ak, bk, A, a_idx, B, bias, 1)
+        assert torch.isfinite(C).all(), (M, N, K)
+        assert _rel(C, r) < REL_TOL, (M, N, K, _rel(C, r))
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_stream_k_accumulate_and_repeatable(cfg):
+    # few tiles, long K: many workgroups per tile, combine by the last arriver
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, N, K = 100, 256, 8192
+    A = torch.randn(M, K, device="cuda", generator=g)
+    B = torch.randn(N, K, device="cuda", generator=g)
+    C0 = torch.randn(M, N, device="cuda", generator=g)
+    outs = []
+    for _ in range(3):
+        C = C0.clone()
+        _gemm(M, N, K, 1, 1, A, None, B, C, epi=1, cfg=cfg, sk=1)
+        outs.append(C)
+    torch.cuda.synchronize()
+    r = C0.double() + A.double() @ B.double().t()
+    assert _rel(outs[0], r) < REL_TOL
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+def test_stream_k_matches_data_parallel_schedule():
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 10541, 512, 512
+    A = torch.randn(M, K, device="cuda", generator=g)
+    idx = torch.randint(0, M, (M,), device="cuda", generator=g, dtype=torch.int32)
+    B = torch.randn(N, K, device="cuda", generator=g)
+    C_dp = torch.empty(M, N, device="cuda")
+    C_sk = torch.empty(M, N, device="cuda")
+    _gemm(M, N, K, 1, 1, A, idx, B, C_dp, cfg=1, sk=0)
+    _gemm(M, N, K, 1, 1, A, idx, B, C_sk, cfg=1, sk=1)
+    torch.cuda.synchronize()
+    r = A.double()[idx.long()] @ B.double().t()
+    assert _rel(C_dp, r) < REL_TOL and _rel(C_sk, r) < REL_TOL
+    assert ((C_dp - C_sk).abs().max() / r.abs().max()).item() < 1e-5
+
+
+def test_split_k_partials():
+    g = torch.Generator(device="cuda").manual_seed(3)
+    M, N, K, S = 128, 256, 3000, 6  # M-major A, N-major B: weight-gradient form
+    A = torch.randn(K, M, device="cuda", generator=g)
+    B = torch.randn(K, N, device="cuda", generator=g)
+    C = torch.empty(S, M, N, device="cuda")
+    _gemm(M, N, K, 0, 0, A, None, B, C, epi=3, splits=S)
+    torch.cuda.synchronize()
+    r = A.double().t() @ B.double()
+    assert _rel(C.sum(0), r) < REL_TOL

@@ -280,3 +280,60 @@ def test_train_step_vs_oracle_larger_graph():
                 assert _rel(v.cpu().numpy(), ref.p[k].detach().numpy()) < 1e-4, k
         finally:
             os.chdir(cwd)
+
+
+def test_fused_adam_matches_backward_plus_adam():
+    """pinsage_engine_backward_adam (Adam inside the gradient reductions)
+    against backward + adam, eager and as the captured step graph.  The
+    arithmetic is the same, but a step is not bitwise repeatable run to run
+    (the transposed-neighbour CSR is filled with atomics, which orders the dq
+    sums; repeated ids' loss gradients are added with float atomics), and
+    Adam's 1/sqrt(v) turns a rounding-level gradient change of a ~0 gradient
+    into up to +-lr on that element, which later steps amplify.  So: three
+    steps at lr = 0 (parameters fixed, the moments still accumulate) compare
+    gradients and moments within 1e-5 relative; one step at the trainer's lr
+    compares parameters element-wise within 2 * lr."""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(6000, 1500, 40000, seed=21)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(6000, 128, seed=22))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 30000, seed=23))
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp,
+                                        nbhds_path=os.path.join(tmp, "nb.pt"))
+            pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)  # neighbourhoods on disk
+
+            def run(fused, use_graph, steps, lr):
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
+                tr.batch_size = 256
+                if lr is not None:
+                    tr.optimizer.param_groups[0]["lr"] = lr
+                tr._fused = f = pt._FusedStep(tr)
+                f.fuse_adam = fused
+                f.use_graph = use_graph
+                torch.manual_seed(6)
+                for _ in range(steps):
+                    batch, _ = tr.next_batch()
+                    tr.train_batch(batch)
+                torch.cuda.synchronize()
+                return ([t.detach().clone() for t in (f.runner.flat, f.grads, f.m, f.v)],
+                        tr.optimizer.param_groups[0]["lr"])
+
+            base, _ = run(False, False, 3, 0.0)
+            for fused, use_graph in ((True, False), (True, True)):
+                other, _ = run(fused, use_graph, 3, 0.0)
+                assert torch.equal(base[0], other[0])
+                for a, b in zip(base[1:], other[1:]):
+                    assert ((a - b).norm() / a.norm()).item() < 1e-5
+            p0, lr = run(False, False, 1, None)
+            p1, _ = run(True, False, 1, None)
+            assert ((p0[0] - p1[0]).abs() <= 2 * lr + 1e-7).all()
+            assert ((p0[0] - p1[0]).norm() / p0[0].norm()).item() < 1e-5
+        finally:
+            os.chdir(cwd)

@@ -1,0 +1,87 @@
+"""Microbenchmark of the fp32 MFMA GEMM through the C-ABI (pinsage_gemm_ex).
+
+    python tools/gemm_bench.py [--reps 50] [--shapes M,N,K,ak,bk[,gather] ...]
+
+Times each shape under every tile configuration (and the size-based pick)
+with HIP events on the launch stream; prints µs per launch and TF/s.  The
+default shapes are the C2 train step's projections (bench.py config c2).
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "gcn-song-embeddings_amd"))
+import _native as nat  # noqa: E402
+
+DEFAULT = [
+    "10541,512,512,1,1,1",    # fwd Q l0: gathered h rows x Q^T
+    "5716,128,1024,1,1,1",    # fwd W l0 (first K segment gathered)
+    "2600,512,128,1,1,1",     # fwd Q l1
+    "1500,128,640,1,1,1",     # fwd W l1
+    "5716,1024,128,1,0,0",    # bwd dcat l0 = dY W
+    "10541,512,512,1,0,0",    # bwd dh l0 = dpq Q (scatter-add in the engine)
+    "8192,512,512,1,1,0",     # reference square-ish shape: 512 tiles of 64x128
+]
+
+
+def vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def run(shape, cfg, sk, reps, lib, stream):
+    # M,N,K,ak,bk[,gather[,splits]]: gather = rows of A (K-major A) or k-rows
+    # of B (N-major B, the weight-gradient form); splits > 1 = split-K slabs
+    M, N, K, ak, bk, *g = [int(x) for x in shape.split(",")]
+    gather = bool(g and g[0])
+    splits = g[1] if len(g) > 1 else 1
+    dev = "cuda"
+    A = torch.randn((M if ak else K), (K if ak else M), device=dev)
+    B = torch.randn((N if bk else K), (K if bk else N), device=dev)
+    C = torch.empty(splits, M, N, device=dev)
+    a_idx = torch.randperm(M, device=dev).to(torch.int32) if gather and ak else None
+    b_idx = torch.randperm(K, device=dev).to(torch.int32) if gather and not ak and not bk else None
+    args = (M, N, K, ak, bk, vp(A), A.shape[1], vp(a_idx), vp(B), B.shape[1], vp(b_idx), vp(C), N,
+            None, 0, 3 if splits > 1 else 0, splits, cfg, sk, ctypes.c_void_p(stream.cuda_stream))
+    rc = lib.pinsage_gemm_ex(*args)
+    if rc != 0:
+        raise RuntimeError(lib.pinsage_last_error().decode())
+    ref = (A[a_idx.long()] if a_idx is not None else A) if ak else A.t()
+    ref = ref @ ((B.t() if bk else (B[b_idx.long()] if b_idx is not None else B)))
+    err = ((C.sum(0) - ref).abs().max() / ref.abs().max()).item()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        lib.pinsage_gemm_ex(*args)
+    e0.record(stream)
+    for _ in range(reps):
+        lib.pinsage_gemm_ex(*args)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    return us, 2.0 * M * N * K / us / 1e6, err
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--shapes", nargs="*", default=DEFAULT)
+    ap.add_argument("--cfgs", default="-1,0,1,2")
+    ap.add_argument("--sk", default="0,1", help="stream-K settings (-1 auto, 0 off, 1 on)")
+    a = ap.parse_args()
+    lib = nat.lib()
+    stream = torch.cuda.current_stream()
+    for s in a.shapes:
+        for cfg in [int(c) for c in a.cfgs.split(",")]:
+            for sk in [int(c) for c in a.sk.split(",")]:
+                if sk == 1 and cfg == 0:
+                    continue
+                us, tf, err = run(s, cfg, sk, a.reps, lib, stream)
+                print(f"{s:24s} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
+                      flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,46 @@
+"""Print one train step's kernel timeline from a rocprofv3 kernel trace.
+
+    python tools/timeline.py gpurun_out/prof/run_kernel_trace.csv [--step -3]
+
+Steps are delimited by the Adam kernel (the last launch of a step).  For the
+chosen step every dispatch is listed with its queue, start offset and duration
+(µs) relative to the end of the previous step's Adam, so gaps between
+dependent launches and the overlap of the side streams are visible.
+"""
+import argparse
+import csv
+import re
+
+
+def short(n):
+    n = re.sub(r"\(.*", "", n.replace("void ", ""))
+    return n[:64]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--step", type=int, default=-3)
+    ap.add_argument("--delim", default="adam_kernel")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if a.delim in r["Kernel_Name"]]
+    k = ends[a.step]
+    lo = ends[a.step - 1] + 1
+    t0 = int(rows[lo - 1]["End_Timestamp"])
+    busy = 0
+    last_end = t0
+    for r in rows[lo:k + 1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        busy += max(0, e - max(s, last_end))
+        last_end = max(last_end, e)
+        grid = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
+        print(f"q{r['Queue_Id']:>2} {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {grid:6d}  "
+              f"{short(r['Kernel_Name'])}")
+    total = (int(rows[k]["End_Timestamp"]) - t0) / 1e3
+    print(f"step span {total:.1f} us, some kernel running {busy / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
