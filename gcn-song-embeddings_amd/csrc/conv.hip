@@ -41,7 +41,15 @@ __global__ void layer_prep_kernel(const int32_t* __restrict__ S_mem, const int* 
                                   const unsigned long long* __restrict__ S_bits,
                                   const uint32_t* __restrict__ S_pref,
                                   const int64_t* __restrict__ ids, int64_t n_ids,
-                                  int32_t* __restrict__ pos_rank) {
+                                  int32_t* __restrict__ pos_rank, float* __restrict__ z, int z_n,
+                                  const int* __restrict__ z_rows) {
+  if (z) {  // zero the layer below's dY rows: the backward scatter-adds into them
+    const int64_t zn4 = (int64_t)(*z_rows) * z_n / 4;
+    float4* z4 = reinterpret_cast<float4*>(z);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zn4;
+         i += (int64_t)gridDim.x * blockDim.x)
+      z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   const int64_t FS = (int64_t)(*nS), FN = (int64_t)(*nN);
   const int64_t total = FS * T + FS + FN + n_ids;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -976,11 +984,13 @@ int launch_layer_prep(const int32_t* S_mem, const int* nS, int64_t S_max, const 
                       const uint32_t* P_pref, const int32_t* nb, const float* wn, int64_t ldT,
                       int T, int32_t* self_src, int32_t* q_src, int32_t* loc, float* wloc,
                       const unsigned long long* S_bits, const uint32_t* S_pref, const int64_t* ids,
-                      int64_t n_ids, int32_t* pos_rank, hipStream_t st) {
+                      int64_t n_ids, int32_t* pos_rank, float* z, int z_n, const int* z_rows,
+                      hipStream_t st) {
+  PS_REQUIRE(!z || z_n % 4 == 0, kErrArg, "layer_prep: zeroed rows must be a multiple of 4 wide");
   const int64_t tot = S_max * T + S_max + N_max + n_ids;
   hipLaunchKernelGGL(layer_prep_kernel, dim3(grid_for(tot, 256)), dim3(256), 0, st, S_mem, nS, N_mem,
                      nN, N_bits, N_pref, P_bits, P_pref, nb, wn, ldT, T, self_src, q_src, loc, wloc,
-                     S_bits, S_pref, ids, n_ids, pos_rank);
+                     S_bits, S_pref, ids, n_ids, pos_rank, z, z_n, z_rows);
   PS_CHECK_LAUNCH();
   return kOk;
 }

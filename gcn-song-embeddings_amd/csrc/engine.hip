@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -36,7 +37,7 @@ int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const
                       const unsigned long long*, const uint32_t*, const unsigned long long*,
                       const uint32_t*, const int32_t*, const float*, int64_t, int, int32_t*,
                       int32_t*, int32_t*, float*, const unsigned long long*, const uint32_t*,
-                      const int64_t*, int64_t, int32_t*, hipStream_t);
+                      const int64_t*, int64_t, int32_t*, float*, int, const int*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_csr_build(const int32_t*, const int*, int64_t, int, const int*, int64_t, int*, int*,
@@ -58,6 +59,11 @@ int csr_prepare();
 int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, const float*,
                            float*, const AdamSlice*, hipStream_t);
 int launch_gather_out(const float*, int, const int32_t*, int64_t, float*, hipStream_t);
+int launch_head_fwd(const float*, int, const int*, int64_t, const float*, const float*,
+                    const float*, float*, float*, hipStream_t);
+int launch_head_bwd(const float*, int, const int*, int64_t, const float*, const float*,
+                    const float*, const float*, const float*, float*, float*, float*, int,
+                    const int*, int*, int64_t, hipStream_t);
 int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
                         int*, float*, hipStream_t);
 
@@ -101,6 +107,15 @@ struct TimingSite {
 struct Engine {
   EngineConfig cfg{};
   bool timing = false;
+  // Which backward work runs beside the caller's stream (PINSAGE_BWD_STREAMS):
+  // 0 the CSR builds and the weight gradients, 1 nothing, 2 the CSR builds
+  // (default), 3 the weight gradients.  Measured at C2 (bench.py): 2.27M /
+  // 2.32M / 2.33M / 2.12M target nodes/s -- weight gradients beside the chain
+  // take CUs from it and add cross-queue waits; the CSR builds (independent
+  // of the head backward) are worth their one wait per layer.
+  int stream_mode = getenv("PINSAGE_BWD_STREAMS") ? atoi(getenv("PINSAGE_BWD_STREAMS")) : 2;
+  // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
+  bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   std::vector<TimingSite> sites;
   std::vector<LayerBuf> L;
   int64_t pG1w = 0, pG1b = 0, pG2w = 0, n_params = 0;
@@ -108,7 +123,11 @@ struct Engine {
   size_t bits_begin = 0, bits_end = 0;  // all bitmaps contiguous (one memset)
   size_t block_sums = 0, ids = 0, pos_rank = 0, H1 = 0, Z = 0, dZ = 0, dP1 = 0;
   size_t G = 0, Kc = 0, part = 0, scal = 0, slab = 0, bslab = 0, varpart = 0;
+  size_t slab_main = 0, bslab_main = 0;  // split-K slabs of the main stream's weight gradient
   int64_t slab_floats = 0;
+  // stream-K scratch of the main stream's GEMMs (gemm.h)
+  size_t sk_slab = 0, sk_cnt = 0;
+  int64_t sk_cnt_len = 0;
   size_t total = 0;
   int64_t max_bsum_blocks = 0;
   // external device pointers (owned by the caller)
@@ -146,6 +165,7 @@ static int ensure_streams(Engine& E) {
 }
 // `to` waits for everything enqueued so far on `from`
 static int dep(Engine& E, hipStream_t from, hipStream_t to) {
+  if (from == to) return kOk;
   hipEvent_t e = E.ev[(size_t)(E.ev_next++ % kEvents)];
   PS_CHECK_HIP(hipEventRecord(e, from));
   PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
@@ -299,12 +319,31 @@ static void layout(Engine& E) {
   E.slab_floats = slab;
   E.slab = carve(cur, slab * 4);
   E.bslab = carve(cur, kMaxSplits * std::max(c.hid, c.out) * 4);
+  E.slab_main = carve(cur, slab * 4);
+  E.bslab_main = carve(cur, kMaxSplits * std::max(c.hid, c.out) * 4);
+  {
+    int64_t max_rows = 0, max_cols = std::max(c.hid, c.out);
+    for (auto& lb : E.L) {
+      max_rows = std::max({max_rows, lb.S.cap, lb.N.cap});
+      max_cols = std::max(max_cols, lb.d + c.hid);
+    }
+    E.sk_cnt_len = ceil_div(max_rows, 32) * ceil_div(max_cols, 128);
+    E.sk_cnt = carve(cur, E.sk_cnt_len * 4);
+    E.sk_slab = carve(cur, gemm_sk_slab_floats() * 4);
+  }
   E.total = (size_t)align_up((int64_t)cur, 256);
 }
 
 template <class T>
 static inline T* at(void* ws, size_t off) {
   return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+// main-stream GEMMs may run stream-K (launch_gemm decides by shape)
+static inline void with_sk(const Engine& E, void* ws, GemmParams& p) {
+  p.sk_slab = at<float>(ws, E.sk_slab);
+  p.sk_cnt = at<int>(ws, E.sk_cnt);
+  p.sk_cnt_len = E.sk_cnt_len;
 }
 
 // ---------------------------------------------------------------- forward
@@ -358,7 +397,9 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
                              prev ? pref(*prev) : nullptr, E.nb, E.wn, E.ldT, T,
                              at<int32_t>(ws, lb.self_src), at<int32_t>(ws, lb.q_src),
                              at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), bits(top.S),
-                             pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank), st));
+                             pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank),
+                             prev ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr, (int)c.out,
+                             prev ? cnt(*prev) : nullptr, st));
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
     const int64_t ldh = l == 0 ? E.ld_f : c.out;
     // Q projection of the distinct neighbours: lrelu(h[u] Q^T + b)
@@ -379,6 +420,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
     q.act = true;
     {
       Timed tt(E, lname("fwd.q_gemm", l), st);
+      with_sk(E, ws, q);
       PS_TRY(launch_gemm(q, st));
     }
     Timed t_agg(E, lname("fwd.agg", l), st);
@@ -406,10 +448,15 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
     w.epi = kEpiL2Norm;
     w.norms = at<float>(ws, lb.nrm);
     Timed tw(E, lname("fwd.w_gemm", l), st);
+    with_sk(E, ws, w);
     PS_TRY(launch_gemm(w, st));
   }
   // head: G2(lrelu(G1 y))
   Timed t_head(E, "fwd.head", st);
+  if (E.fused_head)
+    return launch_head_fwd(at<float>(ws, top.y), (int)c.out, cnt(top.S), top.S.cap,
+                           E.params + E.pG1w, E.params + E.pG1b, E.params + E.pG2w,
+                           at<float>(ws, E.H1), at<float>(ws, E.Z), st);
   GemmParams g1;
   g1.M_dev = cnt(top.S);
   g1.M_hint = (int)top.S.hint;
@@ -431,8 +478,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   g2.c = at<float>(ws, E.Z);
   g2.bias = nullptr;
   g2.act = false;
-  PS_TRY(launch_gemm(g2, st));
-  return kOk;
+  return launch_gemm(g2, st);
 }
 
 // Weight gradient dst[M][N] = A^T [B || B2] over the device row count (split-K
@@ -483,8 +529,13 @@ static AdamSlice adam_slice(const Engine& E, const AdamStep& a, int64_t w_off, i
 
 // after_use: with Adam fused, the reduction (which updates the parameter)
 // waits for this event, recorded behind the main stream's last read of it
+// main: the launch runs on the main stream (its own slabs; the
+// weight-gradient stream may be using the others meanwhile)
 static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st,
-                       const AdamSlice* adam = nullptr, hipEvent_t after_use = nullptr) {
+                       const AdamSlice* adam = nullptr, hipEvent_t after_use = nullptr,
+                       bool main = false) {
+  float* const slab = at<float>(ws, main ? E.slab_main : E.slab);
+  float* const bslab = at<float>(ws, main ? E.bslab_main : E.bslab);
   int cfg = 0, S = 1;
   choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
   GemmParams p;
@@ -505,26 +556,26 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st,
     p.b2 = w.B2;
     p.ldb2 = w.ldb2;
   }
-  p.c = at<float>(ws, E.slab);
+  p.c = slab;
   p.ldc = w.N;
   p.epi = kEpiPartial;
   p.splits = S;
-  p.bias_part = w.dst_b ? at<float>(ws, E.bslab) : nullptr;
+  p.bias_part = w.dst_b ? bslab : nullptr;
   PS_REQUIRE((int64_t)S * w.M * w.N <= E.slab_floats, kErrWorkspace, "engine: split-K slab too small");
   PS_TRY(launch_gemm(p, st));
   if (adam && after_use) PS_CHECK_HIP(hipStreamWaitEvent(st, after_use, 0));
-  return launch_reduce_slabs_2d(at<float>(ws, E.slab), S, (int64_t)w.M * w.N, w.M, w.N, w.dst,
+  return launch_reduce_slabs_2d(slab, S, (int64_t)w.M * w.N, w.M, w.N, w.dst,
                                 w.ld_dst, p.bias_part, w.dst_b, adam, st);
 }
 
 // ---------------------------------------------------------------- backward
 // Starts from dZ (gradient of the head output rows of the unique top nodes).
-// adam != nullptr: the step ends with torch.optim.Adam.  The last gradient,
-// dQ of layer 0, is the step's tail on the weight-gradient stream: its
-// reduction applies Q0's Adam itself, while the main stream (its own chain
-// done) applies Adam to every other parameter (contiguous behind Q0 in the
-// flat layout) once their gradients exist -- the optimizer pass is off the
-// critical path.  No other reduction waits on the main stream.
+// The last gradient, dQ of layer 0, depends on the end of the main chain, so
+// it runs on the main stream itself (no cross-queue hop at the step's tail).
+// adam != nullptr: the step ends with torch.optim.Adam: Q0's reduction applies
+// Q0's Adam itself, and the weight-gradient stream updates every other
+// parameter (contiguous behind Q0 in the flat layout) once the main stream has
+// read W0 for the last time -- the optimizer pass is off the critical path.
 int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   const EngineConfig& c = E.cfg;
   PS_REQUIRE(E.grads, kErrArg, "engine: grad buffer not set");
@@ -532,7 +583,6 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   const LayerBuf& l0 = E.L[0];
   PS_REQUIRE(!adam || (l0.pQw == 0 && l0.pQb == l0.pQw + c.hid * l0.d && l0.pWw == l0.pQb + c.hid),
              kErrArg, "engine: Q0 must lead the flat parameter layout");
-  hipEvent_t others_ready = nullptr;  // s_wg: every gradient but Q0's is written
   const int Lc = (int)c.n_layers, T = (int)c.T;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
@@ -540,6 +590,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   float* gr = E.grads;
   PS_TRY(ensure_streams(E));
   hipStream_t s_csr = E.side[0], s_wg = E.side[1];
+  if (E.stream_mode == 1 || E.stream_mode == 3) s_csr = st;
+  if (E.stream_mode == 1 || E.stream_mode == 2) s_wg = st;
   // the transposes of the neighbour slots depend only on the forward: build
   // them beside the head backward; events mark each layer's CSR done
   PS_TRY(dep(E, st, s_csr));
@@ -558,25 +610,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   }
   // weight gradients run on s_wg, each forked once its inputs exist on st
   Timed t_hb(E, "bwd.head", st);
-  PS_TRY(dep(E, st, s_wg));  // dZ, H1 ready: dG2 (its reduction also waits for dP1)
-  {
-    GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
-    p.M_dev = cnt(top.S);
-    p.M_hint = (int)top.S.hint;
-    p.M_max = (int)top.S.cap;
-    p.N = o;
-    p.K = o;
-    p.a = at<float>(ws, E.dZ);
-    p.lda = o;
-    p.b_kmajor = false;
-    p.b = E.params + E.pG2w;
-    p.ldb = o;
-    p.c = at<float>(ws, E.dP1);
-    p.ldc = o;
-    p.mask = at<float>(ws, E.H1);
-    p.ldm = o;
-    PS_TRY(launch_gemm(p, st));
-  }
+  PS_TRY(dep(E, st, s_wg));  // dZ, H1 ready: dG2 beside the head backward
   {
     Timed tw(E, "bwd.wgrad.head", s_wg);
     WGrad w;
@@ -593,8 +627,44 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.ld_dst = o;
     PS_TRY(weight_grad(E, ws, w, s_wg));
   }
+  // dP1 = (dZ G2) * lrelu'(H1), dY_top = dP1 G1 and the top layer's
+  // normalisation backward (dp_top) in one kernel, which also zeroes the
+  // loss's multiplicity counters (the dY scatter-add targets of the layers
+  // below were zeroed by the forward's layer_prep)
+  if (E.fused_head) {
+    PS_TRY(launch_head_bwd(at<float>(ws, E.dZ), o, cnt(top.S), top.S.cap, at<float>(ws, E.H1),
+                           E.params + E.pG1w, E.params + E.pG2w, at<float>(ws, top.y),
+                           at<float>(ws, top.nrm), at<float>(ws, E.dP1), at<float>(ws, top.dp),
+                           nullptr, o, nullptr, at<int>(ws, E.Kc), 3 * top.S.cap, st));
+  } else {
+    GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
+    p.M_dev = cnt(top.S);
+    p.M_hint = (int)top.S.hint;
+    p.M_max = (int)top.S.cap;
+    p.N = o;
+    p.K = o;
+    p.a = at<float>(ws, E.dZ);
+    p.lda = o;
+    p.b_kmajor = false;
+    p.b = E.params + E.pG2w;
+    p.ldb = o;
+    p.c = at<float>(ws, E.dP1);
+    p.ldc = o;
+    p.mask = at<float>(ws, E.H1);
+    p.ldm = o;
+    PS_TRY(launch_gemm(p, st));
+    GemmParams q = p;  // dY_top = dP1 G1
+    q.a = at<float>(ws, E.dP1);
+    q.b = E.params + E.pG1w;
+    q.c = at<float>(ws, top.dY);
+    q.mask = nullptr;
+    PS_TRY(launch_gemm(q, st));
+    PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, top.y), at<float>(ws, top.nrm),
+                                 at<float>(ws, top.dY), o, cnt(top.S), top.S.cap,
+                                 at<float>(ws, top.dp), nullptr, o, nullptr, at<int>(ws, E.Kc),
+                                 3 * top.S.cap, st));
+  }
   PS_TRY(dep(E, st, s_wg));
-  WGrad g1_wgrad;
   {
     WGrad w;  // dG1 and db1
     w.A = at<float>(ws, E.dP1);
@@ -609,27 +679,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.dst = gr + E.pG1w;
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
-    g1_wgrad = w;
-  }
-  {
-    GemmParams p;  // dY_top = dP1 G1
-    p.M_dev = cnt(top.S);
-    p.M_hint = (int)top.S.hint;
-    p.M_max = (int)top.S.cap;
-    p.N = o;
-    p.K = o;
-    p.a = at<float>(ws, E.dP1);
-    p.lda = o;
-    p.b_kmajor = false;
-    p.b = E.params + E.pG1w;
-    p.ldb = o;
-    p.c = at<float>(ws, top.dY);
-    p.ldc = o;
-    PS_TRY(launch_gemm(p, st));
-  }
-  {
     Timed tw(E, "bwd.wgrad.head", s_wg);
-    PS_TRY(weight_grad(E, ws, g1_wgrad, s_wg));
+    PS_TRY(weight_grad(E, ws, w, s_wg));
   }
   t_hb.stop();
   for (int l = Lc - 1; l >= 0; --l) {
@@ -640,12 +691,10 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     const int64_t ldh = l == 0 ? E.ld_f : c.out;
     float* dp = at<float>(ws, lb.dp);
     float* dYprev = l > 0 ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr;
-    // dp = d(normalize(lrelu(.))); also zeroes dY_{l-1} (scatter-add target
-    // below) and, at the top layer, the loss's multiplicity counters
-    PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
-                                 o, cnt(lb.S), lb.S.cap, dp, dYprev, o,
-                                 l > 0 ? cnt(E.L[(size_t)l - 1].S) : nullptr,
-                                 l == Lc - 1 ? at<int>(ws, E.Kc) : nullptr, 3 * top.S.cap, st));
+    // dp = d(normalize(lrelu(.))); the top layer's came out of the head backward
+    if (l < Lc - 1)
+      PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
+                                   o, cnt(lb.S), lb.S.cap, dp, nullptr, o, nullptr, nullptr, 0, st));
     PS_TRY(dep(E, st, s_wg));
     WGrad w_wgrad;
     {
@@ -696,11 +745,19 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
         p.c = at<float>(ws, lb.dagg);
         p.ldc = hd;
       }
+      with_sk(E, ws, p);
       PS_TRY(launch_gemm(p, st));
     }
     {
       Timed tw(E, lname("bwd.w_wgrad", l), s_wg);
       PS_TRY(weight_grad(E, ws, w_wgrad, s_wg));
+    }
+    if (adam && l == 0) {  // every gradient but Q0's exists on s_wg; W0 was read last
+      PS_TRY(dep(E, st, s_wg));
+      Timed ta(E, "adam", s_wg);
+      PS_TRY(launch_adam(E.params + l0.pWw, E.grads + l0.pWw, E.adam_m + l0.pWw, E.adam_v + l0.pWw,
+                         E.n_params - l0.pWw, adam->coef, adam->beta1, adam->beta2, adam->eps,
+                         s_wg));
     }
     PS_CHECK_HIP(hipStreamWaitEvent(st, csr_done[(size_t)l], 0));
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
@@ -708,7 +765,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
                             at<int>(ws, lb.off), at<int32_t>(ws, lb.occ), at<float>(ws, lb.wloc), T,
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
                             at<float>(ws, lb.dqpart), st));
-    PS_TRY(dep(E, st, s_wg));
+    if (l > 0) PS_TRY(dep(E, st, s_wg));
     WGrad q_wgrad;
     {
       // dQ = dpq^T h[q_src], dQb = colsum(dpq)
@@ -744,24 +801,16 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       p.ldc = o;
       p.c_idx = at<int32_t>(ws, lb.q_src);
       p.epi = kEpiAccum;
+      with_sk(E, ws, p);
       PS_TRY(launch_gemm(p, st));
     }
     {
       AdamSlice q0;
-      if (adam && l == 0) {
-        others_ready = E.ev[(size_t)(E.ev_next++ % kEvents)];
-        PS_CHECK_HIP(hipEventRecord(others_ready, s_wg));
-        q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
-      }
-      Timed tq(E, lname("bwd.q_wgrad", l), s_wg);
-      PS_TRY(weight_grad(E, ws, q_wgrad, s_wg, adam && l == 0 ? &q0 : nullptr));
+      if (adam && l == 0) q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
+      hipStream_t qs = l == 0 ? st : s_wg;
+      Timed tq(E, lname("bwd.q_wgrad", l), qs);
+      PS_TRY(weight_grad(E, ws, q_wgrad, qs, adam && l == 0 ? &q0 : nullptr, nullptr, l == 0));
     }
-  }
-  if (adam) {  // Adam on everything behind Q0, beside Q0's weight gradient
-    PS_CHECK_HIP(hipStreamWaitEvent(st, others_ready, 0));
-    Timed ta(E, "adam", st);
-    PS_TRY(launch_adam(E.params + l0.pWw, E.grads + l0.pWw, E.adam_m + l0.pWw, E.adam_v + l0.pWw,
-                       E.n_params - l0.pWw, adam->coef, adam->beta1, adam->beta2, adam->eps, st));
   }
   // every gradient is written once the side streams drain into st
   PS_TRY(dep(E, s_csr, st));
@@ -769,7 +818,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   return kOk;
 }
 
-// Zero the regions that kernels keep zero after use (loss G / Kc, CSR counts):
+// Zero the regions that kernels keep zero after use (loss G / Kc, CSR counts,
+// stream-K tickets):
 // once per workspace, before its first step.
 int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
   const EngineConfig& c = E.cfg;
@@ -778,6 +828,7 @@ int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.Kc), 0, (size_t)(3 * top) * 4, st));
   for (auto& lb : E.L)
     PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, lb.cnt), 0, (size_t)(lb.N.cap + 1) * 4, st));
+  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.sk_cnt), 0, (size_t)E.sk_cnt_len * 4, st));
   return kOk;
 }
 

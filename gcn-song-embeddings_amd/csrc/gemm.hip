@@ -617,16 +617,18 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
       (p.a_kmajor || !p.a_idx) && (p.b_kmajor || (!p.b_idx && !p.b2_idx));
   bool sk = false;
   if (sk_allowed) {
-    const int skc = p.cfg >= 0 ? p.cfg : 1;  // 64 x 128 tiles: the best k-step rate
+    // by measurement (tools/gemm_bench.py): stream-K pays for long-K launches
+    // whose 32-row tiles leave most slots idle (a lone workgroup per CU runs
+    // ~1 us per k-step); the per-piece fill / publish / combine (~8 us) eats
+    // the gain on short K and on launches that already fill the chip
+    const int skc = p.stream_k == 1 ? (p.cfg >= 0 ? p.cfg : 1) : 2;
     const int64_t tiles_max = (int64_t)((Mmax + kCfgBM[skc] - 1) / kCfgBM[skc]) * tiles_n;
     if (skc != 0 && tiles_max <= p.sk_cnt_len) {
       if (p.stream_k == 1) {
         sk = true;
-      } else {
+      } else if (p.cfg < 0) {
         const int64_t tiles = (int64_t)((Mest + kCfgBM[skc] - 1) / kCfgBM[skc]) * tiles_n;
-        const int64_t units = tiles * ((p.K + 31) / 32);
-        // uneven last round, or too few tiles to cover the slots
-        sk = tiles < 4LL * slots && tiles % slots != 0 && units >= 2LL * p.sk_min_units;
+        sk = p.K >= 512 && tiles <= slots / 2;
       }
       if (sk) cfg = skc;
     }

@@ -1,0 +1,276 @@
+// The PinSage head as two fused row-block kernels (pinsage_model.py:223-224,
+// G2(leaky_relu(G1 y)); and its backward down to the top conv layer's
+// normalisation).  Each workgroup owns 32 rows of the top frontier and keeps
+// the whole 128-wide row chain on chip: both 128 x 128 weights are staged in
+// LDS once, the intermediate rows never leave the CU, and one launch replaces
+// two GEMM launches forward and two GEMMs plus the top layer's
+// normalisation backward in reverse.  The rows are few (one per distinct top
+// node), so the kernels are latency-bound; what they save is launches and
+// round trips, not FLOPs.
+//
+// MFMA convention as in gemm.hip (v_mfma_f32_32x32x2_f32): in the r-th MFMA of
+// k-octet s, lane (l32, h) supplies k = 8s + 4h + r; accumulator element r of
+// lane (l32, h) is row (r & 3) + 8 (r >> 2) + 4h, column l32 of the 32 x 32 tile.
+#include "common.h"
+
+namespace ps {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kHeadRows = 32;   // rows per workgroup
+constexpr int kHeadDim = 128;   // out_dim capacity (4 waves x 32 columns)
+constexpr int kHeadLd = 132;    // padded LDS row (floats): b128 fragment reads spread banks
+
+// acc = A[32][K] * B, A rows in sA (ld kHeadLd).  B(k, n) = sW[n][k] (kNK:
+// an nn.Linear weight [out][in] used as x W^T; b128 fragment reads) or
+// sW[k][n] (!kNK: the weight used as dY W; four b32 reads, consecutive lanes
+// on consecutive n).  Fragments of octet s+1 are read while octet s's MFMAs
+// run (sched_barrier pins that order).
+template <bool kNK>
+__device__ __forceinline__ float4 head_bfrag(const float* sW, int n, int k4) {
+  if constexpr (kNK) {
+    return *reinterpret_cast<const float4*>(sW + n * kHeadLd + k4);
+  } else {
+    return make_float4(sW[(k4 + 0) * kHeadLd + n], sW[(k4 + 1) * kHeadLd + n],
+                       sW[(k4 + 2) * kHeadLd + n], sW[(k4 + 3) * kHeadLd + n]);
+  }
+}
+template <bool kNK>
+__device__ __forceinline__ f32x16 head_mm(const float* sA, const float* sW, int n0, int l32,
+                                          int h) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const float* arow = sA + l32 * kHeadLd + 4 * h;
+  float4 a = *reinterpret_cast<const float4*>(arow);
+  float4 b = head_bfrag<kNK>(sW, n0 + l32, 4 * h);
+#pragma unroll
+  for (int s = 0; s < kHeadDim / 8; ++s) {
+    float4 an = a, bn = b;
+    if (s + 1 < kHeadDim / 8) {
+      an = *reinterpret_cast<const float4*>(arow + 8 * (s + 1));
+      bn = head_bfrag<kNK>(sW, n0 + l32, 8 * (s + 1) + 4 * h);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    a = an;
+    b = bn;
+  }
+  return acc;
+}
+
+// rows [r0, r0+32) of src[R][o] -> sA (zero outside), all threads
+// (every global load of a staging pass is issued before the first LDS write:
+// one memory round trip per pass, not one per float4)
+__device__ __forceinline__ void head_load_rows(float* sA, const float* __restrict__ src, int64_t r0,
+                                               int64_t R, int o, int tid) {
+  constexpr int NI = kHeadRows * (kHeadDim / 4) / 256;
+  float4 v[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
+    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + row < R && c < o) v[j] = *reinterpret_cast<const float4*>(src + (r0 + row) * o + c);
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
+    *reinterpret_cast<float4*>(sA + row * kHeadLd + c) = v[j];
+  }
+}
+// W[o][o] row-major -> sW (same layout, zero padded to 128 x 128)
+__device__ __forceinline__ void head_load_weight(float* sW, const float* __restrict__ W, int o,
+                                                 int tid) {
+  constexpr int NI = kHeadDim * (kHeadDim / 4) / 256;
+  float4 v[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
+    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < o && c < o) v[j] = *reinterpret_cast<const float4*>(W + (int64_t)row * o + c);
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
+    *reinterpret_cast<float4*>(sW + row * kHeadLd + c) = v[j];
+  }
+}
+
+__device__ __forceinline__ int head_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// H1 = lrelu(y G1^T + b1), Z = H1 G2^T over the *nrows rows of y
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int o,
+                                                       const int* __restrict__ nrows,
+                                                       const float* __restrict__ G1w,
+                                                       const float* __restrict__ G1b,
+                                                       const float* __restrict__ G2w,
+                                                       float* __restrict__ H1,
+                                                       float* __restrict__ Z) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* sA = lds;
+  float* sW1 = sA + kHeadRows * kHeadLd;
+  float* sW2 = sW1 + kHeadDim * kHeadLd;
+  const int64_t R = *nrows;
+  const int64_t r0 = (int64_t)blockIdx.x * kHeadRows;
+  if (r0 >= R) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int n0 = 32 * w, col = n0 + l32;
+  head_load_rows(sA, y, r0, R, o, tid);
+  head_load_weight(sW1, G1w, o, tid);
+  head_load_weight(sW2, G2w, o, tid);
+  __syncthreads();
+  f32x16 acc = head_mm<true>(sA, sW1, n0, l32, h);
+  const float b = col < o ? G1b[col] : 0.f;
+  __syncthreads();  // every wave is done reading y from sA
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    const float v = col < o ? lrelu(acc[r] + b) : 0.f;
+    sA[row * kHeadLd + col] = v;
+    if (r0 + row < R && col < o) H1[(r0 + row) * o + col] = v;
+  }
+  __syncthreads();
+  acc = head_mm<true>(sA, sW2, n0, l32, h);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    if (r0 + row < R && col < o) Z[(r0 + row) * o + col] = acc[r];
+  }
+}
+
+// From dZ: dP1 = (dZ G2) * lrelu'(H1); dY = dP1 G1; then the top conv layer's
+// normalisation backward (y = u / ||u||, u = lrelu(pre)):
+//   dp = lrelu'(y) * (dY - y (y . dY)) / ||u||
+// Also zeroes z[0 .. *z_rows * z_n) (the next layer's scatter-add target) and
+// zi[0 .. zi_n) (the loss's multiplicity counters) grid-wide, as the unfused
+// normalisation backward did.
+__global__ __launch_bounds__(256) void head_bwd_kernel(
+    const float* __restrict__ dZ, int o, const int* __restrict__ nrows, const float* __restrict__ H1,
+    const float* __restrict__ G1w, const float* __restrict__ G2w, const float* __restrict__ y,
+    const float* __restrict__ nrm, float* __restrict__ dP1, float* __restrict__ dp,
+    float* __restrict__ z, int z_n, const int* __restrict__ z_rows, int* __restrict__ zi,
+    int64_t zi_n) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* sA = lds;
+  float* sW2 = sA + kHeadRows * kHeadLd;
+  float* sW1 = sW2 + kHeadDim * kHeadLd;
+  float* red = sW1 + kHeadDim * kHeadLd;  // [4 waves][32 rows] partial dots
+  const int tid = threadIdx.x;
+  // z / zi zeroing (no consumer inside this kernel) comes last: the row chain
+  // is the critical path
+  auto zero_tail = [&]() {
+    const int64_t gt = (int64_t)blockIdx.x * 256 + tid, gs = (int64_t)gridDim.x * 256;
+    if (z) {
+      const int64_t zn4 = (int64_t)(*z_rows) * z_n / 4;
+      float4* z4 = reinterpret_cast<float4*>(z);
+      for (int64_t i = gt; i < zn4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (zi)
+      for (int64_t i = gt; i < zi_n; i += gs) zi[i] = 0;
+  };
+  const int64_t R = *nrows;
+  const int64_t r0 = (int64_t)blockIdx.x * kHeadRows;
+  if (r0 >= R) {
+    zero_tail();
+    return;
+  }
+  const int lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int n0 = 32 * w, col = n0 + l32;
+  // this lane's H1 (mask) and y values, fetched beside the staging loads
+  float hv[16], yv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    const bool ok = r0 + row < R && col < o;
+    hv[r] = ok ? H1[(r0 + row) * o + col] : 0.f;
+    yv[r] = ok ? y[(r0 + row) * o + col] : 0.f;
+  }
+  head_load_rows(sA, dZ, r0, R, o, tid);
+  head_load_weight(sW2, G2w, o, tid);
+  head_load_weight(sW1, G1w, o, tid);
+  __syncthreads();
+  f32x16 acc = head_mm<false>(sA, sW2, n0, l32, h);
+  __syncthreads();  // every wave is done reading dZ from sA
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    float v = 0.f;
+    if (r0 + row < R && col < o) {
+      v = acc[r] * lrelu_grad(hv[r]);
+      dP1[(r0 + row) * o + col] = v;
+    }
+    sA[row * kHeadLd + col] = v;
+  }
+  __syncthreads();
+  acc = head_mm<false>(sA, sW1, n0, l32, h);  // dY
+  // row dots y . dY: lane-partial over this wave's 32 columns, then 4 waves
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    float d = yv[r] * acc[r];
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) d += __shfl_xor(d, m, 64);
+    if (l32 == 0) red[w * kHeadRows + row] = d;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    if (r0 + row < R && col < o) {
+      const float dot = (red[row] + red[kHeadRows + row]) + (red[2 * kHeadRows + row] + red[3 * kHeadRows + row]);
+      const float inv = 1.f / nrm[r0 + row];
+      dp[(r0 + row) * o + col] = lrelu_grad(yv[r]) * (acc[r] - yv[r] * dot) * inv;
+    }
+  }
+  zero_tail();
+}
+
+constexpr size_t kHeadFwdLds = (size_t)(kHeadRows + 2 * kHeadDim) * kHeadLd * 4;
+constexpr size_t kHeadBwdLds = kHeadFwdLds + 4 * kHeadRows * 4;
+
+static int head_prepare() {
+  static int rc = [] {
+    if (hipFuncSetAttribute((const void*)head_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kHeadFwdLds) != hipSuccess ||
+        hipFuncSetAttribute((const void*)head_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kHeadBwdLds) != hipSuccess)
+      return (int)kErrHip;
+    return (int)kOk;
+  }();
+  if (rc != kOk) set_error("head: cannot raise the dynamic LDS limit");
+  return rc;
+}
+
+int head_supported(int64_t o) { return o > 0 && o <= kHeadDim && o % 4 == 0; }
+
+int launch_head_fwd(const float* y, int o, const int* nrows, int64_t max_rows, const float* G1w,
+                    const float* G1b, const float* G2w, float* H1, float* Z, hipStream_t st) {
+  PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
+  PS_TRY(head_prepare());
+  if (max_rows <= 0) return kOk;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                     kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_head_bwd(const float* dZ, int o, const int* nrows, int64_t max_rows, const float* H1,
+                    const float* G1w, const float* G2w, const float* y, const float* nrm,
+                    float* dP1, float* dp, float* z, int z_n, const int* z_rows, int* zi,
+                    int64_t zi_n, hipStream_t st) {
+  PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
+  PS_REQUIRE(!z || z_n % 4 == 0, kErrArg, "head: zeroed rows must be a multiple of 4 wide");
+  PS_TRY(head_prepare());
+  if (max_rows <= 0) return kOk;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                     kHeadBwdLds, st, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp, z, z_n, z_rows, zi,
+                     zi_n);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+}  // namespace ps

@@ -2,10 +2,10 @@
 
     python tools/timeline.py gpurun_out/prof/run_kernel_trace.csv [--step -3]
 
-Steps are delimited by the Adam kernel (the last launch of a step).  For the
-chosen step every dispatch is listed with its queue, start offset and duration
-(µs) relative to the end of the previous step's Adam, so gaps between
-dependent launches and the overlap of the side streams are visible.
+Steps are delimited by the frontier's first kernel.  For the chosen step
+every dispatch is listed with its queue, start offset and duration (µs)
+relative to the step's first kernel, so gaps between dependent launches and
+the overlap of the side streams are visible.
 """
 import argparse
 import csv
@@ -21,14 +21,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=-3)
-    ap.add_argument("--delim", default="adam_kernel")
+    ap.add_argument("--delim", default="bits_top_set_kernel",
+                    help="kernel that starts a step (the step ends before its next launch)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if a.delim in r["Kernel_Name"]]
-    k = ends[a.step]
-    lo = ends[a.step - 1] + 1
-    t0 = int(rows[lo - 1]["End_Timestamp"])
+    starts = [i for i, r in enumerate(rows) if a.delim in r["Kernel_Name"]]
+    lo = starts[a.step - 1]
+    k = starts[a.step] - 1
+    t0 = int(rows[lo]["Start_Timestamp"])
     busy = 0
     last_end = t0
     for r in rows[lo:k + 1]:
@@ -38,7 +39,7 @@ def main():
         grid = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
         print(f"q{r['Queue_Id']:>2} {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {grid:6d}  "
               f"{short(r['Kernel_Name'])}")
-    total = (int(rows[k]["End_Timestamp"]) - t0) / 1e3
+    total = (max(int(r["End_Timestamp"]) for r in rows[lo:k + 1]) - t0) / 1e3
     print(f"step span {total:.1f} us, some kernel running {busy / 1e3:.1f} us")
 
 
