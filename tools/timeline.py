@@ -1,6 +1,7 @@
 """Print one train step's kernel timeline from a rocprofv3 kernel trace.
 
     python tools/timeline.py gpurun_out/prof/run_kernel_trace.csv [--step -3]
+    python tools/timeline.py gpurun_out/prof/run_results.db [--step -3]
 
 Steps are delimited by the frontier's first kernel.  For the chosen step
 every dispatch is listed with its queue, start offset and duration (µs)
@@ -24,7 +25,15 @@ def main():
     ap.add_argument("--delim", default="bits_top_set_kernel",
                     help="kernel that starts a step (the step ends before its next launch)")
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
+    if a.trace.endswith(".db"):  # rocpd database (rocprofv3's default output on ROCm 7)
+        import sqlite3
+        c = sqlite3.connect(a.trace)
+        keys = ["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Queue_Id", "Grid_Size_X",
+                "Workgroup_Size_X"]
+        rows = [dict(zip(keys, r)) for r in
+                c.execute("select name, start, end, queue_id, grid_x, workgroup_x from kernels")]
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if a.delim in r["Kernel_Name"]]
     lo = starts[a.step - 1]
