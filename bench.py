@@ -51,9 +51,17 @@ def setup_dist(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
+        # PINSAGE_DIST_BACKEND=gloo rehearses the data-parallel path with ranks
+        # sharing one GPU (device = local rank mod the visible GPUs); the
+        # multi-GPU run uses nccl (= RCCL over xGMI)
+        backend = os.environ.get("PINSAGE_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            torch.distributed.init_process_group(backend)
     return rank, world
 
 

@@ -281,3 +281,23 @@ class RefTrainer:
         with torch.no_grad():
             nfl, var = triplet_monitors(self.feats, hs[0], torch.from_numpy(b))
         return float(loss), float(nfl), float(var), grads
+
+    def step_dp(self, batch, world):
+        """Data-parallel restatement of one step: ``world`` ranks each run the
+        reference train step's forwards and backward on their contiguous slice
+        of the global batch (so put_embeddings' repeated-id semantics hold per
+        rank), the gradients are averaged (the all-reduce), then one Adam step.
+        Returns the per-rank losses."""
+        b = np.asarray(batch)
+        B = b.shape[0] // world
+        self.opt.zero_grad()
+        losses = []
+        for r in range(world):
+            sl = b[r * B:(r + 1) * B]
+            hs = [model_forward(self.p, self.feats, sl[:, c], self.L, self.T, self.w, self.nb,
+                                self.out) for c in range(3)]
+            loss = max_margin_loss(*hs, self.margin)
+            (loss / world).backward()
+            losses.append(float(loss))
+        self.opt.step()
+        return losses
