@@ -67,6 +67,8 @@ _SIGS = {
                                        vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp]),
     "pinsage_weighted_agg": (ctypes.c_int, [vp, i64, vp, vp, i64, i64, vp, vp]),
+    "pinsage_knn_scratch_bytes": (i64, [i64, i64]),
+    "pinsage_knn_cosine": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, i64, f32, vp, i64, vp, vp, vp]),
     "pinsage_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(vp)]),
     "pinsage_engine_destroy": (None, [vp]),
     "pinsage_engine_workspace_bytes": (i64, [vp]),

@@ -34,6 +34,9 @@ int launch_set_finalize(unsigned long long*, const unsigned long long*, const un
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
+int64_t knn_scratch_bytes(int64_t, int64_t);
+int launch_knn_cosine(const float*, int64_t, int64_t, int64_t, const int64_t*, int64_t, int64_t,
+                      float, void*, int64_t, float*, int64_t*, int*, hipStream_t);
 
 // Fisher-Yates prefix of torch.randperm(n): first k entries, all n-1 draws consumed.
 // Only the <= 2k positions the first k swaps touch are stored (open addressing).
@@ -387,6 +390,17 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
     if (const char* e = getenv("PINSAGE_SK_MIN_UNITS")) p.sk_min_units = std::max(1, atoi(e));
   }
   return launch_gemm(p, (hipStream_t)stream);
+}
+
+int64_t pinsage_knn_scratch_bytes(int64_t n, int64_t batch_rows) {
+  return knn_scratch_bytes(n, batch_rows < 1 ? 1 : batch_rows);
+}
+
+int pinsage_knn_cosine(const float* emb, int64_t n, int64_t d, int64_t ld, const int64_t* queries,
+                       int64_t nq, int64_t k, float eps, void* scratch, int64_t scratch_bytes,
+                       float* out_w, int64_t* out_n, void* stream) {
+  return launch_knn_cosine(emb, n, d, ld, queries, nq, k, eps, scratch, scratch_bytes, out_w, out_n,
+                           nullptr, (hipStream_t)stream);
 }
 
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,

@@ -148,6 +148,22 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
                          int64_t n_rows, int64_t T, float* agg, void* stream);
 
+/* ------------------------------------------------------------------ cosine kNN
+ * knn_from_emb (baselines.py:91-103) over cosine_sim_ab (baselines.py:69-77), the
+ * evaluation consumer of the embeddings (eval.py:112-143 save_knn, k = 1000):
+ * for each query row q (int64 ids in [0, n), validated by the caller)
+ *   sim(q, j) = dot(emb[q], emb[j]) / (|emb[q]| |emb[j]| + eps), j in [0, n)
+ * out_w f32 [nq][k] / out_n int64 [nq][k]: the k largest, sorted descending
+ * (exact ties: lower index first).  The reference then drops column 0.
+ * emb: f32 device rows of stride ld (d % 4 == 0); 1 <= k <= min(n, 4096).
+ * scratch: device bytes >= pinsage_knn_scratch_bytes(n, rows) for some
+ * batch of rows >= 1 (the dot products of one batch of queries live there;
+ * larger scratch = fewer batches). */
+int64_t pinsage_knn_scratch_bytes(int64_t n, int64_t batch_rows);
+int pinsage_knn_cosine(const float* emb, int64_t n, int64_t d, int64_t ld, const int64_t* queries,
+                       int64_t nq, int64_t k, float eps, void* scratch, int64_t scratch_bytes,
+                       float* out_w, int64_t* out_n, void* stream);
+
 /* ------------------------------------------------------------------ train-step engine
  * PinSageModel.forward / PinSage.train_batch (pinsage_model.py:246-265,
  * pinsage_training.py:181-214) with device-resident sizes.  Parameters live in

@@ -155,6 +155,32 @@ def sample_neighborhood_topt(indptr, indices, n_all, sources, n_hops, alpha, T, 
     return topk(visit_prob(trace, sources, n_all), T)
 
 
+def ppr_knn(indptr, indices, n_all, nodeset, k, mt, n_hops=1000, alpha=0.85):
+    """PersPageRank.knn (baselines.py:114-151): the same walk / visit_prob as
+    sample_neighborhood (1000 hops, restart 0.85), then topk(k, 1)."""
+    return sample_neighborhood_topt(indptr, indices, n_all, nodeset, n_hops, alpha, k, mt)
+
+
+def cosine_sim_ab(a, b, eps=1e-16):
+    """baselines.py:69-77 (torch CPU fp32, the reference's ops)."""
+    dot = torch.mm(a, b.transpose(1, 0))
+    lengths = torch.mm(torch.norm(a, dim=1).unsqueeze(1), torch.norm(b, dim=1).unsqueeze(0)) + eps
+    return dot / lengths
+
+
+def knn_from_emb(emb, q, k):
+    """baselines.py:91-103: batches of 128 queries, topk(k+1) largest, first column dropped."""
+    emb = torch.as_tensor(emb)
+    q = torch.as_tensor(q)
+    ws, ns = [], []
+    for i in range(0, len(q), 128):
+        sim = cosine_sim_ab(emb[q[i:i + 128], :], emb)
+        w, n = sim.topk(k + 1, dim=1, largest=True)
+        ws.append(w[:, 1:])
+        ns.append(n[:, 1:])
+    return torch.cat(ws, 0).numpy(), torch.cat(ns, 0).numpy()
+
+
 def precompute_topt(indptr, indices, n_all, n_items, n_hops, alpha, T, mt, batch=256):
     """precompute_neighborhoods_topt (pinsage_model.py:109-132) without the file cache."""
     W = np.zeros((n_items, T), np.float64)

@@ -403,9 +403,60 @@ def fx_dataset(ref_psm, ref_pt, ref_sg):
          succ69=succ69, n_track_ids=len(track_ids), col_ids=np.array(col_ids))
 
 
+def _import_reference_baselines():
+    """baselines.py with its unavailable imports stubbed: networkx, fastnode2vec,
+    implicit and lib.gnns are only used by other baseline recommenders, never
+    by PersPageRank, cosine_sim_ab or knn_from_emb."""
+    for name in ("networkx", "networkx.algorithms", "networkx.algorithms.bipartite",
+                 "fastnode2vec", "implicit", "lib", "lib.gnns", "lib.gnns.GNNs_unsupervised"):
+        if name not in sys.modules:
+            sys.modules[name] = types.ModuleType(name)
+    sys.modules["networkx"].algorithms = sys.modules["networkx.algorithms"]
+    sys.modules["networkx.algorithms"].bipartite = sys.modules["networkx.algorithms.bipartite"]
+    sys.modules["lib.gnns.GNNs_unsupervised"].GNN = object
+    import baselines as ref_bl  # noqa: E402
+    return ref_bl
+
+
+def fx_baselines(ref_psm, ref_pt, ref_sg):
+    ref_bl = _import_reference_baselines()
+    # PersPageRank.knn (baselines.py:106-151): 1000-hop walks, topk over N_all;
+    # small: nth_element regime (k*64 > N_all), mid: partial_sort (k = 100) and
+    # nth_element with a mostly-zero tail (k = 1000)
+    for gname, n_src, seed, ks in (("small", 12, 31, (100,)), ("mid", 16, 32, (100, 1000))):
+        pg, ga = graph_arrays(gname)
+        g = stub_graph(pg)
+        rng = np.random.default_rng(seed)
+        nodeset = torch.from_numpy(rng.integers(0, pg.n_tracks, n_src).astype(np.int64))
+        m = ref_bl.PersPageRank()
+        m.train(g, None, None, None, None)
+        out = dict(ga, nodeset=nodeset.numpy(), seed=seed, n_hops=m.n_hops, alpha=m.alpha,
+                   ks=np.array(ks))
+        for k in ks:
+            torch.manual_seed(seed + k)
+            tk = m.knn(nodeset, k)
+            out[f"val_{k}"] = tk.values.numpy()
+            out[f"idx_{k}"] = tk.indices.numpy()
+            out[f"after_{k}"] = next_draws()
+        save(f"ppr_{gname}", **out)
+    # knn_from_emb (baselines.py:91-103) on cosine_sim_ab (:69-77): N(0,1) rows
+    # with exact duplicates (tied similarities) and an all-zero row
+    rng = np.random.default_rng(41)
+    emb = rng.standard_normal((2500, 64), dtype=np.float32)
+    emb[10:15] = emb[0:5]
+    emb[20] = 0.0
+    q = np.concatenate([np.arange(0, 25), rng.integers(0, 2500, 175)]).astype(np.int64)
+    out = dict(emb=emb, q=q)
+    for k in (50, 1000):
+        w, n = ref_bl.knn_from_emb(torch.from_numpy(emb), torch.from_numpy(q), k, None)
+        out[f"w_{k}"] = w.numpy()
+        out[f"n_{k}"] = n.numpy()
+    save("knn_emb", **out)
+
+
 FIXTURES = {"walk": fx_walk, "topk": fx_topk, "precompute": fx_precompute, "frontier": fx_frontier,
             "model": fx_model, "train": fx_train, "batch": fx_batch, "loss": fx_loss,
-            "dataset": fx_dataset}
+            "dataset": fx_dataset, "baselines": fx_baselines}
 
 
 def main(argv):

@@ -192,3 +192,25 @@ def test_train_step_matches():
                 assert _rel(g.numpy(), d[f"s0_g_{k}"]) < 1e-4, k
     for k in tr.order:
         assert _rel(tr.p[k].detach().numpy(), d[f"s1_p_{k}"]) < 1e-6, k
+
+
+@pytest.mark.parametrize("gname", ["small", "mid"])
+def test_ppr_knn_bit_exact(gname):
+    """PersPageRank.knn (baselines.py:106-151) fixtures from the reference."""
+    d = golden(f"ppr_{gname}")
+    indptr, indices, n_all = _csr(d)
+    for k in d["ks"]:
+        mt = orc.MT(int(d["seed"]) + int(k))
+        w, nb = orc.ppr_knn(indptr, indices, n_all, d["nodeset"], int(k), mt, int(d["n_hops"]),
+                            float(d["alpha"]))
+        assert (w == d[f"val_{k}"]).all() and (nb == d[f"idx_{k}"]).all(), k
+        assert _after_ok(mt, d[f"after_{k}"])
+
+
+def test_knn_from_emb_matches_reference():
+    """knn_from_emb / cosine_sim_ab (baselines.py:69-103) restated with the same
+    torch CPU ops: bitwise equal to the reference's output."""
+    d = golden("knn_emb")
+    for k in (50, 1000):
+        w, n = orc.knn_from_emb(d["emb"], d["q"], k)
+        assert np.array_equal(w, d[f"w_{k}"]) and np.array_equal(n, d[f"n_{k}"]), k
