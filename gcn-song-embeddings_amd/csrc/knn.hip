@@ -74,10 +74,13 @@ __global__ __launch_bounds__(kKnnBlock) void knn_select_kernel(
   const int64_t b = blockIdx.x;
   const float* row = dots + b * n;
   const float na = qn[b];
-  auto key_at = [&](int64_t j) __attribute__((always_inline)) {
+  auto key_of = [&](float dot, float nj) __attribute__((always_inline)) {
     // (|a| |b| + eps) rounded like torch's rank-1 mm then add: no contraction
-    return f2key(row[j] / __fadd_rn(__fmul_rn(na, norms[j]), eps));
+    return f2key(dot / __fadd_rn(__fmul_rn(na, nj), eps));
   };
+  auto key_at = [&](int64_t j) __attribute__((always_inline)) { return key_of(row[j], norms[j]); };
+  // rows of n % 4 == 0 floats start 16-byte aligned (the dot rows are n apart)
+  const bool vec = (n % 4) == 0;
 
   // ---- radix select of the k-th largest key: digits of 12, 12 and 8 bits
   uint32_t prefix = 0, need = (uint32_t)k;
@@ -89,10 +92,28 @@ __global__ __launch_bounds__(kKnnBlock) void knn_select_kernel(
     for (int i = tid; i < nb; i += kKnnBlock) hist[i] = 0;
     __syncthreads();
     const int hs = sh + widths[p];  // bits above this digit must equal the prefix
-    for (int64_t j = tid; j < n; j += kKnnBlock) {
-      const uint32_t key = key_at(j);
+    auto count = [&](uint32_t key) __attribute__((always_inline)) {
       if (hs >= 32 || (key >> hs) == prefix) atomicAdd(&hist[(key >> sh) & (nb - 1)], 1u);
+    };
+    // 4 x 16-byte loads of dots and norms in flight per thread (the row is
+    // streamed four times: memory-level parallelism, not LDS, bounds a pass)
+    const int64_t n16 = vec ? (n / 16) * 16 : 0;
+    for (int64_t j0 = (int64_t)tid * 16; j0 < n16; j0 += (int64_t)kKnnBlock * 16) {
+      float4 dv[4], nv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        dv[u] = *reinterpret_cast<const float4*>(row + j0 + 4 * u);
+        nv[u] = *reinterpret_cast<const float4*>(norms + j0 + 4 * u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        count(key_of(dv[u].x, nv[u].x));
+        count(key_of(dv[u].y, nv[u].y));
+        count(key_of(dv[u].z, nv[u].z));
+        count(key_of(dv[u].w, nv[u].w));
+      }
     }
+    for (int64_t j = n16 + tid; j < n; j += kKnnBlock) count(key_at(j));
     __syncthreads();
     if (wv == 0) {  // scan bins from the top: the bin holding the need-th largest
       const int per = nb / 64;
@@ -217,7 +238,9 @@ int launch_knn_cosine(const float* emb, int64_t n, int64_t d, int64_t ld, const 
   if (nq == 0) return kOk;
   // batch of query rows that fits the scratch
   int64_t qb = std::min<int64_t>(nq, 65535);
-  while (qb > 1 && knn_scratch_bytes(n, qb) > scratch_bytes) qb = (qb + 1) / 2;
+  qb = std::min<int64_t>(qb, std::max<int64_t>(1, (scratch_bytes - align_up(n * 4, 256) - 1024) /
+                                                     (n * 4 + 8)));
+  while (qb > 1 && knn_scratch_bytes(n, qb) > scratch_bytes) --qb;
   PS_REQUIRE(knn_scratch_bytes(n, qb) <= scratch_bytes, kErrWorkspace, "knn: scratch too small");
   char* s = (char*)scratch;
   float* norms = (float*)s;
