@@ -100,6 +100,7 @@ def _install_stubs():
 
 
 def _import_reference():
+    sys.dont_write_bytecode = True  # /root/reference is read-only: no __pycache__ there
     _install_stubs()
     if REF not in sys.path:
         sys.path.insert(0, REF)

@@ -153,6 +153,55 @@ def test_spotify_graph_matches_reference_loader():
         shutil.rmtree(tmp)
 
 
+def test_spotify_graph_binary_cache(monkeypatch):
+    """Second load reads pinsage_cache/ (no graph.json parse, no per-track
+    feature files) and returns the same graph, edge order and features; a
+    changed graph.json invalidates the cache."""
+    import json
+    import spotify_graph
+    import synthetic
+    pg = synthetic.make_playlist_graph(500, 80, 3000, seed=4)
+    ids = [f"t{i:05d}" for i in range(500)]
+    tmp = tempfile.mkdtemp()
+    try:
+        ds_dir = os.path.join(tmp, "ds")
+        synthetic.write_spotify_dataset(ds_dir, pg, track_ids=ids, seed=5)
+        fdir = os.path.join(ds_dir, "features")
+        os.makedirs(fdir)
+        raw = np.random.default_rng(1).standard_normal((500, 6)).astype(np.float32)
+        for i, tid in enumerate(ids):
+            torch.save(torch.from_numpy(raw[i].copy()), os.path.join(fdir, tid + ".pt"))
+        g1, t1, c1, f1 = spotify_graph.SpotifyGraph(ds_dir, fdir).to_dgl_graph()
+        assert os.path.isfile(os.path.join(ds_dir, "pinsage_cache", "graph.npz"))
+        assert os.path.isfile(os.path.join(ds_dir, "pinsage_cache", "features.npz"))
+        parsed = []
+        real_load = json.load
+
+        def spy(f, *a, **k):
+            parsed.append(os.path.basename(f.name))
+            return real_load(f, *a, **k)
+
+        monkeypatch.setattr(spotify_graph.json, "load", spy)
+        monkeypatch.setattr(spotify_graph.torch, "load", None)  # per-track features unused
+        g2, t2, c2, f2 = spotify_graph.SpotifyGraph(ds_dir, fdir).to_dgl_graph()
+        assert "graph.json" not in parsed
+        assert t2 == t1 and c2 == c1 and torch.equal(f1, f2)
+        assert np.array_equal(g1.indptr, g2.indptr) and np.array_equal(g1.indices, g2.indices)
+        for a, b in zip(g1.edges(), g2.edges()):
+            assert torch.equal(a, b)
+        # a changed graph.json (one edge dropped) is parsed again
+        with open(os.path.join(ds_dir, "graph.json")) as f:
+            gj = real_load(f)
+        gj["edges"] = gj["edges"][:-1]
+        with open(os.path.join(ds_dir, "graph.json"), "w") as f:
+            json.dump(gj, f)
+        parsed.clear()
+        g3, *_ = spotify_graph.SpotifyGraph(ds_dir, fdir).to_dgl_graph()
+        assert "graph.json" in parsed and g3.number_of_edges() == g1.number_of_edges() - 1
+    finally:
+        shutil.rmtree(tmp)
+
+
 def test_csr_graph_api():
     import graph
     src = [5, 0, 0, 3, 5, 1, 0]
