@@ -234,6 +234,9 @@ def main():
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             elapsed = float(t.item())
         ms_per_step = elapsed / args.steps * 1e3
+        if pt._HOST_T is not None:
+            log("[bench] host ms/step by section: " +
+                json.dumps({k: round(v / (args.steps + args.warmup) * 1e3, 4) for k, v in pt._HOST_T.items()}))
         value = 3 * cfg["batch"] * world * args.steps / elapsed
 
         # per-kernel timing pass (HIP events on the launch stream), separate from the timed

@@ -54,6 +54,7 @@ _SIGS = {
     "pinsage_batch_sampler_create": (ctypes.c_int, [vp, i64, i64, i64, vp]),
     "pinsage_batch_sampler_destroy": (None, [vp]),
     "pinsage_batch_sampler_next": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp, ctypes.c_int]),
+    "pinsage_batch_sampler_peek": (ctypes.c_int, [vp, vp, i64]),
     "pinsage_walk_mt_workspace": (i64, [i64, i64]),
     "pinsage_walk_mt": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, vp, vp, i64, vp, vp]),
     "pinsage_walk_philox": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, u64, u32, i64, vp, vp]),
@@ -67,6 +68,8 @@ _SIGS = {
                                        vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp]),
     "pinsage_weighted_agg": (ctypes.c_int, [vp, i64, vp, vp, i64, i64, vp, vp]),
+    "pinsage_step_stage": (ctypes.c_int, [vp, i64, i64, vp, i64, i64, vp, i64, vp, vp]),
+    "pinsage_step_publish": (ctypes.c_int, [vp, i64, vp, i64, vp, vp]),
     "pinsage_knn_scratch_bytes": (i64, [i64, i64]),
     "pinsage_knn_cosine": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, i64, f32, vp, i64, vp, vp, vp]),
     "pinsage_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(vp)]),
@@ -77,6 +80,8 @@ _SIGS = {
     "pinsage_engine_offsets": (ctypes.c_int, [vp, ctypes.POINTER(EngineOffsets)]),
     "pinsage_engine_set_tensors": (ctypes.c_int, [vp, vp, i64, vp, vp, i64, vp, vp, vp, vp]),
     "pinsage_engine_forward": (ctypes.c_int, [vp, vp, vp, i64, vp]),
+    "pinsage_engine_frontier": (ctypes.c_int, [vp, vp, vp, i64, vp]),
+    "pinsage_engine_forward_layers": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_gather_output": (ctypes.c_int, [vp, vp, i64, vp, vp]),
     "pinsage_engine_loss": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_int, vp]),
     "pinsage_engine_set_output_grad": (ctypes.c_int, [vp, vp, vp, i64, vp]),

@@ -347,7 +347,13 @@ static inline void with_sk(const Engine& E, void* ws, GemmParams& p) {
 }
 
 // ---------------------------------------------------------------- forward
-int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st) {
+// The forward in two phases.  engine_frontier depends only on the ids and the
+// neighbourhood table (never on parameters): the frontier sets of every layer
+// and each layer's index tables (layer_prep, which also zeroes that step's dY
+// scatter targets).  engine_layers runs the projections, aggregations and the
+// head.  A trainer with two workspaces runs step i+1's frontier beside step
+// i's backward (pinsage_training._FusedStep).
+int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st) {
   const EngineConfig& c = E.cfg;
   PS_REQUIRE(E.feats && E.nb && E.wn && E.params, kErrArg, "engine: pointers not set");
   PS_REQUIRE(n_pos > 0 && n_pos <= c.max_pos, kErrArg, "engine: n_pos out of range");
@@ -385,9 +391,7 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
                                  cnt(lo.S), st));
     }
   }
-  t_front.stop();
-
-  // layers, bottom-up
+  // index tables of every layer, bottom-up
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
     const SetBuf* prev = l > 0 ? &E.L[(size_t)l - 1].S : nullptr;
@@ -400,6 +404,18 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
                              pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank),
                              prev ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr, (int)c.out,
                              prev ? cnt(*prev) : nullptr, st));
+  }
+  return kOk;
+}
+
+int engine_layers(Engine& E, void* ws, hipStream_t st) {
+  const EngineConfig& c = E.cfg;
+  PS_REQUIRE(E.feats && E.nb && E.wn && E.params, kErrArg, "engine: pointers not set");
+  const int Lc = (int)c.n_layers, T = (int)c.T;
+  auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
+  LayerBuf& top = E.L[(size_t)Lc - 1];
+  for (int l = 0; l < Lc; ++l) {
+    LayerBuf& lb = E.L[(size_t)l];
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
     const int64_t ldh = l == 0 ? E.ld_f : c.out;
     // Q projection of the distinct neighbours: lrelu(h[u] Q^T + b)
@@ -479,6 +495,11 @@ int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, h
   g2.bias = nullptr;
   g2.act = false;
   return launch_gemm(g2, st);
+}
+
+int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st) {
+  PS_TRY(engine_frontier(E, ws, ids_dev, n_pos, st));
+  return engine_layers(E, ws, st);
 }
 
 // Weight gradient dst[M][N] = A^T [B || B2] over the device row count (split-K
@@ -998,6 +1019,15 @@ int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream) {
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                            void* stream) {
   return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
+}
+
+int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
+                            void* stream) {
+  return engine_frontier(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
+}
+
+int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream) {
+  return engine_layers(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
 }
 
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,

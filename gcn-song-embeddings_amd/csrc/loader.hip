@@ -1,6 +1,6 @@
 // Batch sampler runtime: reference-exact training batches (easy negatives,
-// pinsage_training.py:53-77, 89-97) with the NEXT batch drawn speculatively on
-// a native worker thread.
+// pinsage_training.py:53-77, 89-97) with the next batches drawn speculatively
+// on a native worker thread.
 //
 // The reference draws each batch from torch's global CPU generator; the O(P)
 // part is torch.randperm(P) consuming P-1 draws of which only the first B
@@ -12,6 +12,7 @@
 // reference's, and the randperm skip leaves the training loop's critical path.
 // Pure host code; no GPU calls.
 #include <condition_variable>
+#include <deque>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -41,14 +42,21 @@ struct BatchSampler {
   const int64_t* pos = nullptr;
   int64_t P = 0, n_items = 0, B = 0;
 
+  // The worker draws a chain of batches ahead: the batch starting at the state
+  // the last request handed back, then the one after it, ... up to kDepth
+  // finished draws (so a caller that peeks at the next batch right after a
+  // request finds it drawn during the previous step).  A request whose start
+  // state is not the chain's next one discards the chain.
+  static constexpr int kDepth = 2;
   std::mutex mu;
   std::condition_variable cv;
   std::thread worker;
   bool stop = false;
-  bool queued = false;   // spec holds a start state to draw
-  bool running = false;  // the worker is drawing spec
-  bool done = false;     // spec holds a finished draw
-  Draw spec;
+  bool running = false;          // the worker is drawing from run_start
+  uint64_t generation = 0;       // bumped when the chain is discarded
+  std::vector<uint8_t> chain;    // start state of the next draw (empty: none)
+  std::vector<uint8_t> run_start;
+  std::deque<Draw> ready;        // finished draws, in chain order
 
   void draw(Draw& d) const {
     MTState g;
@@ -76,34 +84,77 @@ struct BatchSampler {
   void loop() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      cv.wait(lk, [&] { return stop || queued; });
+      cv.wait(lk, [&] { return stop || (!chain.empty() && (int)ready.size() < kDepth); });
       if (stop) return;
-      queued = false;
+      Draw d;
+      d.start = chain;
+      run_start = chain;
       running = true;
+      const uint64_t gen = generation;
       lk.unlock();
-      draw(spec);  // spec is owned by the worker while running
+      draw(d);
       lk.lock();
       running = false;
-      done = true;
+      if (gen == generation) {
+        if (d.rc == kOk) {
+          chain = d.after;
+          ready.push_back(std::move(d));
+        } else {
+          chain.clear();  // a failing draw fails again synchronously, with its message
+        }
+      }
       cv.notify_all();
     }
   }
 
-  // Wait for the worker to go idle and take its finished draw (if any).
-  bool take(Draw& out) {
+  static bool same(const std::vector<uint8_t>& a, const uint8_t* b, int64_t nbytes) {
+    return (int64_t)a.size() == nbytes && std::memcmp(a.data(), b, (size_t)nbytes) == 0;
+  }
+
+  // The chain's draw for this start state, if it is the chain's next one
+  // (waiting for it if the worker is on it); otherwise discard the chain.
+  bool take(const uint8_t* state, int64_t nbytes, Draw& out) {
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return !running && !queued; });
-    if (!done) return false;
-    done = false;
-    std::swap(out, spec);
+    for (;;) {
+      if (!ready.empty()) {
+        if (same(ready.front().start, state, nbytes)) {
+          out = std::move(ready.front());
+          ready.pop_front();
+          cv.notify_all();
+          return true;
+        }
+        break;
+      }
+      // the worker is on it, or about to start it
+      if ((running && same(run_start, state, nbytes)) ||
+          (!running && same(chain, state, nbytes))) {
+        cv.wait(lk, [&] { return !ready.empty() || (!running && chain.empty()); });
+        if (ready.empty()) break;
+        continue;
+      }
+      break;
+    }
+    ready.clear();
+    chain.clear();
+    ++generation;
+    return false;
+  }
+
+  // The next draw of the chain (the batch the next request will get if it
+  // starts where the last one ended), waiting for the worker if needed.
+  bool peek(std::vector<int64_t>& batch) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return !ready.empty() || (!running && chain.empty()) || stop; });
+    if (ready.empty()) return false;
+    batch = ready.front().batch;
     return true;
   }
 
+  // Start the chain at this state unless it already runs past it (a hit).
   void submit(const std::vector<uint8_t>& start) {
     std::lock_guard<std::mutex> lk(mu);
-    spec.start = start;
-    done = false;
-    queued = true;
+    if (!chain.empty()) return;
+    chain = start;
     cv.notify_all();
   }
 
@@ -154,8 +205,7 @@ int pinsage_batch_sampler_next(pinsage_batch_sampler* h, const uint8_t* state, i
     return kErrArg;
   }
   Draw d;
-  const bool hit = s->take(d) && d.rc == kOk && (int64_t)d.start.size() == nbytes &&
-                   std::memcmp(d.start.data(), state, (size_t)nbytes) == 0;
+  const bool hit = s->take(state, nbytes, d);
   if (!hit) {
     d.start.assign(state, state + nbytes);
     s->draw(d);
@@ -170,6 +220,18 @@ int pinsage_batch_sampler_next(pinsage_batch_sampler* h, const uint8_t* state, i
   std::memcpy(state_after, d.after.data(), (size_t)nbytes);
   if (speculate) s->submit(d.after);
   return hit ? 1 : kOk;
+}
+
+int pinsage_batch_sampler_peek(pinsage_batch_sampler* h, int64_t* batch_out, int64_t max_rows) {
+  auto* s = reinterpret_cast<BatchSampler*>(h);
+  if (!s || !batch_out || max_rows < 0) {
+    set_error("batch_sampler_peek: bad argument");
+    return kErrArg;
+  }
+  std::vector<int64_t> b;
+  if (!s->peek(b) || (int64_t)b.size() > 3 * max_rows) return 0;
+  std::memcpy(batch_out, b.data(), b.size() * sizeof(int64_t));
+  return (int)(b.size() / 3);
 }
 
 }  // extern "C"

@@ -156,7 +156,21 @@ class _BatchPrefetcher:
         nat.check(min(rc, 0), "sample_batch")
         self.hits += rc
         torch.set_rng_state(after)
+        self.last = (B, torch.get_rng_state())
         return torch.from_numpy(out), torch.from_numpy(ns[:n_ns.value])
+
+    def peek(self, batch_size):
+        """The batch the next sample() of this size will return if nothing
+        touches torch's generator before it ([B, 3] int64 numpy), or None.
+        A hint only: whoever acts on it compares it with the batch it gets."""
+        if not self.speculate or self.h is None or self.key is None or self.key[4] != batch_size:
+            return None
+        last = getattr(self, "last", None)
+        if last is None or not torch.equal(last[1], torch.get_rng_state()):
+            return None
+        out = np.empty((last[0], 3), np.int64)
+        rows = nat.lib().pinsage_batch_sampler_peek(self.h, out.ctypes.data_as(nat.vp), last[0])
+        return out[:rows] if rows == last[0] else None
 
 
 _PREFETCH = _BatchPrefetcher()
@@ -197,9 +211,44 @@ def average_gradients(flat):
 
 
 # ----------------------------------------------------------------------------- trainer
+# PINSAGE_HOST_TIMING=1: accumulate host seconds per section of the train step
+_HOST_T = {} if os.environ.get("PINSAGE_HOST_TIMING") else None
+_HOST_LAST = [0.0]
+
+
+def _tick(name):
+    if _HOST_T is not None:
+        t = time.perf_counter()
+        if name != "pre":
+            _HOST_T[name] = _HOST_T.get(name, 0.0) + t - _HOST_LAST[0]
+        _HOST_LAST[0] = t
+
+
 class _FusedStep:
-    """Device state of the fused train step: flat param/grad/Adam buffers,
-    engine workspace, batch staging and scalar outputs."""
+    """Device state of the fused train step: flat param/grad/Adam buffers, two
+    engine workspaces (steps alternate between them), the host hand-off ring
+    and the scalar outputs.
+
+    One step is ONE graph launch and nothing else on the stream.  The host
+    writes the step's ids and Adam coefficients into a slot of a pinned ring;
+    the graph's first kernel stages them from the slot a device counter picks
+    (pinsage_step_stage), its last kernel publishes (loss, node_feat_loss,
+    variance) into the step's entry of a device ring and advances the counter
+    (pinsage_step_publish); train_batch returns views of that entry, valid for
+    ``OUT_RING`` steps.
+
+    The frontier of a step (pinsage_engine_frontier) reads only its ids and the
+    neighbourhood table.  So step i's graph also computes, on a branch beside
+    its backward, the frontier of the batch the native sampler has already
+    drawn for step i+1 (in the other workspace).  Step i+1 checks its batch is
+    that one (it is whenever nothing else used torch's generator in between);
+    otherwise it first launches its own frontier graph.  Results are the same
+    either way.  PINSAGE_FRONTIER_AHEAD: "start" (default: the branch forks at
+    the graph's start), "graph" (it forks before the backward) or "0" (no
+    look-ahead); measured at C2: 0.649 / 0.657 / 0.697 ms per step."""
+
+    HOST_RING = 8
+    OUT_RING = 1 << 16
 
     def __init__(self, trainer):
         self.tr = trainer
@@ -207,19 +256,23 @@ class _FusedStep:
         self.runner = model.runner()
         self.dev = self.runner.dev
         self.B = 0
+        self.wss = None
         self.ws = None
         self.m = self.v = None
         self.grads = None
-        self.host_batch = None
         self._tuned = False
         self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
-        # the device step (forward, loss, backward, Adam) is captured once into a
-        # hipGraph and replayed: one launch instead of ~90 per step
+        # the device step is captured into hipGraphs and replayed
         self.use_graph = os.environ.get("PINSAGE_HIPGRAPH", "1") != "0"
         # Adam fused into the gradient reductions (0: separate optimizer pass)
         self.fuse_adam = os.environ.get("PINSAGE_FUSED_ADAM", "1") != "0"
-        self.graph = None
+        mode = os.environ.get("PINSAGE_FRONTIER_AHEAD", "start")
+        self.ahead = mode != "0"
+        self.ahead_mode = mode
+        self.graphs = None
         self.graph_B = None
+        self.parity = 0
+        self.ahead_hits = 0
 
     def ensure(self, B):
         r = self.runner
@@ -230,25 +283,30 @@ class _FusedStep:
             self.m = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
             self.v = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
             self.adopt_optimizer_state()
-        if self.ws is None or r.engine is None or r.engine.cfg.max_pos < 3 * B:
+        if self.wss is None or r.engine is None or r.engine.cfg.max_pos < 3 * B:
             r.ensure_engine(3 * B)
-            self.ws = r.engine.new_workspace(self.dev)
+            self.wss = [r.engine.new_workspace(self.dev) for _ in range(2)]
             self.B = B
             off = r.engine.off
             mp = r.engine.cfg.max_pos
-            self.ids_view = r.engine.view(self.ws, int(off.ids), torch.int64, mp)
-            # ids and, behind them, this step's Adam coefficients travel in ONE
-            # host-to-device copy (pinsage_engine_adam)
-            self.stage_view = self.ws[int(off.ids):int(off.ids) + mp * 8 + 16]
-            self.scal = r.engine.view(self.ws, int(off.scalars), torch.float32, 4)
-            # two pinned staging buffers: the host fills one while the previous
-            # step's H2D copy from the other may still be queued
-            self.host_batch = [torch.empty(mp * 8 + 16, dtype=torch.uint8).pin_memory()
-                               for _ in range(2)]
-            self.host_ev = [None, None]
-            self.slot = 0
+            self.ids_view = [r.engine.view(w, int(off.ids), torch.int64, mp) for w in self.wss]
+            # ids, and behind them the step's Adam coefficients (pinsage_engine_adam)
+            self.stage_view = [w[int(off.ids):int(off.ids) + mp * 8 + 16] for w in self.wss]
+            self.scal = [r.engine.view(w, int(off.scalars), torch.float32, 4) for w in self.wss]
+            # pinned hand-off ring: slot = [ids of this step | ids of the next
+            # (look-ahead) | Adam coefficients]
+            self.slot_ids, self.slot_next, self.slot_coef = 0, mp * 8, 2 * mp * 8
+            self.slot_bytes = 2 * mp * 8 + 16
+            self.ring = torch.empty((self.HOST_RING, self.slot_bytes), dtype=torch.uint8).pin_memory()
+            self.ring_ev = [None] * self.HOST_RING
+            self.ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)
+            self.out_ring = torch.zeros((self.OUT_RING, 4), dtype=torch.float32, device=self.dev)
+            self.nstep = 0
+            self.pending = [None, None]  # ids whose frontier already sits in workspace q
+            self.parity = 0
+            self.ws = self.wss[0]
             self._tuned = False
-            self.graph = None
+            self.graphs = None
 
     def adopt_optimizer_state(self):
         """Use the optimizer's Adam state (if any, e.g. after load_state_dict) as
@@ -284,38 +342,57 @@ class _FusedStep:
         lr = float(g["lr"])
         return lr / (1 - b1 ** step), (1 - b2 ** step) ** 0.5
 
-    def _stage(self, batch, B):
-        """Copy the [B, 3] batch, and the Adam coefficients of the step about to
-        run, into the engine's device id buffer (one host-to-device copy)."""
-        k = self.slot
-        self.slot ^= 1
-        if self.host_ev[k] is not None:
-            self.host_ev[k].synchronize()
-        n = 3 * B * 8
-        hb = self.host_batch[k]
-        ids = hb[:n].view(torch.int64)
-        ids.copy_(batch.reshape(-1).to(torch.int64))
+    # ---- host side of the hand-off ring
+    def _slot_write_ids(self, k, off, batch, B):
+        ids = self.ring[k, off:off + 3 * B * 8].view(torch.int64)
+        ids.copy_(torch.as_tensor(batch).reshape(-1).to(torch.int64))
         n_items = int(self.runner.engine.cfg.n_items)
         if int(ids.min()) < 0 or int(ids.max()) >= n_items:
             raise IndexError(f"batch ids out of range for {n_items} items")
-        hb[n:n + 8].view(torch.float32).copy_(torch.tensor(self._adam_coef(self.host_step + 1),
-                                                           dtype=torch.float32))
-        self.stage_view[:n + 8].copy_(hb[:n + 8], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.host_ev[k] = ev
 
-    def _device_step(self, B, with_adam):
+    def _slot_write_coef(self, k):
+        self.ring[k, self.slot_coef:self.slot_coef + 8].view(torch.float32).copy_(
+            torch.tensor(self._adam_coef(self.host_step + 1), dtype=torch.float32))
+
+    # ---- device phases
+    def _stage(self, B, src_off, q_ids, p_coef):
+        """Copy 3B ids at src_off of the counter's slot into workspace q_ids (if
+        not None) and the coefficients into workspace p_coef (if not None)."""
+        dst = self.ids_view[q_ids] if q_ids is not None else None
+        coef = (ctypes.c_void_p(self.stage_view[p_coef].data_ptr() + 3 * B * 8)
+                if p_coef is not None else None)
+        nat.check(nat.lib().pinsage_step_stage(
+            nat.ptr(self.ring), self.slot_bytes, self.HOST_RING, nat.ptr(self.ctr), src_off,
+            3 * B * 8 if dst is not None else 0, nat.ptr(dst), self.slot_coef, coef,
+            nat.stream_ptr()), "step_stage")
+
+    def _publish(self, p):
+        nat.check(nat.lib().pinsage_step_publish(nat.ptr(self.scal[p]), 4, nat.ptr(self.out_ring),
+                                                 self.OUT_RING, nat.ptr(self.ctr), nat.stream_ptr()),
+                  "step_publish")
+
+    def _frontier(self, B, q):
+        e = self.runner.engine
+        nat.check(nat.lib().pinsage_engine_frontier(e.h, nat.ptr(self.wss[q]), nat.ptr(self.ids_view[q]),
+                                                    3 * B, nat.stream_ptr()), "frontier")
+
+    def _main(self, B, p, with_adam, before_backward=None):
+        """Layers, head, loss, backward (and Adam) of workspace p's frontier;
+        before_backward() is called (to fork work) between loss and backward."""
         tr = self.tr
         e = self.runner.engine
         st = nat.stream_ptr()
         L = nat.lib()
-        nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
-                  "forward")
-        nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
-        self._backward(with_adam)
+        nat.check(L.pinsage_engine_forward_layers(e.h, nat.ptr(self.wss[p]), st), "forward_layers")
+        nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.wss[p]), B, float(tr.margin), 1, st), "loss")
+        if not self._tuned:  # once: frontier sizes of a real batch pick the GEMM tiles
+            e.tune(self.wss[p])
+            self._tuned = True
+        if before_backward is not None:
+            before_backward()
+        self._backward(p, with_adam)
 
-    def _backward(self, with_adam):
+    def _backward(self, p, with_adam):
         """Backward; with_adam: Adam fused into the gradient reductions
         (pinsage_engine_backward_adam, bitwise equal to backward + adam)."""
         e = self.runner.engine
@@ -323,37 +400,87 @@ class _FusedStep:
             g = self.tr.optimizer.param_groups[0]
             b1, b2 = g["betas"]
             nat.check(nat.lib().pinsage_engine_backward_adam(
-                e.h, nat.ptr(self.ws), self._coef_ptr(), float(b1), float(b2), float(g["eps"]),
+                e.h, nat.ptr(self.wss[p]), self._coef_ptr(p), float(b1), float(b2), float(g["eps"]),
                 nat.stream_ptr()), "backward_adam")
             return
-        nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(self.ws), nat.stream_ptr()),
+        nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(self.wss[p]), nat.stream_ptr()),
                   "backward")
         if with_adam:
-            self._adam()
+            self._adam(p)
 
-    def _coef_ptr(self):
-        return ctypes.c_void_p(self.stage_view.data_ptr() + 3 * self.B_cur * 8)
+    def _coef_ptr(self, p):
+        return ctypes.c_void_p(self.stage_view[p].data_ptr() + 3 * self.B_cur * 8)
 
-    def _adam(self):
+    def _adam(self, p):
         g = self.tr.optimizer.param_groups[0]
         b1, b2 = g["betas"]
-        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, self._coef_ptr(), float(b1),
+        nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, self._coef_ptr(p), float(b1),
                                                 float(b2), float(g["eps"]), nat.stream_ptr()), "adam")
 
     def _signature(self, feats, table):
         return (self.runner.flat.data_ptr(), self.grads.data_ptr(), self.m.data_ptr(),
                 self.v.data_ptr(), feats.data_ptr(), table.nb32.data_ptr(), table.wn.data_ptr(),
-                self.ws.data_ptr(), id(self.runner.engine))
+                self.wss[0].data_ptr(), self.wss[1].data_ptr(), id(self.runner.engine))
 
     def _capture(self, B, sig):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._device_step(B, with_adam=not self.dist)
-        self.graph = g
+        """Per workspace p: the frontier graph (stage this step's ids, frontier),
+        the step graph (stage coefficients, layers ... Adam, publish), and the
+        step graph whose branch stages the predicted next ids into workspace
+        1-p and computes their frontier there."""
+        adam = not self.dist
+        side = torch.cuda.Stream()
+        graphs = []
+        for p in (0, 1):
+            gf, gm, ga = (torch.cuda.CUDAGraph() for _ in range(3))
+            with torch.cuda.graph(gf):
+                self._stage(B, self.slot_ids, p, None)
+                self._frontier(B, p)
+            with torch.cuda.graph(gm):
+                self._stage(B, 0, None, p)
+                self._main(B, p, with_adam=adam)
+                self._publish(p)
+            with torch.cuda.graph(ga):
+                cur = torch.cuda.current_stream()
+
+                def fork_next_frontier():
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        self._frontier(B, 1 - p)
+
+                # the next step's ids go to workspace 1-p, whose last user
+                # (the previous step) is done: graph launches are stream-ordered
+                self._stage(B, self.slot_next, 1 - p, p)
+                if self.ahead_mode == "start":
+                    fork_next_frontier()
+                    self._main(B, p, with_adam=adam)
+                else:  # beside the backward: a latency-bound chain with CUs to spare
+                    self._main(B, p, with_adam=adam, before_backward=fork_next_frontier)
+                cur.wait_stream(side)
+                self._publish(p)
+            graphs.append((gf, gm, ga))
+        self.graphs = graphs
         self.graph_B = B
         self.graph_sig = sig
 
+    def _predicted(self, B):
+        """This rank's slice of the batch the sampler drew ahead, or None."""
+        if not self.ahead:
+            return None
+        rank, world = self.tr._dp()
+        nxt = _PREFETCH.peek(self.tr.batch_size * world)
+        if nxt is None or nxt.shape[0] != B * world:
+            return None
+        return nxt[rank * B:(rank + 1) * B]
+
     def __call__(self, batch):
+        if _HOST_T is not None:
+            t0 = time.perf_counter()
+            out = self._call(batch)
+            _HOST_T["call"] = _HOST_T.get("call", 0.0) + time.perf_counter() - t0
+            return out
+        return self._call(batch)
+
+    def _call(self, batch):
         tr = self.tr
         batch = torch.as_tensor(batch)
         B = int(batch.shape[0])
@@ -363,30 +490,55 @@ class _FusedStep:
         table = r.table(tr.nbhds)
         r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)
         self.B_cur = B
-        self._stage(batch, B)
+        p = self.parity
+        self.parity ^= 1
+        self.ws = self.wss[p]
         sig = self._signature(feats, table)
-        if self.graph is not None and (self.graph_B != B or self.graph_sig != sig or not self.use_graph):
-            self.graph = None  # buffers moved: the captured pointers are stale
-        if self.graph is not None:
-            self.graph.replay()
+        if self.graphs is not None and (self.graph_B != B or self.graph_sig != sig or not self.use_graph):
+            self.graphs = None  # buffers moved: the captured pointers are stale
+        _tick("pre")
+        k = self.nstep % self.HOST_RING
+        if self.ring_ev[k] is not None:  # the step that used this slot is done
+            self.ring_ev[k].synchronize()
+        self._slot_write_coef(k)
+        _tick("slot_wait")
+        if self.graphs is not None:
+            gf, gm, ga = self.graphs[p]
+            pend = self.pending[p]
+            if pend is not None and np.array_equal(pend, batch.reshape(B, 3).cpu().numpy()):
+                self.ahead_hits += 1
+            else:
+                self._slot_write_ids(k, self.slot_ids, batch, B)
+                gf.replay()
+            self.pending[p] = None
+            nxt = self._predicted(B)
+            _tick("peek")
+            if nxt is not None:
+                self._slot_write_ids(k, self.slot_next, nxt, B)
+                ga.replay()
+            else:
+                gm.replay()
+            self.pending[1 - p] = nxt
+            _tick("replay")
         else:
-            e = r.engine
-            st = nat.stream_ptr()
-            L = nat.lib()
-            nat.check(L.pinsage_engine_forward(e.h, nat.ptr(self.ws), nat.ptr(self.ids_view), 3 * B, st),
-                      "forward")
-            nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.ws), B, float(tr.margin), 1, st), "loss")
-            if not self._tuned:  # once: frontier sizes of a real batch pick the GEMM tiles
-                e.tune(self.ws)
-                self._tuned = True
-            self._backward(with_adam=not self.dist)
-            if self.use_graph and self._tuned and self.graph is None:
+            self._slot_write_ids(k, self.slot_ids, batch, B)
+            self._stage(B, self.slot_ids, p, p)
+            self._frontier(B, p)
+            self._main(B, p, with_adam=not self.dist)
+            self._publish(p)
+            self.pending = [None, None]
+            if self.use_graph and self._tuned:
                 self._capture(B, sig)
         if self.dist:
             average_gradients(self.grads)
-            self._adam()
+            self._adam(p)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.ring_ev[k] = ev
+        out = self.out_ring[self.nstep % self.OUT_RING]
+        self.nstep += 1
         self.host_step += 1
-        out = self.scal.clone()
+        _tick("tail")
         return out[0], out[1], out[3]
 
 

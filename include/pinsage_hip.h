@@ -74,6 +74,14 @@ void pinsage_batch_sampler_destroy(pinsage_batch_sampler* s);
 int pinsage_batch_sampler_next(pinsage_batch_sampler* s, const uint8_t* state, int64_t nbytes,
                                int64_t* batch_out, int64_t* nodeset_out, int64_t* n_nodeset,
                                uint8_t* state_after, int speculate);
+/* The batch the worker drew speculatively for the NEXT request (from the
+ * generator state the last pinsage_batch_sampler_next handed back), without
+ * consuming it: waits for the worker, copies rows x 3 int64 ids into
+ * batch_out and returns rows (0 if there is no finished draw or it exceeds
+ * max_rows).  The next request still verifies its start state; a caller that
+ * acts on a peeked batch (the trainer computes that batch's frontier ahead)
+ * must compare it with the batch it is finally given. */
+int pinsage_batch_sampler_peek(pinsage_batch_sampler* h, int64_t* batch_out, int64_t max_rows);
 
 /* ------------------------------------------------------------------ sampler (device)
  * do_random_walks (pinsage_model.py:32-53).  CSR: indptr int64 [n_all+1],
@@ -148,6 +156,20 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
                          int64_t n_rows, int64_t T, float* agg, void* stream);
 
+/* ------------------------------------------------------------------ step hand-off
+ * (PinSage.train_batch, pinsage_training.py:181-214, as ONE graph launch per step)
+ * pinsage_step_stage: copy nbytes at src_off of slot (*ctr % R) of a pinned host
+ * ring (slot_bytes each) to dst, and 8 bytes at coef_off to coef_dst (if set);
+ * offsets and sizes multiples of 8.  pinsage_step_publish: ring_out[*ctr % R2]
+ * [0..n) = scal[0..n) (n <= 64), then *ctr += 1.  Both read the counter on the
+ * device, so a captured step graph stages and publishes the step the host
+ * wrote, without copies between launches. */
+int pinsage_step_stage(const void* ring, int64_t slot_bytes, int64_t R, const int64_t* ctr,
+                       int64_t src_off, int64_t nbytes, void* dst, int64_t coef_off, void* coef_dst,
+                       void* stream);
+int pinsage_step_publish(const float* scal, int64_t n, float* ring_out, int64_t R2, int64_t* ctr,
+                         void* stream);
+
 /* ------------------------------------------------------------------ cosine kNN
  * knn_from_emb (baselines.py:91-103) over cosine_sim_ab (baselines.py:69-77), the
  * evaluation consumer of the embeddings (eval.py:112-143 save_knn, k = 1000):
@@ -208,6 +230,15 @@ int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream);
  * IndexError like the reference's features[nodeset]). */
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                            void* stream);
+/* The forward's two phases (pinsage_engine_forward = frontier, then layers).
+ * The frontier phase (relevant_nodes_per_layer_precomp, pinsage_model.py:156-168,
+ * plus every layer's index tables) reads only the ids and the neighbourhood
+ * table -- no parameters -- so a trainer with two workspaces runs the next
+ * step's frontier on a side stream while this step's layers and backward run
+ * in the other workspace. */
+int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
+                            void* stream);
+int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream);
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
                                  void* stream);
 /* max_margin_loss + monitors on the last forward of a [B][3] batch; writes dZ */

@@ -337,3 +337,51 @@ def test_fused_adam_matches_backward_plus_adam():
             assert ((p0[0] - p1[0]).norm() / p0[0].norm()).item() < 1e-5
         finally:
             os.chdir(cwd)
+
+
+def test_frontier_ahead_matches_serial_step():
+    """The step graph that also computes the next batch's frontier (from the
+    sampler's speculative draw) trains exactly like the serial step: same
+    losses and parameters (within rounding: the CSR fill order uses atomics),
+    with look-ahead hits; a batch that is not the predicted one (here a
+    caller-made batch) falls back to its own frontier first."""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(6000, 1500, 40000, seed=31)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(6000, 128, seed=32))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 30000, seed=33))
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp,
+                                        nbhds_path=os.path.join(tmp, "nb.pt"))
+            pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
+
+            def run(ahead):
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
+                tr.batch_size = 256
+                tr._fused = f = pt._FusedStep(tr)
+                f.ahead = ahead
+                torch.manual_seed(6)
+                losses = []
+                for s in range(6):
+                    batch, _ = tr.next_batch()
+                    if s == 4:  # not what the sampler predicted
+                        batch = batch.flip(0).contiguous()
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                return losses, f.runner.flat.detach().clone(), f.ahead_hits
+
+            l0, p0, h0 = run(False)
+            l1, p1, h1 = run(True)
+            assert h0 == 0 and h1 >= 2
+            for a, b in zip(l0, l1):
+                assert abs(a - b) <= 1e-4 * abs(a) + 1e-7
+            assert ((p0 - p1).abs() <= 2 * 1e-4 * 6 + 1e-7).all()
+            assert ((p0 - p1).norm() / p0.norm()).item() < 1e-4
+        finally:
+            os.chdir(cwd)

@@ -281,6 +281,31 @@ def test_batch_sampler_speculation_is_exact():
         assert torch.equal(n2, b2.flatten().unique())
 
 
+def test_batch_sampler_peek_is_the_next_batch():
+    """peek() (the trainer computes that batch's frontier ahead) returns the
+    batch the next sample() draws, and None once another generator user has
+    moved torch's state; the chained speculation keeps hitting."""
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(3000, 500, 20000, seed=9)
+    pos = torch.from_numpy(synthetic.make_positives(pg, 8000, seed=3))
+    all_ids = torch.arange(3000)
+    pt._PREFETCH.close()
+    pt._PREFETCH.speculate = True
+    pt._PREFETCH.hits = 0
+    torch.manual_seed(3)
+    pt.sample_batch(all_ids, pos, 64, None, hard_negatives=False)
+    for _ in range(6):
+        nxt = pt._PREFETCH.peek(64)
+        b, _ = pt.sample_batch(all_ids, pos, 64, None, hard_negatives=False)
+        assert nxt is not None and np.array_equal(nxt, b.numpy())
+    assert pt._PREFETCH.hits >= 5
+    torch.randint(10, ())
+    assert pt._PREFETCH.peek(64) is None
+    assert pt._PREFETCH.peek(32) is None
+    pt._PREFETCH.close()
+
+
 @pytest.mark.parametrize("n", [(1 << 21) + 7, 3_000_017, 12_345_678])
 def test_mt_long_skip_jumps_exactly(n):
     """Skips of >= 2^21 draws use the GF(2) jump-ahead (mt_jump.h); the state
