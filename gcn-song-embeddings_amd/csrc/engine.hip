@@ -108,12 +108,11 @@ struct Engine {
   EngineConfig cfg{};
   bool timing = false;
   // Which backward work runs beside the caller's stream (PINSAGE_BWD_STREAMS):
-  // 0 the CSR builds and the weight gradients, 1 nothing, 2 the CSR builds
-  // (default), 3 the weight gradients.  Measured at C2 (bench.py): 2.27M /
-  // 2.32M / 2.33M / 2.12M target nodes/s -- weight gradients beside the chain
-  // take CUs from it and add cross-queue waits; the CSR builds (independent
-  // of the head backward) are worth their one wait per layer.
-  int stream_mode = getenv("PINSAGE_BWD_STREAMS") ? atoi(getenv("PINSAGE_BWD_STREAMS")) : 2;
+  // 0 the CSR builds and the weight gradients (default), 1 nothing, 2 the CSR
+  // builds, 3 the weight gradients, 4 the CSR builds and layer 0's W gradient +
+  // the optimizer pass.  Measured at C2 in the one-launch step graph (bench.py):
+  // 0.605-0.615 / - / 0.645-0.648 / 0.611-0.640 / 0.620-0.626 ms per step.
+  int stream_mode = getenv("PINSAGE_BWD_STREAMS") ? atoi(getenv("PINSAGE_BWD_STREAMS")) : 0;
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   std::vector<TimingSite> sites;
@@ -612,7 +611,11 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   PS_TRY(ensure_streams(E));
   hipStream_t s_csr = E.side[0], s_wg = E.side[1];
   if (E.stream_mode == 1 || E.stream_mode == 3) s_csr = st;
-  if (E.stream_mode == 1 || E.stream_mode == 2) s_wg = st;
+  if (E.stream_mode == 1 || E.stream_mode == 2 || E.stream_mode == 4) s_wg = st;
+  // mode 4: layer 0's W gradient and the optimizer pass of every parameter but
+  // Q0 go beside the chain's tail (the transposed aggregation and dQ0, which
+  // do not need them); the other weight gradients stay on the chain
+  hipStream_t s_wg0 = E.stream_mode == 4 ? E.side[1] : s_wg;
   // the transposes of the neighbour slots depend only on the forward: build
   // them beside the head backward; events mark each layer's CSR done
   PS_TRY(dep(E, st, s_csr));
@@ -716,7 +719,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     if (l < Lc - 1)
       PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
                                    o, cnt(lb.S), lb.S.cap, dp, nullptr, o, nullptr, nullptr, 0, st));
-    PS_TRY(dep(E, st, s_wg));
+    hipStream_t s_w = l == 0 ? s_wg0 : s_wg;
+    PS_TRY(dep(E, st, s_w));
     WGrad w_wgrad;
     {
       WGrad w;  // dW = dp^T [h_self || agg], dWb = colsum(dp)
@@ -770,15 +774,15 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       PS_TRY(launch_gemm(p, st));
     }
     {
-      Timed tw(E, lname("bwd.w_wgrad", l), s_wg);
-      PS_TRY(weight_grad(E, ws, w_wgrad, s_wg));
+      Timed tw(E, lname("bwd.w_wgrad", l), s_w);
+      PS_TRY(weight_grad(E, ws, w_wgrad, s_w));
     }
-    if (adam && l == 0) {  // every gradient but Q0's exists on s_wg; W0 was read last
-      PS_TRY(dep(E, st, s_wg));
-      Timed ta(E, "adam", s_wg);
+    if (adam && l == 0) {  // every gradient but Q0's exists on s_w; W0 was read last
+      PS_TRY(dep(E, st, s_w));
+      Timed ta(E, "adam", s_w);
       PS_TRY(launch_adam(E.params + l0.pWw, E.grads + l0.pWw, E.adam_m + l0.pWw, E.adam_v + l0.pWw,
                          E.n_params - l0.pWw, adam->coef, adam->beta1, adam->beta2, adam->eps,
-                         s_wg));
+                         s_w));
     }
     PS_CHECK_HIP(hipStreamWaitEvent(st, csr_done[(size_t)l], 0));
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
@@ -836,6 +840,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   // every gradient is written once the side streams drain into st
   PS_TRY(dep(E, s_csr, st));
   PS_TRY(dep(E, s_wg, st));
+  if (s_wg0 != s_wg) PS_TRY(dep(E, s_wg0, st));
   return kOk;
 }
 
