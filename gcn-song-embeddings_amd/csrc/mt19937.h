@@ -112,15 +112,18 @@ struct MTState {
   void skip(int64_t n) {
     if (n >= kJumpMin && mtjump::available()) {
       // the array s holds outputs x_b .. x_{b+623}, of which c are consumed;
-      // jump the window to start at the last skipped output, then resume at
-      // its second word (next = 1, the first is consumed)
+      // jump the window to start at a skipped output x_{b+J}, J <= c + n - 1,
+      // then resume at its second word (next = 1, the first is consumed).  J is
+      // rounded down to a multiple of 1024 so that x^J mod phi is a cached
+      // power (no per-call shift); the < 1024 draws left are twisted through.
       const int64_t c = 625 - left;
+      const int64_t J = (c + n - 1) & ~int64_t(1023);
       uint32_t out[N];
-      mtjump::jump_window(s, c + n - 1, out);
+      mtjump::jump_window(s, J, out);
       std::memcpy(s, out, sizeof(s));
       next = 1;
       left = N;
-      return;
+      n -= J + 1 - c;  // draws the jump covered
     }
     while (n > 0) {
       int64_t a = avail();

@@ -199,6 +199,42 @@ inline Poly power(int64_t J) {
   return shift_mod(base, J - E, T.phi);
 }
 
+// Horner evaluation of p(T) over 8-bit digits (most significant first): the
+// window lives in a linear buffer (a T step appends one word; the live window
+// is the last kN words), so every digit's XOR of a 624-word table entry is one
+// contiguous, vectorisable loop; the buffer slides back every kSlide digits.
+constexpr int kHornerBuf = kN + 8 * 64;
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+__attribute__((target_clones("avx2", "default")))
+#endif
+inline void horner(const uint64_t* p, int deg, const uint32_t* V, uint32_t* b, uint32_t* out) {
+  constexpr int Q = 8, kBuf = kHornerBuf;
+  for (int i = 0; i < kBuf; ++i) b[i] = 0u;
+  int o = 0;  // live window: b[o .. o + kN)
+  const int nd = deg / Q + 1;
+  for (int d = nd - 1; d >= 0; --d) {
+    if (o + kN + Q > kBuf) {
+      std::memmove(b, b + o, sizeof(uint32_t) * kN);
+      o = 0;
+    }
+    int mask = 0;
+    for (int j = Q - 1; j >= 0; --j) {
+      // one T step: x[o + kN] = x[o + kM] ^ f(x[o], x[o + 1]); window moves by one
+      const uint32_t y = (b[o] & 0x80000000u) | (b[o + 1] & 0x7fffffffu);
+      b[o + kN] = b[o + kM] ^ (y >> 1) ^ ((b[o + 1] & 1u) ? 0x9908b0dfu : 0u);
+      ++o;
+      const int64_t i = (int64_t)d * Q + j;
+      if (i < kDeg && ((p[i >> 6] >> (i & 63)) & 1u)) mask |= 1 << j;
+    }
+    if (mask) {
+      uint32_t* __restrict__ w = b + o;
+      const uint32_t* __restrict__ v = V + (size_t)mask * kN;
+      for (int i = 0; i < kN; ++i) w[i] ^= v[i];
+    }
+  }
+  std::memcpy(out, b + o, sizeof(uint32_t) * kN);
+}
+
 // window(t + J) from window(t) (logical order, word 0 first).  Horner over
 // 8-coefficient digits: r <- T^8 r ^ V[digit], V[mask] = sum of T^j window(t)
 // over the set bits j of mask (256 precomputed windows), so ~2.5k window XORs
@@ -227,21 +263,13 @@ inline void jump_window(const uint32_t* win, int64_t J, uint32_t* out) {
   }
   int deg = kDeg - 1;
   while (deg >= 0 && !bit(p, deg)) --deg;
-  Win r;
-  std::memset(r.w, 0, sizeof(r.w));
-  if (deg >= 0) {
-    const int nd = deg / Q + 1;  // digits, most significant first
-    for (int d = nd - 1; d >= 0; --d) {
-      int mask = 0;
-      for (int j = Q - 1; j >= 0; --j) {
-        step(r);
-        const int64_t i = (int64_t)d * Q + j;
-        if (i < kDeg && bit(p, i)) mask |= 1 << j;
-      }
-      if (mask) xor_in(r, &V[(size_t)mask * kN]);
-    }
+  if (deg < 0) {
+    std::memset(out, 0, sizeof(uint32_t) * kN);
+    return;
   }
-  for (int j = 0; j < kN; ++j) out[j] = r.w[(r.o + j) % kN];
+  static thread_local std::vector<uint32_t> buf;
+  buf.resize((size_t)kHornerBuf);
+  horner(p.data(), deg, V.data(), buf.data(), out);
 }
 
 inline bool available() { return !tables().phi.empty(); }
