@@ -158,8 +158,36 @@ struct SkPlan {
   }
 };
 
-// WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK.
-template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK>
+// s_waitcnt vmcnt(younger * NG): retire a stage while `younger` later stages
+// (NG DMAs per wave each) stay in flight (the immediate must be a constant)
+template <int NG, int MAXY>
+__device__ __forceinline__ void wait_stage(int younger) {
+  static_assert(MAXY * NG <= 63, "vmcnt immediate");
+  if constexpr (MAXY >= 4) {
+    if (younger >= 4) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NG) : "memory");
+      return;
+    }
+  }
+  if constexpr (MAXY >= 3) {
+    if (younger == 3) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NG) : "memory");
+      return;
+    }
+  }
+  if constexpr (MAXY >= 2) {
+    if (younger == 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+      return;
+    }
+  }
+  if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK; at most
+// NSMAX stage buffers in the ring.
+template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
@@ -171,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   // the k-row windows exist only for MN-major (possibly gathered) operands
   constexpr int IDXF = (GA ? kIdxWin : 0) + (GB ? kIdxWin : 0);
   constexpr int NSA = (kLdsBudget / 4 - IDXF) / SZS;
-  constexpr int NS = NSA > 4 ? 4 : NSA;
+  constexpr int NS = NSA > NSMAX ? NSMAX : NSA;
   static_assert(NS >= 3, "stage buffers do not fit");
   __shared__ __attribute__((aligned(16))) float smem[NS * SZS + IDXF];
   int* const sidxA = reinterpret_cast<int*>(smem + NS * SZS);
@@ -295,14 +323,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
     for (int it = 0; it < nk; ++it) {
       // retire this wave's DMAs of stage it; the younger stages stay in flight
       const int younger = min(NS - 2, nk - 1 - it);
-      if constexpr (NS == 4) {
-        if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
-        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      wait_stage<NG, NS - 2>(younger);
       float* cur = slot(it);
       if (tail && it == nk - 1) {  // zero the k-tail this thread's DMAs brought in
         const int k0 = kb + it * BK;

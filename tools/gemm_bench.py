@@ -32,17 +32,22 @@ def vp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def run(shape, cfg, sk, reps, lib, stream):
+def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1):
     # M,N,K,ak,bk[,gather[,splits]]: gather = rows of A (K-major A) or k-rows
     # of B (N-major B, the weight-gradient form); splits > 1 = split-K slabs
     M, N, K, ak, bk, *g = [int(x) for x in shape.split(",")]
     gather = bool(g and g[0])
     splits = g[1] if len(g) > 1 else 1
     dev = "cuda"
-    A = torch.randn((M if ak else K), (K if ak else M), device=dev)
+    rows = max(M, pool) if (ak and gather) else M
+    A = torch.randn((rows if ak else K), (K if ak else M), device=dev)
     B = torch.randn((N if bk else K), (K if bk else N), device=dev)
     C = torch.empty(splits, M, N, device=dev)
-    a_idx = torch.randperm(M, device=dev).to(torch.int32) if gather and ak else None
+    # pool > M: gathered rows from a larger table, `sets` different row sets
+    # cycled over the repetitions (cold: sets x M rows exceed the Infinity Cache)
+    idx_sets = [torch.randperm(rows, device=dev)[:M].to(torch.int32) for _ in range(sets)] \
+        if gather and ak else [None]
+    a_idx = idx_sets[0]
     b_idx = torch.randperm(K, device=dev).to(torch.int32) if gather and not ak and not bk else None
     args = (M, N, K, ak, bk, vp(A), A.shape[1], vp(a_idx), vp(B), B.shape[1], vp(b_idx), vp(C), N,
             None, 0, 3 if splits > 1 else 0, splits, cfg, sk, ctypes.c_void_p(stream.cuda_stream))
@@ -55,9 +60,11 @@ def run(shape, cfg, sk, reps, lib, stream):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
         lib.pinsage_gemm_ex(*args)
+    all_args = [tuple(vp(ix) if i == 7 else a for i, a in enumerate(args)) for ix in idx_sets] \
+        if idx_sets[0] is not None else [args]
     e0.record(stream)
-    for _ in range(reps):
-        lib.pinsage_gemm_ex(*args)
+    for r in range(reps):
+        lib.pinsage_gemm_ex(*all_args[r % len(all_args)])
     e1.record(stream)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
@@ -70,6 +77,8 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=DEFAULT)
     ap.add_argument("--cfgs", default="-1,0,1,2")
     ap.add_argument("--sk", default="0,1", help="stream-K settings (-1 auto, 0 off, 1 on)")
+    ap.add_argument("--pool", type=int, default=0, help="rows of the gathered table (0 = M)")
+    ap.add_argument("--sets", type=int, default=1, help="row sets cycled over repetitions")
     a = ap.parse_args()
     lib = nat.lib()
     stream = torch.cuda.current_stream()
@@ -78,7 +87,7 @@ def main():
             for sk in [int(c) for c in a.sk.split(",")]:
                 if sk == 1 and cfg == 0:
                     continue
-                us, tf, err = run(s, cfg, sk, a.reps, lib, stream)
+                us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets)
                 print(f"{s:24s} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
                       flush=True)
 
