@@ -82,6 +82,7 @@ _SIGS = {
     "pinsage_engine_forward": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_frontier": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_forward_layers": (ctypes.c_int, [vp, vp, vp]),
+    "pinsage_engine_set_fork": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_gather_output": (ctypes.c_int, [vp, vp, i64, vp, vp]),
     "pinsage_engine_loss": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_int, vp]),
     "pinsage_engine_set_output_grad": (ctypes.c_int, [vp, vp, vp, i64, vp]),

@@ -113,9 +113,20 @@ struct Engine {
   // the optimizer pass.  Measured at C2 in the one-launch step graph (bench.py):
   // 0.605-0.615 / - / 0.645-0.648 / 0.611-0.640 / 0.620-0.626 ms per step.
   int stream_mode = getenv("PINSAGE_BWD_STREAMS") ? atoi(getenv("PINSAGE_BWD_STREAMS")) : 0;
+  // weight-gradient GEMMs beside the chain use at most this many workgroups
+  // (PINSAGE_SIDE_GRID; 0 = no cap), leaving the other CUs to the chain
+  int side_grid = getenv("PINSAGE_SIDE_GRID") ? atoi(getenv("PINSAGE_SIDE_GRID")) : 0;
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   std::vector<TimingSite> sites;
+  // pinsage_engine_set_fork: the next forward_layers call forks another
+  // workspace's frontier onto `stream` right after the layer-0 Q projection
+  struct Fork {
+    hipStream_t stream = nullptr;
+    void* ws = nullptr;
+    const int64_t* ids = nullptr;
+    int64_t n = 0;
+  } fork;
   std::vector<LayerBuf> L;
   int64_t pG1w = 0, pG1b = 0, pG2w = 0, n_params = 0;
   // workspace layout
@@ -438,6 +449,11 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       with_sk(E, ws, q);
       PS_TRY(launch_gemm(q, st));
     }
+    if (l == 0 && E.fork.stream) {  // the next batch's frontier beside the rest of the step
+      PS_TRY(ensure_streams(E));
+      PS_TRY(dep(E, st, E.fork.stream));
+      PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
+    }
     Timed t_agg(E, lname("fwd.agg", l), st);
     PS_TRY(launch_agg(at<float>(ws, lb.q), (int)c.hid, at<int32_t>(ws, lb.loc),
                       at<float>(ws, lb.wloc), T, cnt(lb.S), lb.S.cap, at<float>(ws, lb.agg), st));
@@ -553,13 +569,14 @@ static AdamSlice adam_slice(const Engine& E, const AdamStep& a, int64_t w_off, i
 // weight-gradient stream may be using the others meanwhile)
 static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st,
                        const AdamSlice* adam = nullptr, hipEvent_t after_use = nullptr,
-                       bool main = false) {
+                       bool main = false, bool beside = false) {
   float* const slab = at<float>(ws, main ? E.slab_main : E.slab);
   float* const bslab = at<float>(ws, main ? E.bslab_main : E.bslab);
   int cfg = 0, S = 1;
   choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
   GemmParams p;
   p.cfg = cfg;
+  if (beside) p.grid_cap = E.side_grid;
   p.M = w.M;
   p.N = w.N;
   p.K_dev = w.K_dev;
@@ -649,7 +666,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.K_hint = top.S.hint;
     w.dst = gr + E.pG2w;
     w.ld_dst = o;
-    PS_TRY(weight_grad(E, ws, w, s_wg));
+    PS_TRY(weight_grad(E, ws, w, s_wg, nullptr, nullptr, false, s_wg != st));
   }
   // dP1 = (dZ G2) * lrelu'(H1), dY_top = dP1 G1 and the top layer's
   // normalisation backward (dp_top) in one kernel, which also zeroes the
@@ -704,7 +721,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
     Timed tw(E, "bwd.wgrad.head", s_wg);
-    PS_TRY(weight_grad(E, ws, w, s_wg));
+    PS_TRY(weight_grad(E, ws, w, s_wg, nullptr, nullptr, false, s_wg != st));
   }
   t_hb.stop();
   for (int l = Lc - 1; l >= 0; --l) {
@@ -775,7 +792,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     }
     {
       Timed tw(E, lname("bwd.w_wgrad", l), s_w);
-      PS_TRY(weight_grad(E, ws, w_wgrad, s_w));
+      PS_TRY(weight_grad(E, ws, w_wgrad, s_w, nullptr, nullptr, false, s_w != st));
     }
     if (adam && l == 0) {  // every gradient but Q0's exists on s_w; W0 was read last
       PS_TRY(dep(E, st, s_w));
@@ -834,7 +851,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       if (adam && l == 0) q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
       hipStream_t qs = l == 0 ? st : s_wg;
       Timed tq(E, lname("bwd.q_wgrad", l), qs);
-      PS_TRY(weight_grad(E, ws, q_wgrad, qs, adam && l == 0 ? &q0 : nullptr, nullptr, l == 0));
+      PS_TRY(weight_grad(E, ws, q_wgrad, qs, adam && l == 0 ? &q0 : nullptr, nullptr, l == 0,
+                         qs != st));
     }
   }
   // every gradient is written once the side streams drain into st
@@ -1033,6 +1051,17 @@ int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int
 
 int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream) {
   return engine_layers(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
+}
+
+int pinsage_engine_set_fork(pinsage_engine* e, void* ws_next, const int64_t* ids_next,
+                            int64_t n_ids, void* side_stream) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  if (side_stream && (!ws_next || !ids_next || n_ids <= 0 || n_ids > E->cfg.max_pos)) {
+    set_error("engine_set_fork: bad argument");
+    return kErrArg;
+  }
+  E->fork = Engine::Fork{(hipStream_t)side_stream, ws_next, ids_next, n_ids};
+  return kOk;
 }
 
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,

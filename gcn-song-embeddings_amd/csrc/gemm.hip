@@ -667,6 +667,7 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
     const int G = splits > 1 ? splits : tiles_m, W = splits > 1 ? tiles_m * tiles_n : tiles_n;
     const int64_t iters = 8LL * ((G + 7) / 8) * W;
     grid = (int)(iters < 1024 ? iters : 1024);
+    if (p.grid_cap > 0 && grid > p.grid_cap) grid = p.grid_cap;
     grid = (grid + 7) / 8 * 8;
   }
   dim3 g(grid);

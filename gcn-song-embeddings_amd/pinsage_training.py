@@ -244,8 +244,10 @@ class _FusedStep:
     that one (it is whenever nothing else used torch's generator in between);
     otherwise it first launches its own frontier graph.  Results are the same
     either way.  PINSAGE_FRONTIER_AHEAD: "start" (default: the branch forks at
-    the graph's start), "graph" (it forks before the backward) or "0" (no
-    look-ahead); measured at C2: 0.649 / 0.657 / 0.697 ms per step."""
+    the graph's start), "fwd" (forked by the engine after the layer-0 Q
+    projection), "graph" (it forks before the backward) or "0" (no look-ahead);
+    measured at C2 (ms/step, run-to-run noise ~4 %): 0.57-0.62 / 0.62 / 0.64 /
+    0.70."""
 
     HOST_RING = 8
     OUT_RING = 1 << 16
@@ -453,6 +455,16 @@ class _FusedStep:
                 if self.ahead_mode == "start":
                     fork_next_frontier()
                     self._main(B, p, with_adam=adam)
+                elif self.ahead_mode == "fwd":  # forked inside, after the layer-0 Q projection
+                    side.wait_stream(cur)
+                    e = self.runner.engine
+                    nat.check(nat.lib().pinsage_engine_set_fork(
+                        e.h, nat.ptr(self.wss[1 - p]), nat.ptr(self.ids_view[1 - p]), 3 * B,
+                        ctypes.c_void_p(side.cuda_stream)), "set_fork")
+                    try:
+                        self._main(B, p, with_adam=adam)
+                    finally:
+                        nat.lib().pinsage_engine_set_fork(e.h, None, None, 0, None)
                 else:  # beside the backward: a latency-bound chain with CUs to spare
                     self._main(B, p, with_adam=adam, before_backward=fork_next_frontier)
                 cur.wait_stream(side)

@@ -239,6 +239,12 @@ int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int6
 int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                             void* stream);
 int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream);
+/* Until reset with side_stream = NULL: each pinsage_engine_forward_layers call
+ * also runs pinsage_engine_frontier(ws_next, ids_next, n_ids) on side_stream,
+ * forked (event) right after the layer-0 Q projection, so it overlaps the rest
+ * of the step.  The caller joins side_stream back. */
+int pinsage_engine_set_fork(pinsage_engine* e, void* ws_next, const int64_t* ids_next,
+                            int64_t n_ids, void* side_stream);
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
                                  void* stream);
 /* max_margin_loss + monitors on the last forward of a [B][3] batch; writes dZ */
