@@ -1,0 +1,107 @@
+"""The trainer API around the train step (pinsage_training.py:108-339) on the
+GPU: the epoch loop with its per-epoch ExponentialLR decay and per-batch
+checkpoint, resuming from that checkpoint (the reference's state.pt keys and
+formats), and embedding export (embed, save_embeddings / load_embeddings).
+"""
+import os
+import tempfile
+import types
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N = 3000
+
+
+def _problem(tmp):
+    import graph
+    import synthetic
+    pg = synthetic.make_playlist_graph(N, 600, 20000, seed=41)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
+    feats = torch.from_numpy(synthetic.make_features(N, 128, seed=42))  # d_in >= out_dim (reference)
+    pos = torch.from_numpy(synthetic.make_positives(pg, 12000, seed=43))
+    return g, feats, pos
+
+
+def test_train_loop_checkpoint_and_resume():
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=True)
+            tr.epochs, tr.b_per_e, tr.batch_size = 2, 3, 32
+            p0 = [p.detach().clone() for p in tr.model.parameters()]
+            torch.manual_seed(2)
+            tr.train()
+            assert (tr.e, tr.b) == (2, 0)
+            assert abs(tr.optimizer.param_groups[0]["lr"] - 1e-4 * 0.95 ** 2) < 1e-15
+            assert all(not torch.equal(a, b.detach()) for a, b in zip(p0, tr.model.parameters()))
+            path = os.path.join("runs", tr.run_name, "state.pt")
+            prog = torch.load(path, weights_only=True)
+            assert set(prog) == {"epochs_done", "batches_done", "model_state", "optimizer_state"}
+            # the last checkpoint was written after the last batch of epoch 2
+            assert (prog["epochs_done"], prog["batches_done"]) == (1, 2)
+            assert set(prog["model_state"]) == set(tr.model.state_dict())
+            st = prog["optimizer_state"]["state"]
+            assert all(int(float(v["step"])) == 6 for v in st.values())  # 2 epochs x 3 batches
+            for k, v in tr.model.state_dict().items():
+                assert torch.equal(prog["model_state"][k], v.detach().cpu()), k
+            # resume: the constructor loads state.pt (reference load_model semantics)
+            torch.manual_seed(1)
+            tr2 = pt.PinSage(g, N, feats, pos, log=False, load_save=True)
+            assert (tr2.e, tr2.b) == (1, 2)
+            for a, b in zip(tr.model.parameters(), tr2.model.parameters()):
+                assert torch.equal(a.detach().cpu(), b.detach().cpu())
+            sd1, sd2 = tr.optimizer.state_dict(), tr2.optimizer.state_dict()
+            for k in sd1["state"]:
+                for kk in ("exp_avg", "exp_avg_sq"):
+                    assert torch.equal(sd1["state"][k][kk].cpu(), sd2["state"][k][kk].cpu())
+            # and keeps training from there (one more batch through the fused step)
+            tr2.batch_size = 32
+            torch.manual_seed(3)
+            batch, _ = tr2.next_batch()
+            loss, _, _ = tr2.train_batch(batch)
+            assert np.isfinite(float(loss))
+            tr2._sync_state()  # (save_model syncs the optimizer's step counters)
+            assert all(int(float(v["step"])) == 7 for v in tr2.optimizer.state_dict()["state"].values())
+        finally:
+            os.chdir(cwd)
+
+
+def test_embed_and_embedding_files():
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            ids = torch.tensor([5, 17, 5, 2999, 0])
+            e = tr.embed(ids)
+            assert e.shape == (5, 128)
+            ref = tr.model(tr.features, ids)
+            assert torch.allclose(e.cpu(), ref.detach().cpu(), rtol=1e-5, atol=1e-6)
+            assert torch.allclose(e[0], e[2])                     # a repeated id, same row
+            # batched branch: the reference resets ids to range(len(ids)) (pinsage_training.py:270-273)
+            eb = tr.embed(ids, bsize=2)
+            rng = tr.model(tr.features, torch.arange(5)).detach().cpu()
+            assert torch.allclose(eb.cpu(), rng, rtol=1e-5, atol=1e-6)
+            ds = types.SimpleNamespace(tracks={f"track{i:05d}": {} for i in range(N)})
+            pt.save_embeddings(tr, ds, base_run_dir=os.path.join(tmp, "runs"))
+            emb_dir = os.path.join(tmp, "runs", tr.run_name, "emb")
+            assert len(os.listdir(emb_dir)) == N
+            one = torch.load(os.path.join(emb_dir, "track00017.pt"), weights_only=True)
+            assert one.shape == (128,) and one.dtype == torch.float32
+            allv = pt.load_embeddings(tr, ds, base_run_dir=os.path.join(tmp, "runs"))
+            full = tr.embed().detach().cpu()
+            assert torch.allclose(allv, full, rtol=1e-5, atol=1e-6)
+        finally:
+            os.chdir(cwd)
