@@ -11,6 +11,7 @@ on a synthetic playlist graph resident in HBM.  N > 1: one process per GPU
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -246,7 +247,12 @@ def main():
         nat.lib().pinsage_engine_timing(eng.h, 1)
         n_t = max(5, min(20, args.steps))
         sizes = []
+        hold_stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         for _ in range(n_t):
+            # hold the stream while the host queues the step, so the events time the
+            # kernels back to back (an eager step's host enqueue is ~0.5 ms: without
+            # the hold, an idle GPU would charge each launch's host gap to its kernel)
+            nat.lib().pinsage_stream_hold(3000, hold_stream)
             step()
             torch.cuda.synchronize()
             off = eng.off

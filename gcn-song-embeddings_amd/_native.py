@@ -70,6 +70,9 @@ _SIGS = {
     "pinsage_weighted_agg": (ctypes.c_int, [vp, i64, vp, vp, i64, i64, vp, vp]),
     "pinsage_step_stage": (ctypes.c_int, [vp, i64, i64, vp, i64, i64, vp, i64, vp, vp]),
     "pinsage_step_publish": (ctypes.c_int, [vp, i64, vp, i64, vp, vp]),
+    "pinsage_stream_hold": (ctypes.c_int, [i64, vp]),
+    "pinsage_segment_wmean": (ctypes.c_int, [vp, i64, i64, i64, vp, vp, vp, i64, ctypes.c_int, vp, i64,
+                                             vp]),
     "pinsage_knn_scratch_bytes": (i64, [i64, i64]),
     "pinsage_knn_cosine": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, i64, f32, vp, i64, vp, vp, vp]),
     "pinsage_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(vp)]),

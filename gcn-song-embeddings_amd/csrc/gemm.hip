@@ -26,6 +26,7 @@ namespace ps {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kLdsBudget = 81920;  // bytes per workgroup: two workgroups per CU
+constexpr int kLdsBudget3 = 54272;  // three workgroups per CU (cfg 3)
 constexpr int kIdxWin = 1024;  // gathered k-rows staged in LDS at a time
 
 // One 16-B LDS-DMA per lane (global_load_lds_dwordx4; LDS destination = M0 +
@@ -187,8 +188,8 @@ __device__ __forceinline__ void wait_stage(int younger) {
 
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK; at most
 // NSMAX stage buffers in the ring.
-template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4>
-__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
+template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2>
+__global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
   using OpB = typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type;
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   // ring depth: as many stage buffers as fit two workgroups per CU (3 or 4);
   // the k-row windows exist only for MN-major (possibly gathered) operands
   constexpr int IDXF = (GA ? kIdxWin : 0) + (GB ? kIdxWin : 0);
-  constexpr int NSA = (kLdsBudget / 4 - IDXF) / SZS;
+  constexpr int NSA = ((WPC == 2 ? kLdsBudget : kLdsBudget3) / 4 - IDXF) / SZS;
   constexpr int NS = NSA > NSMAX ? NSMAX : NSA;
   static_assert(NS >= 3, "stage buffers do not fit");
   __shared__ __attribute__((aligned(16))) float smem[NS * SZS + IDXF];
@@ -448,7 +449,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
         }
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        int64_t dsts[16];  // scatter rows loaded before the stores (see below)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          dsts[r] = row < M ? (p.c_idx ? (int64_t)p.c_idx[row] : (int64_t)row) : -1;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int lrow = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -458,7 +465,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
           for (int q = 0; q < WN; ++q) tot += red[q * BM + lrow];
           const float nrm = sqrtf(tot);
-          const int64_t dst = p.c_idx ? p.c_idx[row] : row;
+          const int64_t dst = dsts[r];
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int col = n0 + (wn * TN + j) * 32 + l32;
@@ -466,8 +473,18 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
           }
           if (p.norms && wn == 0 && l32 == 0) p.norms[row] = nrm;
         }
+      }
     } else {
+      // the bias is read into registers before the first store (interleaved,
+      // each store may alias the next bias load, which was then re-issued and
+      // waited on per element)
       const bool accum = p.epi == kEpiAccum;
+      float bj[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + (wn * TN + j) * 32 + l32;
+        bj[j] = (p.bias && col < N) ? p.bias[col] : 0.f;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -479,8 +496,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
           for (int j = 0; j < TN; ++j) {
             const int col = n0 + (wn * TN + j) * 32 + l32;
             if (col >= N) continue;
-            float v = acc[i][j][r];
-            if (p.bias) v += p.bias[col];
+            float v = acc[i][j][r] + bj[j];
             if (p.act) v = lrelu(v);
             if (p.mask) v *= lrelu_grad(p.mask[(int64_t)row * p.ldm + col]);
             if (p.c2 && col >= p.N1) {
@@ -556,7 +572,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmParams p) {
   }
 }
 
-constexpr int kCfgBM[3] = {128, 64, 32};
+constexpr int kCfgBM[4] = {128, 64, 32, 64};
 
 int gemm_slots() {
   static const int slots = [] {
@@ -575,9 +591,16 @@ int64_t gemm_sk_slab_floats() { return (int64_t)gemm_slots() * 2 * 64 * 128; }
 // Cost model: tiles are dealt round-robin over 256 CUs, so a launch takes
 // ~ceil(tiles / 256) tile-times and a tile-time is ~ BM (fixed BN, same K).
 // Pick the cheapest; ties go to the larger tile (fewer operand re-reads).
+// Exception: 64-row tiles that overflow two resident workgroups per CU but fit
+// three go to cfg 3 (64 x 128 x 16, three per CU): one round instead of a full
+// round plus a tail of lone workgroups (tools/gemm_bench.py: 10541x512x512
+// 73 -> 69 us, 5716x1024x128 32 -> 28 us; at 1024 tiles cfg 3 is slower).
 int gemm_pick_config(int M, int N, int splits) {
   if (splits > 1) return 0;
   const int64_t tn = (N + 127) / 128;
+  const int64_t cus = gemm_slots() / 2;
+  const int64_t t64 = ((M + 63) / 64) * tn;
+  if (t64 > 2 * cus && t64 <= 3 * cus) return 3;
   int best = 0;
   int64_t best_cost = -1;
   for (int c = 0; c < 3; ++c) {
@@ -597,8 +620,10 @@ static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16>), g, dim3(256), 0, st, p);
   else if (cfg == 1)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 32>), g, dim3(256), 0, st, p);
-  else
+  else if (cfg == 2)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32>), g, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3>), g, dim3(256), 0, st, p);
 }
 
 int launch_gemm(const GemmParams& p_in, hipStream_t st) {

@@ -33,6 +33,14 @@ __global__ void step_publish_kernel(const float* __restrict__ scal, int n, float
   if (threadIdx.x == 0) *ctr += 1;
 }
 
+// one wave that holds the stream for `ticks` of the 100 MHz constant clock
+// (measurement only: the launches queued behind it then run back to back, so
+// events around them time the GPU work and not the host's enqueue gaps)
+__global__ void stream_hold_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 }  // namespace ps
 
 using namespace ps;
@@ -64,6 +72,16 @@ int pinsage_step_publish(const float* scal, int64_t n, float* ring_out, int64_t 
   }
   hipLaunchKernelGGL(step_publish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, scal, (int)n,
                      ring_out, R2, ctr);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int pinsage_stream_hold(int64_t us, void* stream) {
+  if (us < 0 || us > 1000000) {
+    set_error("stream_hold: us must be in [0, 1e6]");
+    return kErrArg;
+  }
+  hipLaunchKernelGGL(stream_hold_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint64_t)us * 100u);
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -169,6 +169,25 @@ int pinsage_step_stage(const void* ring, int64_t slot_bytes, int64_t R, const in
                        void* stream);
 int pinsage_step_publish(const float* scal, int64_t n, float* ring_out, int64_t R2, int64_t* ctr,
                          void* stream);
+/* Measurement only (bench.py's per-kernel timing pass): one wave that holds the
+ * stream for `us` microseconds (0..1e6) of the constant 100 MHz clock, so the
+ * launches the host queues behind it run back to back and events around them
+ * time the kernels rather than the host's enqueue gaps. */
+int pinsage_stream_hold(int64_t us, void* stream);
+
+/* ------------------------------------------------------------------ lib/gnns MEAN aggregator
+ * GNN_model.aggregate, agg_func 'MEAN' (lib/gnns/GNNs_unsupervised.py:537-588):
+ * mask.mm(embed_matrix) with the dense [F, U] mask kept as a CSR.  For each
+ * segment i in [0, n_seg), entries j in [seg_ptr[i], seg_ptr[i+1]):
+ *   out[i, :] = sum_j w[j] * h[cols[j], :] / den_i
+ * den_i = max(sum_j |w[j]|, 1e-12) (F.normalize(p=1)) if normalize, else 1.
+ * h f32 [n_h][ldh], out f32 [n_seg][ldo], seg_ptr int64 [n_seg + 1], cols int32,
+ * w f32 (device).  Entries whose col is outside [0, n_h) are skipped (the
+ * caller validates).  The backward (dH = mask^T dOut) is the same call over the
+ * transposed CSR with pre-normalised weights and normalize = 0. */
+int pinsage_segment_wmean(const float* h, int64_t ldh, int64_t n_h, int64_t d, const int64_t* seg_ptr,
+                          const int32_t* cols, const float* w, int64_t n_seg, int normalize, float* out,
+                          int64_t ldo, void* stream);
 
 /* ------------------------------------------------------------------ cosine kNN
  * knn_from_emb (baselines.py:91-103) over cosine_sim_ab (baselines.py:69-77), the

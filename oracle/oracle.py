@@ -327,3 +327,45 @@ class RefTrainer:
             losses.append(float(loss))
         self.opt.step()
         return losses
+
+
+# ----------------------------------------------------------------------------- lib/gnns
+def gnns_mean_aggregate(nodes, emb, unique, samp, adj_indptr, adj_indices, adj_data, gcn):
+    """``GNN_model.aggregate`` with agg_func 'MEAN', gat False
+    (lib/gnns/GNNs_unsupervised.py:537-588) as the reference computes it: a
+    dense [F, U] float32 mask of ones at the sampled neighbours (the node itself
+    dropped unless gcn, :543-544), times sqrt(edge count) (:553-554, float32),
+    L1-normalised per row with eps 1e-12 (F.normalize, :572), then mask @ emb
+    (:577) where emb is the unique-node rows unless it already has U rows
+    (:546-549).  ``samp`` is a list of iterables (the sampled sets).
+    Returns (agg [F, d], mask [F, U], emb_rows) so a test can form gradients."""
+    U = len(unique)
+    col_of = {int(u): j for j, u in enumerate(unique)}
+    mask = np.zeros((len(nodes), U), np.float32)
+    for i, s in enumerate(samp):
+        s = {int(x) for x in s}
+        if not gcn:
+            s = s - {int(nodes[i])}
+        for v in s:
+            mask[i, col_of[v]] = 1.0
+    # edge_counts = adj_matrix[nodes][:, unique_nodes_list].toarray() (:553)
+    ec = np.zeros((len(nodes), U), np.float32)
+    for i, r in enumerate(nodes):
+        for p in range(int(adj_indptr[r]), int(adj_indptr[r + 1])):
+            c = int(adj_indices[p])
+            if c in col_of:
+                ec[i, col_of[c]] = np.float32(adj_data[p])
+    mask = mask * np.sqrt(ec, dtype=np.float32)
+    den = np.maximum(np.abs(mask).sum(1, keepdims=True, dtype=np.float32), np.float32(1e-12))
+    mask = (mask / den).astype(np.float32)
+    rows = np.arange(U) if len(emb) == U else np.asarray(unique, np.int64)
+    agg = (mask.astype(np.float64) @ np.asarray(emb, np.float64)[rows]).astype(np.float32)
+    return agg, mask, rows
+
+
+def gnns_mean_aggregate_grad(mask, rows, G, n_emb):
+    """d(sum(agg * G)) / d emb for gnns_mean_aggregate: mask^T G scattered to
+    the embedding rows it read."""
+    g = np.zeros((n_emb, G.shape[1]), np.float64)
+    np.add.at(g, rows, mask.T.astype(np.float64) @ np.asarray(G, np.float64))
+    return g.astype(np.float32)

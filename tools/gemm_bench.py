@@ -32,7 +32,7 @@ def vp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1):
+def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_idx=False):
     # M,N,K,ak,bk[,gather[,splits]]: gather = rows of A (K-major A) or k-rows
     # of B (N-major B, the weight-gradient form); splits > 1 = split-K slabs
     M, N, K, ak, bk, *g = [int(x) for x in shape.split(",")]
@@ -47,15 +47,20 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1):
     # cycled over the repetitions (cold: sets x M rows exceed the Infinity Cache)
     idx_sets = [torch.randperm(rows, device=dev)[:M].to(torch.int32) for _ in range(sets)] \
         if gather and ak else [None]
+    if sort_idx and idx_sets[0] is not None:  # the frontier's sorted distinct rows
+        idx_sets = [ix.sort().values for ix in idx_sets]
+    bias = torch.randn(N, device=dev) if bias_act else None
     a_idx = idx_sets[0]
     b_idx = torch.randperm(K, device=dev).to(torch.int32) if gather and not ak and not bk else None
     args = (M, N, K, ak, bk, vp(A), A.shape[1], vp(a_idx), vp(B), B.shape[1], vp(b_idx), vp(C), N,
-            None, 0, 3 if splits > 1 else 0, splits, cfg, sk, ctypes.c_void_p(stream.cuda_stream))
+            vp(bias), int(bias_act), 3 if splits > 1 else 0, splits, cfg, sk, ctypes.c_void_p(stream.cuda_stream))
     rc = lib.pinsage_gemm_ex(*args)
     if rc != 0:
         raise RuntimeError(lib.pinsage_last_error().decode())
     ref = (A[a_idx.long()] if a_idx is not None else A) if ak else A.t()
     ref = ref @ ((B.t() if bk else (B[b_idx.long()] if b_idx is not None else B)))
+    if bias_act:
+        ref = torch.nn.functional.leaky_relu(ref + bias)
     err = ((C.sum(0) - ref).abs().max() / ref.abs().max()).item()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
@@ -79,6 +84,8 @@ def main():
     ap.add_argument("--sk", default="0,1", help="stream-K settings (-1 auto, 0 off, 1 on)")
     ap.add_argument("--pool", type=int, default=0, help="rows of the gathered table (0 = M)")
     ap.add_argument("--sets", type=int, default=1, help="row sets cycled over repetitions")
+    ap.add_argument("--bias-act", action="store_true", help="bias + LeakyReLU epilogue (the Q projection)")
+    ap.add_argument("--sorted", action="store_true", help="gathered rows in ascending order")
     a = ap.parse_args()
     lib = nat.lib()
     stream = torch.cuda.current_stream()
@@ -87,7 +94,7 @@ def main():
             for sk in [int(c) for c in a.sk.split(",")]:
                 if sk == 1 and cfg == 0:
                     continue
-                us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets)
+                us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets, a.bias_act, a.sorted)
                 print(f"{s:24s} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
                       flush=True)
 
