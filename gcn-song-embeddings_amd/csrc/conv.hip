@@ -91,24 +91,44 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int h4 = hid >> 2;
+  constexpr int U = 8;  // neighbour rows whose loads are in flight together (16 spills)
   for (int64_t f = wid; f < F; f += nw) {
     for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
       float4 a[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) a[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int t = 0; t < T; ++t) {
-        const int64_t r = loc[f * T + t];
-        const float w = wloc[f * T + t];
-        const float4* qr = reinterpret_cast<const float4*>(q + r * hid);
+      // the row's slots are read by the lanes (64 at a time) and broadcast, so
+      // U neighbour rows' loads issue back to back instead of one index load ->
+      // row load round trip per slot; the summation order stays t = 0, 1, ...
+      for (int tb = 0; tb < T; tb += 64) {
+        const int tn = min(64, T - tb);
+        const int myr = lane < tn ? loc[f * T + tb + lane] : 0;
+        const float myw = lane < tn ? wloc[f * T + tb + lane] : 0.f;
+        for (int t0 = 0; t0 < tn; t0 += U) {
+          float4 x[U][VEC];
+          float w[U];
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          const int c = c0 + v * 64 + lane;
-          if (c < h4) {
-            const float4 x = qr[c];
-            a[v].x = fmaf(w, x.x, a[v].x);
-            a[v].y = fmaf(w, x.y, a[v].y);
-            a[v].z = fmaf(w, x.z, a[v].z);
-            a[v].w = fmaf(w, x.w, a[v].w);
+          for (int u = 0; u < U; ++u) {
+            const int t = min(t0 + u, tn - 1);
+            const int64_t r = __shfl(myr, t, 64);
+            w[u] = t0 + u < tn ? __shfl(myw, t, 64) : 0.f;
+            const float4* qr = reinterpret_cast<const float4*>(q + r * hid);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+              const int c = min(c0 + v * 64 + lane, h4 - 1);
+              x[u][v] = qr[c];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (t0 + u >= tn) break;
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+              a[v].x = fmaf(w[u], x[u][v].x, a[v].x);
+              a[v].y = fmaf(w[u], x[u][v].y, a[v].y);
+              a[v].z = fmaf(w[u], x[u][v].z, a[v].z);
+              a[v].w = fmaf(w[u], x[u][v].w, a[v].w);
+            }
           }
         }
       }
