@@ -91,9 +91,15 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int h4 = hid >> 2;
-  constexpr int U = 8;  // neighbour rows whose loads are in flight together (16 spills)
-  for (int64_t f = wid; f < F; f += nw) {
-    for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
+  // neighbour rows whose loads are in flight together (16 x 2 float4 spill)
+  constexpr int U = VEC == 1 ? 16 : 8;
+  // work item = (row, 64*VEC-float4 column chunk): hid 512 at VEC 1 gives two
+  // waves per row, each with all of a T <= 16 row's loads in one round
+  const int nch = (h4 + 64 * VEC - 1) / (64 * VEC);
+  for (int64_t item = wid; item < F * nch; item += nw) {
+    const int64_t f = item / nch;
+    {
+      const int c0 = (int)(item - f * nch) * 64 * VEC;
       float4 a[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) a[v] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -119,15 +125,16 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
               x[u][v] = qr[c];
             }
           }
+          // padded slots select the old sum (a break here made x a scratch array)
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            if (t0 + u >= tn) break;
+            const bool ok = t0 + u < tn;
 #pragma unroll
             for (int v = 0; v < VEC; ++v) {
-              a[v].x = fmaf(w[u], x[u][v].x, a[v].x);
-              a[v].y = fmaf(w[u], x[u][v].y, a[v].y);
-              a[v].z = fmaf(w[u], x[u][v].z, a[v].z);
-              a[v].w = fmaf(w[u], x[u][v].w, a[v].w);
+              a[v].x = ok ? fmaf(w[u], x[u][v].x, a[v].x) : a[v].x;
+              a[v].y = ok ? fmaf(w[u], x[u][v].y, a[v].y) : a[v].y;
+              a[v].z = ok ? fmaf(w[u], x[u][v].z, a[v].z) : a[v].z;
+              a[v].w = ok ? fmaf(w[u], x[u][v].w, a[v].w) : a[v].w;
             }
           }
         }
@@ -1019,13 +1026,14 @@ int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, i
                const int* nS, int64_t S_max, float* agg, hipStream_t st) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "agg: hidden dim must be a multiple of 4");
   if (S_max <= 0) return kOk;
-  const int grid = grid_for(S_max * 64, 256, 4096);
+  // hid >= 512: one wave per row (2 float4 per lane per slot, 8 slots in flight);
+  // measured faster than two waves per row with all 16 slots in flight
   if (hid >= 512)
-    hipLaunchKernelGGL((agg_kernel<2>), dim3(grid), dim3(256), 0, st, q, hid, loc, wloc, T, nS,
-                       S_max, agg);
+    hipLaunchKernelGGL((agg_kernel<2>), dim3(grid_for(S_max * 64, 256, 4096)), dim3(256), 0, st, q, hid,
+                       loc, wloc, T, nS, S_max, agg);
   else
-    hipLaunchKernelGGL((agg_kernel<1>), dim3(grid), dim3(256), 0, st, q, hid, loc, wloc, T, nS,
-                       S_max, agg);
+    hipLaunchKernelGGL((agg_kernel<1>), dim3(grid_for(S_max * ((hid / 4 + 63) / 64) * 64, 256, 8192)),
+                       dim3(256), 0, st, q, hid, loc, wloc, T, nS, S_max, agg);
   PS_CHECK_LAUNCH();
   return kOk;
 }
