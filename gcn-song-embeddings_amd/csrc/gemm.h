@@ -85,7 +85,8 @@ int gemm_slots();
 //   0: 128 x 128 x 16  (2x2 waves of 64x64)      large M
 //   1:  64 x 128 x 32  (2x2 waves of 32x64)      medium M
 //   2:  32 x 128 x 32  (1x4 waves of 32x32)      small M, N = 128 (W projection)
-int gemm_pick_config(int M, int N, int splits);
+//   3:  64 x 128 x 16  (2x2 waves of 32x64), three workgroups per CU
+int gemm_pick_config(int M, int N, int K, int splits);
 
 int launch_gemm(const GemmParams& p, hipStream_t st);
 

@@ -594,13 +594,17 @@ int64_t gemm_sk_slab_floats() { return (int64_t)gemm_slots() * 2 * 64 * 128; }
 // Exception: 64-row tiles that overflow two resident workgroups per CU but fit
 // three go to cfg 3 (64 x 128 x 16, three per CU): one round instead of a full
 // round plus a tail of lone workgroups (tools/gemm_bench.py: 10541x512x512
-// 73 -> 69 us, 5716x1024x128 32 -> 28 us; at 1024 tiles cfg 3 is slower).
-int gemm_pick_config(int M, int N, int splits) {
+// 73 -> 69 us, 5716x1024x128 32 -> 28 us; at 1024 tiles cfg 3 is slower), and
+// so do short-K launches (K <= 256) of more than two 64-row tiles per CU, where
+// the per-tile fill and epilogue dominate and a third resident workgroup hides
+// them (K = 128, bias + LeakyReLU: 24369 x 512 69 -> 48 us, 49152 x 512
+// 100 -> 92 us against the 128 x 128 tiles this model picked before).
+int gemm_pick_config(int M, int N, int K, int splits) {
   if (splits > 1) return 0;
   const int64_t tn = (N + 127) / 128;
   const int64_t cus = gemm_slots() / 2;
   const int64_t t64 = ((M + 63) / 64) * tn;
-  if (t64 > 2 * cus && t64 <= 3 * cus) return 3;
+  if (t64 > 2 * cus && (t64 <= 3 * cus || K <= 256)) return 3;
   int best = 0;
   int64_t best_cost = -1;
   for (int c = 0; c < 3; ++c) {
@@ -652,7 +656,7 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
-  int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, splits);
+  int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, Kmax, splits);
   const int tiles_n = (p.N + 127) / 128;
   const int slots = gemm_slots();
 
