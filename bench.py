@@ -128,8 +128,8 @@ def pmc_traffic(config, site):
         except Exception:
             continue
         if d.get("site") == site and d.get("config") == config:
-            return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
-    return None, None
+            return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO), d.get("mfma_busy")
+    return None, None, None
 
 
 def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
@@ -279,7 +279,7 @@ def main():
     agg_bytes = U0 * hid * 4 + F0 * T * 8 + F0 * hid * 4
     agg_logical = F0 * T * hid * 4 + F0 * T * 8 + F0 * hid * 4
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "calls": v[1]} for k, v in sorted(kt.items())}
-    traffic, traffic_src = pmc_traffic(args.config, "fwd.q_gemm.l0")
+    traffic, traffic_src, mfma_busy = pmc_traffic(args.config, "fwd.q_gemm.l0")
     result = {
         "metric": "PinSAGE train-step nodes/sec (2-hop, batch 512) at 1/2/4/8 MI355X",
         "value": value,
@@ -301,7 +301,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "fwd.q_gemm.l0 (gather + fp32 MFMA Q projection)",
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
-                     "traffic_source": traffic_src,
+                     "traffic_source": traffic_src, "mfma_busy_pmc": mfma_busy,
                      "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg,
                      "algorithmic_bytes_per_launch": 4.0 * (U0 * d + d * hid + U0 * hid)},
         "gather_kernel": {"kernel": "fwd.agg.l0", "bound": "hbm", "avg_launch_ms": a_avg,
