@@ -7,9 +7,13 @@
 //
 // Per batch of query rows: one fp32 MFMA GEMM (launch_gemm: gathered query
 // rows x the whole table, K = d) writes the dot products to HBM, then one
-// workgroup per query row selects its top k by an MSB-first radix select on
-// the order-preserving uint32 image of the similarity (12 + 12 + 8 bit digits,
-// histograms in LDS) and sorts the k survivors in LDS.  Exact ties at the
+// workgroup per query row selects its top k: a threshold from the row's first
+// 4096 keys (LDS radix select), ONE pass that keeps every key >= it in per-wave
+// LDS segments, a radix select of the k-th key among those candidates, and an
+// LDS bitonic sort of the keys >= it.  Rows where that cannot be exact (fewer
+// than k candidates, a full segment) take the original path: an MSB-first
+// radix select over the whole row on the order-preserving uint32 image of the
+// similarity (12 + 12 + 8 bit digits, histograms in LDS), then the same sort.  Exact ties at the
 // k-th key keep the lowest column indices; the final order is (sim desc,
 // index asc).  The row of dot products stays in the Infinity Cache across the
 // select's four passes when the batch is sized to it.
@@ -59,6 +63,87 @@ __global__ void knn_ids_kernel(const int64_t* __restrict__ q, int64_t nq, int64_
 }
 
 // one workgroup per query row b: dots[b][0..n) -> top k of sim, sorted
+constexpr int kKnnSample = 4096;  // leading keys of a row that set the candidate threshold
+constexpr int kKnnSeg = 512;      // candidate slots per wave (16 waves: 8192 per row)
+
+// In-LDS bitonic sort of P (a power of two) (key, index) pairs into the final
+// order: key descending, then index ascending.  All threads of the block call it.
+__device__ void knn_bitonic(uint32_t* key, int32_t* idx, int P) {
+  for (int kk = 2; kk <= P; kk <<= 1) {
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      for (int i = threadIdx.x; i < P; i += kKnnBlock) {
+        const int l = i ^ jj;
+        if (l > i) {
+          const uint32_t ka = key[i], kb = key[l];
+          const int32_t ia = idx[i], ib = idx[l];
+          const bool a_first = ka > kb || (ka == kb && ia < ib);
+          const bool up = (i & kk) == 0;
+          if (up ? !a_first : a_first) {
+            key[i] = kb;
+            key[l] = ka;
+            idx[i] = ib;
+            idx[l] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// The rank-th largest of keys held in LDS (12 + 12 + 8 bit MSB-first radix
+// select; `get(i)` reads key i of `cnt`): returns it, and in *need_eq how
+// many keys equal to it are within the top `rank`.  All threads call it.
+template <class Get>
+__device__ uint32_t knn_lds_kth(Get get, int cnt, uint32_t rank, uint32_t* hist, uint32_t* sh,
+                                uint32_t* need_eq) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t prefix = 0, need = rank;
+  const int shifts[3] = {20, 8, 0};
+  const int widths[3] = {12, 12, 8};
+#pragma unroll 1
+  for (int p = 0; p < 3; ++p) {
+    const int sh_ = shifts[p], nb = 1 << widths[p], hs = sh_ + widths[p];
+    for (int i = tid; i < nb; i += kKnnBlock) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < cnt; i += kKnnBlock) {
+      const uint32_t key = get(i);
+      if (hs >= 32 || (key >> hs) == prefix) atomicAdd(&hist[(key >> sh_) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const int per = nb / 64;
+      uint32_t s = 0;
+      for (int i = 0; i < per; ++i) s += hist[nb - 1 - (lane * per + i)];
+      uint32_t inc = s;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      const uint32_t before = inc - s;
+      if (before < need && need <= inc) {
+        uint32_t c = before;
+        for (int i = 0; i < per; ++i) {
+          const int bin = nb - 1 - (lane * per + i);
+          const uint32_t h = hist[bin];
+          if (c + h >= need) {
+            sh[0] = (prefix << widths[p]) | (uint32_t)bin;
+            sh[1] = need - c;
+            break;
+          }
+          c += h;
+        }
+      }
+    }
+    __syncthreads();
+    prefix = sh[0];
+    need = sh[1];
+    __syncthreads();
+  }
+  *need_eq = need;
+  return prefix;
+}
+
 __global__ __launch_bounds__(kKnnBlock) void knn_select_kernel(
     const float* __restrict__ dots, int64_t n, const float* __restrict__ norms,
     const float* __restrict__ qn, float eps, int k, int P, float* __restrict__ out_w,
@@ -81,6 +166,120 @@ __global__ __launch_bounds__(kKnnBlock) void knn_select_kernel(
   auto key_at = [&](int64_t j) __attribute__((always_inline)) { return key_of(row[j], norms[j]); };
   // rows of n % 4 == 0 floats start 16-byte aligned (the dot rows are n apart)
   const bool vec = (n % 4) == 0;
+
+  // ---- one pass.  A threshold t = a key of the row's leading kKnnSample keys
+  // whose rank there lies (with wide slack) below k's expected rank; one pass
+  // keeps every key >= t in per-wave LDS segments (no shared counter).  If at
+  // least k keys reach t, the k-th largest key does too, so the candidates hold
+  // the whole top k and its ties: a radix select over them gives the k-th key,
+  // and sorting the keys >= it gives the exact result.  Otherwise (too few,
+  // a full segment, or more than kKnnMaxK keys >= the k-th) the 4-pass radix
+  // select below runs.
+  __shared__ uint32_t ckey[16 * kKnnSeg];
+  __shared__ int32_t cidx[16 * kKnnSeg];
+  __shared__ int seg_cnt[kKnnBlock / 64];
+  __shared__ uint32_t sh2[2];
+  {
+    const int S = (int)min<int64_t>(n, kKnnSample);
+    for (int i = tid; i < S; i += kKnnBlock) skey[i] = key_at(i);
+    __syncthreads();
+    const double er = (double)k * S / (double)n;
+    const uint32_t r = S == n ? (uint32_t)k : (uint32_t)min<double>(S, er * 1.5 + 4.0 * sqrt(er) + 8.0);
+    uint32_t dummy;
+    const uint32_t t = knn_lds_kth([&](int i) { return skey[i]; }, S, r, hist, sh2, &dummy);
+    int cw = 0;  // this wave's candidates (wave-uniform)
+    bool over = false;
+    uint32_t* const wk = ckey + wv * kKnnSeg;
+    int32_t* const wi = cidx + wv * kKnnSeg;
+    auto take = [&](uint32_t key, int64_t j, bool valid) __attribute__((always_inline)) {
+      const bool c = valid && key >= t;
+      const unsigned long long m = __ballot(c);
+      if (c) {
+        const int slot = cw + __popcll(m & ((1ull << lane) - 1ull));
+        if (slot < kKnnSeg) {
+          wk[slot] = key;
+          wi[slot] = (int32_t)j;
+        }
+      }
+      cw += __popcll(m);
+    };
+    // block-uniform trip counts: take() uses wave-wide ballots
+    const int64_t n16 = vec ? (n / 16) * 16 : 0;
+    for (int64_t base = 0; base < n16; base += (int64_t)kKnnBlock * 16) {
+      const int64_t j0 = base + (int64_t)tid * 16;
+      const bool ok = j0 < n16;
+      const int64_t jl = ok ? j0 : 0;
+      float4 dv[4], nv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        dv[u] = *reinterpret_cast<const float4*>(row + jl + 4 * u);
+        nv[u] = *reinterpret_cast<const float4*>(norms + jl + 4 * u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        take(key_of(dv[u].x, nv[u].x), j0 + 4 * u, ok);
+        take(key_of(dv[u].y, nv[u].y), j0 + 4 * u + 1, ok);
+        take(key_of(dv[u].z, nv[u].z), j0 + 4 * u + 2, ok);
+        take(key_of(dv[u].w, nv[u].w), j0 + 4 * u + 3, ok);
+      }
+    }
+    for (int64_t j0 = n16; j0 < n; j0 += kKnnBlock) {
+      const int64_t j = j0 + tid;
+      take(j < n ? key_at(j) : 0u, j, j < n);
+    }
+    over = cw > kKnnSeg;
+    if (lane == 0) seg_cnt[wv] = over ? -1 : cw;
+    __syncthreads();
+    int tot = 0;
+    bool bad = false;
+    for (int w = 0; w < kKnnBlock / 64; ++w) {
+      bad |= seg_cnt[w] < 0;
+      tot += seg_cnt[w] < 0 ? 0 : seg_cnt[w];
+    }
+    if (!bad && tot >= k) {
+      // candidate i (0 <= i < 16 * kKnnSeg) lives in segment i / kKnnSeg
+      auto cand = [&](int i) -> uint32_t {
+        const int w = i / kKnnSeg, o = i - w * kKnnSeg;
+        return o < seg_cnt[w] ? ckey[i] : 0u;  // key 0 sorts below every real key
+      };
+      uint32_t need_eq;
+      const uint32_t thr = knn_lds_kth(cand, 16 * kKnnSeg, (uint32_t)k, hist, sh2, &need_eq);
+      // keys >= thr: the n_gt keys above it plus every tie
+      if (tid == 0) sh_gt = 0;
+      __syncthreads();
+      for (int i0 = 0; i0 < 16 * kKnnSeg; i0 += kKnnBlock) {  // block-uniform: ballots below
+        const int i = i0 + tid, w = i / kKnnSeg, o = i - w * kKnnSeg;
+        const bool c = o < seg_cnt[w] && ckey[i] >= thr;
+        const unsigned long long mm = __ballot(c);
+        int base = 0;
+        if (lane == 0 && mm) base = atomicAdd(&sh_gt, __popcll(mm));
+        base = __shfl(base, 0, 64);
+        const int sl = base + __popcll(mm & ((1ull << lane) - 1ull));
+        if (c && sl < kKnnMaxK) {
+          skey[sl] = ckey[i];
+          sidx[sl] = cidx[i];
+        }
+      }
+      __syncthreads();
+      const int m = sh_gt;
+      if (m <= kKnnMaxK) {
+        int PC = 64;
+        while (PC < m) PC <<= 1;
+        for (int i = m + tid; i < PC; i += kKnnBlock) {
+          skey[i] = 0u;
+          sidx[i] = 0x7fffffff;
+        }
+        __syncthreads();
+        knn_bitonic(skey, sidx, PC);
+        for (int i = tid; i < k; i += kKnnBlock) {
+          out_w[b * k + i] = key2f(skey[i]);
+          out_n[b * k + i] = sidx[i];
+        }
+        return;  // block-uniform (m is a shared value read after a barrier)
+      }
+    }
+    __syncthreads();
+  }
 
   // ---- radix select of the k-th largest key: digits of 12, 12 and 8 bits
   uint32_t prefix = 0, need = (uint32_t)k;
@@ -197,27 +396,7 @@ __global__ __launch_bounds__(kKnnBlock) void knn_select_kernel(
     sidx[i] = 0x7fffffff;
   }
   __syncthreads();
-  for (int kk = 2; kk <= P; kk <<= 1) {
-    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-      for (int i = tid; i < P; i += kKnnBlock) {
-        const int l = i ^ jj;
-        if (l > i) {
-          const uint32_t ka = skey[i], kb = skey[l];
-          const int32_t ia = sidx[i], ib = sidx[l];
-          // "a before b" in the final order
-          const bool a_first = ka > kb || (ka == kb && ia < ib);
-          const bool up = (i & kk) == 0;
-          if (up ? !a_first : a_first) {
-            skey[i] = kb;
-            skey[l] = ka;
-            sidx[i] = ib;
-            sidx[l] = ia;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  knn_bitonic(skey, sidx, P);
   for (int i = tid; i < k; i += kKnnBlock) {
     out_w[b * k + i] = key2f(skey[i]);
     out_n[b * k + i] = sidx[i];
