@@ -72,8 +72,10 @@ def _as_csr(g):
     raise TypeError("graph must be a graph.CSRGraph (spotify_graph.SpotifyGraph.to_dgl_graph())")
 
 
-def _walk_device(g, nodeset, n_hops, alpha):
-    """int32 trace [n, n_hops] on the GPU; consumes RNG like the reference."""
+def _walk_device(g, nodeset, n_hops, alpha, philox=None):
+    """int32 trace [n, n_hops] on the GPU; consumes RNG like the reference.
+    philox=(seed, src_base): Philox mode with a given seed and absolute source
+    position of nodeset[0] (draws nothing from torch's generator)."""
     g = _as_csr(g)
     dev = nat.device()
     indptr, indices = g.device_csr(dev)
@@ -97,11 +99,14 @@ def _walk_device(g, nodeset, n_hops, alpha):
                                         int(n_hops), alpha32, mt.p, nat.ptr(ws), ws.numel(),
                                         nat.ptr(trace), nat.stream_ptr()), "walk")
     else:
-        with nat.torch_rng() as mt:
-            d = mt.draws(2)
-        seed = (int(d[0]) << 32) | int(d[1])
+        if philox is None:
+            with nat.torch_rng() as mt:
+                d = mt.draws(2)
+            seed, base = (int(d[0]) << 32) | int(d[1]), 0
+        else:
+            seed, base = philox
         nat.check(L.pinsage_walk_philox(nat.ptr(indptr), nat.ptr(indices), n_all, nat.ptr(src), n,
-                                        int(n_hops), alpha32, seed, 0, 0, nat.ptr(trace),
+                                        int(n_hops), alpha32, seed, 0, int(base), nat.ptr(trace),
                                         nat.stream_ptr()), "walk")
     return src, trace
 
@@ -151,28 +156,83 @@ def sample_neighborhood_topt(g, n_items, nodeset, n_hops, alpha, T):
     return torch.return_types.topk((w.to(out_dev), nb.to(out_dev)))
 
 
+def _shard():
+    """(rank, world) of an initialised torch.distributed job (precompute is
+    sharded by source over its ranks), else (0, 1).  PINSAGE_SHARD_PRECOMPUTE=0
+    makes every rank compute the whole table."""
+    d = torch.distributed
+    if (os.environ.get("PINSAGE_SHARD_PRECOMPUTE", "1") != "0" and d.is_available()
+            and d.is_initialized() and d.get_world_size() > 1):
+        return d.get_rank(), d.get_world_size()
+    return 0, 1
+
+
+def _set_stream_position(st0, draws):
+    """torch's CPU generator = state st0 advanced by `draws` MT19937 words
+    (exact GF(2) jump-ahead for long skips)."""
+    mt = nat.MT.from_state(st0)
+    mt.skip(int(draws))
+    mt.to_torch()
+
+
 def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
     """Top-T PPR neighbourhoods of all items, cached at ``path`` as
-    ``(weights f64 [n,T], nodes i64 [n,T])`` (pinsage_model.py:109-132)."""
+    ``(weights f64 [n,T], nodes i64 [n,T])`` (pinsage_model.py:109-132).
+
+    Sources are independent, so under torch.distributed the chunks of sources
+    are dealt over the ranks and the table is summed across
+    them (every row comes from exactly one rank).  The RNG stream stays the
+    single-process one: in MT19937 mode source s draws words
+    [3*n_hops*s, 3*n_hops*(s+1)) of the reference's source-major stream, so a
+    rank jumps its generator to its chunk's start; in Philox mode one seed
+    (two words) serves the whole table and each draw is keyed by the source's
+    absolute position.  Afterwards every rank's generator is where the
+    single-process run leaves it, and the table is bitwise the same."""
     if path and os.path.isfile(path):
         a, b = torch.load(path, weights_only=True)
         if b.shape[0] == n_items and b.shape[1] == T:
             return (a, b)
     t0 = time.time()
     dev = nat.device()
-    all_w = torch.empty((n_items, T), dtype=torch.float64)
-    all_nb = torch.empty((n_items, T), dtype=torch.int64)
-    # sources in order, as the reference's 256-source batches consume the stream
+    rank, world = _shard()
+    all_w = torch.zeros((n_items, T), dtype=torch.float64)
+    all_nb = torch.zeros((n_items, T), dtype=torch.int64)
+    st0 = torch.get_rng_state().numpy().copy()
+    mt_mode = _RNG_MODE == "mt19937"
+    philox = None
+    if not mt_mode:
+        with nat.torch_rng() as mt:
+            d = mt.draws(2)
+        philox = (int(d[0]) << 32) | int(d[1])
+    # sources in order; each chunk's draws are positioned absolutely, so the
+    # chunking (and the rank that runs a chunk) does not change the result
     chunk = 1 << 18
-    for i in range(0, n_items, chunk):
+    if world > 1:
+        chunk = min(chunk, max(1, -(-n_items // world)))
+    starts = list(range(0, n_items, chunk))
+    for ci, i in enumerate(starts):
+        if ci % world != rank:
+            continue
+        if mt_mode:
+            _set_stream_position(st0, 3 * int(n_hops) * i)
         ids = torch.arange(i, min(i + chunk, n_items), dtype=torch.int64, device=dev)
-        src, trace = _walk_device(g, ids, n_hops, alpha)
+        src, trace = _walk_device(g, ids, n_hops, alpha, None if mt_mode else (philox, i))
         w, nb, _, _ = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T))
         all_w[i:i + ids.shape[0]] = w.cpu()
         all_nb[i:i + ids.shape[0]] = nb.cpu()
         print(f"{min(i + chunk, n_items)}/{n_items} done.")
+    if mt_mode:
+        _set_stream_position(st0, 3 * int(n_hops) * n_items)
+    if world > 1:
+        d = torch.distributed
+        on_dev = d.get_backend() == "nccl"
+        for t in (all_w, all_nb):
+            x = t.to(dev) if on_dev else t
+            d.all_reduce(x)
+            if on_dev:
+                t.copy_(x.cpu())
     print(f"{time.time() - t0}s elapsed.")
-    if path:
+    if path and rank == 0:
         torch.save((all_w, all_nb), path)
     return (all_w, all_nb)
 

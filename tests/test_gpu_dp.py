@@ -136,3 +136,54 @@ def test_dp_two_ranks_match_oracle_dp():
         diff = np.abs(v.astype(np.float64) - rv)
         assert (diff <= 2 * lr * STEPS + 1e-6).all(), k
         assert np.linalg.norm(diff) <= 1e-4 * np.linalg.norm(rv), k
+
+
+def _precompute_worker(rank, world, port, tmp, mode, out_q):
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    import pinsage_model as pm
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g, _, _ = _problem(tmp)
+        pm.set_rng_mode(mode)
+        torch.manual_seed(0)
+        w, nb = pm.precompute_neighborhoods_topt(g, N_TRACKS, 200, 0.85, 20, None)
+        out_q.put((rank, w.numpy(), nb.numpy(), torch.get_rng_state().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["mt19937", "philox"])
+def test_precompute_sharded_over_ranks_matches_single_process(mode):
+    """the precompute is dealt over the ranks by source chunk and
+    summed; table and the generator state afterwards are bitwise those of one
+    process computing everything (MT19937: exact jump-ahead to each chunk)."""
+    import pinsage_model as pm
+    tmp = tempfile.mkdtemp()
+    g, _, _ = _problem(tmp)
+    pm.set_rng_mode(mode)
+    try:
+        torch.manual_seed(0)
+        w1, nb1 = pm.precompute_neighborhoods_topt(g, N_TRACKS, 200, 0.85, 20, None)
+        st1 = torch.get_rng_state().numpy()
+    finally:
+        pm.set_rng_mode("mt19937")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_precompute_worker, args=(r, 3, port, tmp, mode, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for _, w, nb, st in res:
+        assert np.array_equal(w, w1.numpy()) and np.array_equal(nb, nb1.numpy())
+        assert np.array_equal(st, st1)
