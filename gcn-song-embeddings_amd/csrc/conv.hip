@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int h4 = hid >> 2;
   // neighbour rows whose loads are in flight together (16 x 2 float4 spill)
-  constexpr int U = VEC == 1 ? 16 : 8;
+  constexpr int U = VEC == 1 ? 16 : 10;  // 10: a fanout-10 row in one round
   // work item = (row, 64*VEC-float4 column chunk): hid 512 at VEC 1 gives two
   // waves per row, each with all of a T <= 16 row's loads in one round
   const int nch = (h4 + 64 * VEC - 1) / (64 * VEC);
