@@ -348,7 +348,7 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
                     int epi, int splits, int cfg, int stream_k, void* stream) {
   if (M < 0 || N <= 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX ||
       (epi != kEpiStore && epi != kEpiAccum && epi != kEpiPartial) || splits < 1 || cfg < -1 ||
-      cfg > 3) {
+      cfg > 4) {
     set_error("gemm_ex: bad argument");
     return kErrArg;
   }

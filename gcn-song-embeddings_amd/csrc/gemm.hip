@@ -27,6 +27,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kLdsBudget = 81920;  // bytes per workgroup: two workgroups per CU
 constexpr int kLdsBudget3 = 54272;  // three workgroups per CU (cfg 3)
+constexpr int kLdsBudget4 = 40960;  // four workgroups per CU (cfg 4)
 constexpr int kIdxWin = 1024;  // gathered k-rows staged in LDS at a time
 
 // One 16-B LDS-DMA per lane (global_load_lds_dwordx4; LDS destination = M0 +
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   // ring depth: as many stage buffers as fit two workgroups per CU (3 or 4);
   // the k-row windows exist only for MN-major (possibly gathered) operands
   constexpr int IDXF = (GA ? kIdxWin : 0) + (GB ? kIdxWin : 0);
-  constexpr int NSA = ((WPC == 2 ? kLdsBudget : kLdsBudget3) / 4 - IDXF) / SZS;
+  constexpr int NSA = ((WPC == 2 ? kLdsBudget : WPC == 3 ? kLdsBudget3 : kLdsBudget4) / 4 - IDXF) / SZS;
   constexpr int NS = NSA > NSMAX ? NSMAX : NSA;
   static_assert(NS >= 3, "stage buffers do not fit");
   __shared__ __attribute__((aligned(16))) float smem[NS * SZS + IDXF];
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   }
 }
 
-constexpr int kCfgBM[4] = {128, 64, 32, 64};
+constexpr int kCfgBM[5] = {128, 64, 32, 64, 64};
 
 int gemm_slots() {
   static const int slots = [] {
@@ -626,6 +627,10 @@ static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 32>), g, dim3(256), 0, st, p);
   else if (cfg == 2)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32>), g, dim3(256), 0, st, p);
+  else if (cfg == 3)
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3>), g, dim3(256), 0, st, p);
+  else if constexpr (AK && BKM)  // four per CU: K-major operands only (no k-row windows)
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 3, 4>), g, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3>), g, dim3(256), 0, st, p);
 }
