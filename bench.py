@@ -1,6 +1,7 @@
 """PinSAGE train-step throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--scaling weak|strong]
+                    [--no-cpu-baseline]
 
 A step = sample_batch (reference RNG semantics, host) + PinSage.train_batch
 (fused HIP forward of the query/positive/negative ids, loss, backward, Adam)
@@ -35,8 +36,10 @@ CONFIGS = {
                d_in=512, n_layers=2, T=25, batch=2048),
     "c4": dict(workload="synthetic 10M nodes / 100M edges, 128-d features, 2-layer, per-GPU batch 512",
                n_tracks=8_000_000, n_cols=2_000_000, memberships=50_000_000, d_in=128, n_layers=2,
-               T=10, batch=512),
+               T=10, batch=512, global_batch=4096),
 }
+# --scaling strong: the global batch stays fixed (C4 B_global 4096, per-GPU
+# 4096/g); configs without a global_batch keep their batch as the global one
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
@@ -132,13 +135,41 @@ def pmc_traffic(config, site):
     return None, None, None
 
 
+def host_cores():
+    """(threads to use, facts): the host's physical cores (lscpu), capped by what
+    this process may run on (affinity, cgroup CPU quota -- a GPU box grants one
+    job a share of a large host)."""
+    import subprocess
+    facts = {}
+    try:
+        out = subprocess.run(["lscpu", "-p=Core,Socket"], capture_output=True, text=True, timeout=10).stdout
+        facts["physical_cores"] = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")})
+    except Exception:
+        pass
+    facts["affinity_cpus"] = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            facts["cgroup_cpu_quota"] = int(q) / int(per)
+    except Exception:
+        pass
+    cands = [facts.get("physical_cores"), facts["affinity_cpus"], facts.get("cgroup_cpu_quota")]
+    threads = max(1, int(min(c for c in cands if c)))
+    return threads, facts
+
+
 def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
     """The oracle's restatement of the reference train step (dense clone
-    put_embeddings, f64 aggregation, torch CPU) on the same workload."""
+    put_embeddings, f64 aggregation, torch CPU) on the same workload, on all the
+    physical cores this job may use."""
     from oracle import oracle as orc
     import pinsage_model as pm
-    threads = min(16, os.cpu_count() or 1)
+    threads, facts = host_cores()
     torch.set_num_threads(threads)
+    # the restatement's backward at the reference init makes denormals the reference's op
+    # order does not (its step time grew 1.6 -> 8 s); flushed so it times the algorithm
+    # (tools/refcpu_ratio.py: refcpu / reference time ratio with the same setting)
+    torch.set_flush_denormal(True)
     torch.manual_seed(1)
     dims = (cfg["d_in"], 512, 128)
     tmp = {}
@@ -162,10 +193,16 @@ def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
         tr.step(b)
         times.append(time.time() - t0)
     t_step = float(np.median(times[1:] if len(times) > 2 else times))
+    torch.set_flush_denormal(False)
+    ratio = None
+    rp = os.path.join(REPO, "profiles", "r02", "refcpu_ratio.json")
+    if os.path.isfile(rp):
+        ratio = json.load(open(rp)).get("refcpu_over_reference")
     return dict(value=3 * cfg["batch"] / t_step, unit="target nodes/s", cores=threads, kind="port",
                 sample=f"{len(times)} train steps (median) of the oracle's reference restatement "
                        f"(torch CPU, {threads} threads) on the same synthetic graph and config",
-                ms_per_step=t_step * 1e3)
+                ms_per_step=t_step * 1e3, host=facts, refcpu_over_reference=ratio,
+                refcpu_over_reference_source="profiles/r02/refcpu_ratio.json (dev container, 8 threads)")
 
 
 def main():
@@ -176,9 +213,16 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precompute-rng", default="philox", choices=["philox", "mt19937"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: per-GPU batch fixed; strong: global batch fixed (per-GPU = global / N)")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
     rank, world = setup_dist(args.gpus)
+    if args.scaling == "strong":
+        gb = cfg.get("global_batch", cfg["batch"])
+        if gb % world:
+            raise SystemExit(f"--scaling strong: global batch {gb} not divisible by {world} ranks")
+        cfg["batch"] = gb // world
 
     import pinsage_training as pt
     import _native as nat
@@ -289,7 +333,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded playlist graph, N(0,1) features, co-membership positives)",

@@ -35,7 +35,8 @@ class EngineOffsets(ctypes.Structure):
     _fields_ = [("ids", i64), ("pos_rank", i64), ("z", i64), ("dz", i64), ("scalars", i64),
                 ("n_layers", i64), ("count_S", i64 * 8), ("count_N", i64 * 8),
                 ("members_S", i64 * 8), ("members_N", i64 * 8), ("cap_S", i64 * 8),
-                ("cap_N", i64 * 8), ("y", i64 * 8), ("param_offsets", i64 * 8)]
+                ("cap_N", i64 * 8), ("y", i64 * 8), ("param_offsets", i64 * 8),
+                ("hinge", i64)]
 
 
 # name -> (restype, argtypes)

@@ -620,16 +620,27 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
     const float* __restrict__ Z, int d, const int32_t* __restrict__ pos_rank, int B, float margin,
     const float* __restrict__ feats, int64_t ld_f, int d_in, const int64_t* __restrict__ batch,
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ part,
-    float* __restrict__ colpart) {
+    float* __restrict__ colpart, float* __restrict__ hinge) {
   __shared__ float red[4][4];  // per wave: loss, nfl, sum||h_q||^2, unused
-  // per-block column sums of the query rows (variance monitor), d <= 512
+  // per-block column sum and sum of squared deviations from the block's own
+  // column mean over its (<= 4) query rows (variance monitor, merged by Chan's
+  // formula in loss_finish_kernel: no cancellation when the rows collapse)
   {
     const int b0 = blockIdx.x * 4;
+    const int nb = min(4, B - b0);
     for (int c = threadIdx.x; c < d; c += blockDim.x) {
+      float x[4];
       float s = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        x[k] = k < nb ? Z[(int64_t)pos_rank[3 * (b0 + k)] * d + c] : 0.f;
+        s += x[k];
+      }
+      const float mb = s / (float)nb;
+      float m2 = 0.f;
       for (int k = 0; k < 4; ++k)
-        if (b0 + k < B) s += Z[(int64_t)pos_rank[3 * (b0 + k)] * d + c];
-      colpart[(int64_t)blockIdx.x * d + c] = s;
+        if (k < nb) m2 += (x[k] - mb) * (x[k] - mb);
+      colpart[(int64_t)blockIdx.x * 2 * d + c] = s;
+      colpart[(int64_t)blockIdx.x * 2 * d + d + c] = m2;
     }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -657,6 +668,7 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
                 nn = fmaxf(sqrtf(dn_), 1e-12f);
     const float cqp = qp / (nq * np), cqn = qn / (nq * nn);
     const float ds = cqn - cqp + margin;
+    if (hinge && lane == 0) hinge[b] = ds;  // the hinge argument (parity tests read it)
     lossv = ds >= 0.f ? ds : 0.f;
     const float g = ds >= 0.f ? 1.f / (float)B : 0.f;
     if (g != 0.f) {
@@ -729,7 +741,8 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
 // backward kernel).  Block 0 also reduces, in a fixed order, the per-block loss
 // partials into scal[0] = loss, scal[1] = node-feature loss, and the variance
 // monitor (pinsage_training.py:99-103): sum((h - mean)^2)/(B-1) over the B query
-// rows = (sum |h|^2 - B |mean|^2)/(B-1), from per-block column sums.
+// rows, merged from the per-block (sum, M2) column partials by Chan's formula
+// M2 = sum_g M2_g + n_g (mean_g - mean)^2 (deviations, never |h|^2 - |mean|^2).
 __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G,
                                                            const int* __restrict__ Kc, int64_t S_max,
                                                            const int* __restrict__ nS, int d,
@@ -764,13 +777,14 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
   }
   // column sums of the query rows: thread (grp, c) sums parts grp, grp+ng, ...
   const int ng = 1024 / d, c = t % d, grp = t / d;
+  const int64_t ld2 = 2 * (int64_t)d;
   float cv = 0.f;
   if (grp < ng) {
     int g = grp;
     for (; g + 3 * ng < nparts; g += 4 * ng)
-      cv += (colpart[(int64_t)g * d + c] + colpart[(int64_t)(g + ng) * d + c]) +
-            (colpart[(int64_t)(g + 2 * ng) * d + c] + colpart[(int64_t)(g + 3 * ng) * d + c]);
-    for (; g < nparts; g += ng) cv += colpart[(int64_t)g * d + c];
+      cv += (colpart[g * ld2 + c] + colpart[(g + ng) * ld2 + c]) +
+            (colpart[(g + 2 * ng) * ld2 + c] + colpart[(g + 3 * ng) * ld2 + c]);
+    for (; g < nparts; g += ng) cv += colpart[g * ld2 + c];
   }
   cs[t] = cv;
   l = wave_sum(l);
@@ -782,16 +796,25 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
     wred[wv][2] = sq;
   }
   __syncthreads();
-  float msq = 0.f;
+  __shared__ float mean_s[1024];
   if (t < d) {
     float tot = 0.f;
     for (int q = 0; q < ng; ++q) tot += cs[q * d + t];
-    const float m = tot / (float)B;
-    msq = m * m;
+    mean_s[t] = tot / (float)B;
   }
-  msq = wave_sum(msq);
   __syncthreads();
-  if (lane == 0) cs[wv] = msq;
+  // second pass: Chan's merge of the block partials around the batch mean
+  float m2 = 0.f;
+  if (grp < ng) {
+    const float m = mean_s[c];
+    for (int g = grp; g < nparts; g += ng) {
+      const int n_g = min(4, B - 4 * g);
+      const float dm = colpart[g * ld2 + c] / (float)n_g - m;
+      m2 += colpart[g * ld2 + d + c] + (float)n_g * dm * dm;
+    }
+  }
+  m2 = wave_sum(m2);
+  if (lane == 0) cs[wv] = m2;
   __syncthreads();
   if (t == 0) {
     float lsum = 0.f, nfs = 0.f, sqs = 0.f, ms = 0.f;
@@ -804,7 +827,7 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
     scal[0] = lsum / (float)B;
     scal[1] = nfs / (float)B;
     scal[2] = sqs;
-    scal[3] = (sqs - (float)B * ms) / (float)(B - 1);
+    scal[3] = ms / (float)(B - 1);
   }
 }
 
@@ -1127,12 +1150,12 @@ int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int
 int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float margin,
                 const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
                 int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
-                hipStream_t st) {
+                float* hinge, hipStream_t st) {
   // G and Kc are zero on entry (init_workspace; then loss_finish / the first
   // backward kernel leave them zero)
   const int nblk = ceil_div(B, 4);
   hipLaunchKernelGGL(loss_triple_kernel, dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, margin,
-                     feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart);
+                     feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge);
   PS_CHECK_LAUNCH();
   PS_REQUIRE(d <= 1024, kErrArg, "loss: out_dim must be <= 1024");
   hipLaunchKernelGGL(loss_finish_kernel, dim3(grid_for(S_max * d, 1024, 256)), dim3(1024), 0, st, G,

@@ -52,7 +52,7 @@ int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const i
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
-                hipStream_t);
+                float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
                 hipStream_t);
 int csr_prepare();
@@ -132,7 +132,7 @@ struct Engine {
   // workspace layout
   size_t bits_begin = 0, bits_end = 0;  // all bitmaps contiguous (one memset)
   size_t block_sums = 0, ids = 0, pos_rank = 0, H1 = 0, Z = 0, dZ = 0, dP1 = 0;
-  size_t G = 0, Kc = 0, part = 0, scal = 0, slab = 0, bslab = 0, varpart = 0;
+  size_t G = 0, Kc = 0, part = 0, scal = 0, slab = 0, bslab = 0, varpart = 0, hinge = 0;
   size_t slab_main = 0, bslab_main = 0;  // split-K slabs of the main stream's weight gradient
   int64_t slab_floats = 0;
   // stream-K scratch of the main stream's GEMMs (gemm.h)
@@ -318,7 +318,8 @@ static void layout(Engine& E) {
   E.G = carve(cur, 3 * top * c.out * 4);
   E.Kc = carve(cur, 3 * top * 4);
   E.part = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * 4 * 4);
-  E.varpart = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * c.out * 4);
+  E.varpart = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * 2 * c.out * 4);  // (sum, M2)
+  E.hinge = carve(cur, (c.max_pos / 3 + 1) * 4);  // per-triple hinge argument of the last loss
   E.scal = carve(cur, 64);
   // split-K slabs: any split count up to kMaxSplits (it is chosen from size hints)
   int64_t slab = kMaxSplits * c.out * c.out;
@@ -953,6 +954,7 @@ int pinsage_engine_offsets(const pinsage_engine* e, pinsage_engine_offsets_t* o)
   o->z = (int64_t)E->Z;
   o->dz = (int64_t)E->dZ;
   o->scalars = (int64_t)E->scal;
+  o->hinge = (int64_t)E->hinge;
   o->n_layers = E->cfg.n_layers;
   for (int64_t l = 0; l < E->cfg.n_layers && l < 8; ++l) {
     o->count_S[l] = (int64_t)E->L[(size_t)l].S.count;
@@ -1085,7 +1087,8 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
                      margin, with_monitors ? E->feats : nullptr, E->ld_f, (int)c.d_in,
                      at<int64_t>(ws, E->ids), at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap,
                      at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
-                     at<float>(ws, E->varpart), at<float>(ws, E->scal), (hipStream_t)stream);
+                     at<float>(ws, E->varpart), at<float>(ws, E->scal), at<float>(ws, E->hinge),
+                     (hipStream_t)stream);
 }
 
 int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,

@@ -175,16 +175,42 @@ def _set_stream_position(st0, draws):
     mt.to_torch()
 
 
+def _shard_range(n_items, rank, world):
+    """Equal contiguous source shard of a rank: [rank*per, min((rank+1)*per, n))."""
+    per = -(-n_items // world) if n_items else 0
+    lo = min(rank * per, n_items)
+    return lo, min(lo + per, n_items), per
+
+
+def _gather_shards(w_sh, nb_sh, n_items, per, dev):
+    """All-gather of the equal-sized (zero-padded) shards: ONE collective per
+    table instead of reducing full-size tables."""
+    d = torch.distributed
+    world = d.get_world_size()
+    out = []
+    for t in (w_sh, nb_sh):
+        if d.get_backend() == "nccl":  # RCCL over xGMI: device buffers
+            x = t.to(dev)
+            full = torch.empty((world * per,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+            d.all_gather_into_tensor(full, x)
+            out.append(full[:n_items].cpu())
+        else:
+            parts = [torch.empty_like(t) for _ in range(world)]
+            d.all_gather(parts, t)
+            out.append(torch.cat(parts, 0)[:n_items].contiguous())
+    return out[0], out[1]
+
+
 def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
     """Top-T PPR neighbourhoods of all items, cached at ``path`` as
     ``(weights f64 [n,T], nodes i64 [n,T])`` (pinsage_model.py:109-132).
 
-    Sources are independent, so under torch.distributed the chunks of sources
-    are dealt over the ranks and the table is summed across
-    them (every row comes from exactly one rank).  The RNG stream stays the
+    Sources are independent, so under torch.distributed each rank walks an
+    equal contiguous shard of the sources and the shards are exchanged with
+    one all-gather per table.  The RNG stream stays the
     single-process one: in MT19937 mode source s draws words
     [3*n_hops*s, 3*n_hops*(s+1)) of the reference's source-major stream, so a
-    rank jumps its generator to its chunk's start; in Philox mode one seed
+    rank jumps its generator to its shard's start; in Philox mode one seed
     (two words) serves the whole table and each draw is keyed by the source's
     absolute position.  Afterwards every rank's generator is where the
     single-process run leaves it, and the table is bitwise the same."""
@@ -195,8 +221,10 @@ def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
     t0 = time.time()
     dev = nat.device()
     rank, world = _shard()
-    all_w = torch.zeros((n_items, T), dtype=torch.float64)
-    all_nb = torch.zeros((n_items, T), dtype=torch.int64)
+    lo, hi, per = _shard_range(n_items, rank, world)
+    rows = per if world > 1 else n_items
+    sh_w = torch.zeros((rows, T), dtype=torch.float64)
+    sh_nb = torch.zeros((rows, T), dtype=torch.int64)
     st0 = torch.get_rng_state().numpy().copy()
     mt_mode = _RNG_MODE == "mt19937"
     philox = None
@@ -207,30 +235,21 @@ def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
     # sources in order; each chunk's draws are positioned absolutely, so the
     # chunking (and the rank that runs a chunk) does not change the result
     chunk = 1 << 18
-    if world > 1:
-        chunk = min(chunk, max(1, -(-n_items // world)))
-    starts = list(range(0, n_items, chunk))
-    for ci, i in enumerate(starts):
-        if ci % world != rank:
-            continue
+    for i in range(lo, hi, chunk):
         if mt_mode:
             _set_stream_position(st0, 3 * int(n_hops) * i)
-        ids = torch.arange(i, min(i + chunk, n_items), dtype=torch.int64, device=dev)
+        ids = torch.arange(i, min(i + chunk, hi), dtype=torch.int64, device=dev)
         src, trace = _walk_device(g, ids, n_hops, alpha, None if mt_mode else (philox, i))
         w, nb, _, _ = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T))
-        all_w[i:i + ids.shape[0]] = w.cpu()
-        all_nb[i:i + ids.shape[0]] = nb.cpu()
-        print(f"{min(i + chunk, n_items)}/{n_items} done.")
+        sh_w[i - lo:i - lo + ids.shape[0]] = w.cpu()
+        sh_nb[i - lo:i - lo + ids.shape[0]] = nb.cpu()
+        print(f"{min(i + chunk, hi)}/{n_items} done.")
     if mt_mode:
         _set_stream_position(st0, 3 * int(n_hops) * n_items)
     if world > 1:
-        d = torch.distributed
-        on_dev = d.get_backend() == "nccl"
-        for t in (all_w, all_nb):
-            x = t.to(dev) if on_dev else t
-            d.all_reduce(x)
-            if on_dev:
-                t.copy_(x.cpu())
+        all_w, all_nb = _gather_shards(sh_w, sh_nb, n_items, per, dev)
+    else:
+        all_w, all_nb = sh_w, sh_nb
     print(f"{time.time() - t0}s elapsed.")
     if path and rank == 0:
         torch.save((all_w, all_nb), path)
@@ -569,9 +588,10 @@ class _EngineRunner:
         n = int(ids.shape[0])
         if n == 0:
             return torch.empty((0, m.out_dim), device=out_dev)
-        if int(ids.min()) < 0 or int(ids.max()) >= feats.shape[0]:
-            # the reference's features[nodeset] raises the same way
-            raise IndexError(f"node ids out of range for {feats.shape[0]} items")
+        n_valid = min(int(feats.shape[0]), int(m.n_items))
+        if int(ids.min()) < 0 or int(ids.max()) >= n_valid:
+            # the reference's features[nodeset] / all_w[nodeset] raise the same way
+            raise IndexError(f"node ids out of range for {n_valid} items")
         self.pack()
         self.ensure_engine(n)
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.params())

@@ -263,6 +263,7 @@ class _FusedStep:
         self.B = 0
         self.wss = None
         self.ws = None
+        self.eng = None  # the engine the workspaces and staged views belong to
         self.m = self.v = None
         self.grads = None
         self._tuned = False
@@ -288,8 +289,13 @@ class _FusedStep:
             self.m = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
             self.v = torch.zeros(n_params, dtype=torch.float32, device=self.dev)
             self.adopt_optimizer_state()
-        if self.wss is None or r.engine is None or r.engine.cfg.max_pos < 3 * B:
+        # a forward over more ids (embed(), evaluation) may have replaced the
+        # runner's engine: workspaces, staged views and graphs of the old one
+        # are then stale and are rebuilt for the new one
+        if (self.wss is None or r.engine is None or r.engine is not self.eng
+                or r.engine.cfg.max_pos < 3 * B):
             r.ensure_engine(3 * B)
+            self.eng = r.engine
             self.wss = [r.engine.new_workspace(self.dev) for _ in range(2)]
             self.B = B
             off = r.engine.off

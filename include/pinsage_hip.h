@@ -225,6 +225,7 @@ typedef struct {
   int64_t ids, pos_rank, z, dz, scalars, n_layers;
   int64_t count_S[8], count_N[8], members_S[8], members_N[8], cap_S[8], cap_N[8], y[8];
   int64_t param_offsets[8];
+  int64_t hinge; /* f32 [batch]: cos(q,n) - cos(q,p) + margin of each triple of the last loss */
 } pinsage_engine_offsets_t;
 
 int pinsage_engine_create(const pinsage_engine_config* cfg, pinsage_engine** out);

@@ -1,0 +1,190 @@
+"""Train-step parity helpers shared by the GPU tests.
+
+The reference's hinge (``max_margin_loss``, pinsage_training.py:31-41, margin
+1e-5 at :149) is evaluated on nearly collapsed embeddings at initialisation:
+the argument ``cos(q,n) - cos(q,p) + margin`` of many triples is within fp32
+rounding of 0, so a triple can be active on one side and not on the other,
+and the loss gradient (a difference of nearly equal unit vectors) amplifies
+rounding-level forward differences.  The step is therefore pinned in parts,
+each one well conditioned:
+
+1. forward rows the loss read (the engine's Z) vs the oracle's outputs,
+   row-norm relative;
+2. hinge arguments: the engine's per-triple value (written by its loss kernel)
+   vs the oracle's; a triple whose activity differs must have |arg| <= 1e-6;
+3. loss within 1e-4 relative;
+4. (A) the oracle's gradient over the GPU's active set, with the oracle's own
+   forward, vs the GPU's gradients;
+5. (B) the oracle's backward driven by the cotangent of the GPU's own outputs
+   (the loss derivative evaluated on Z in f64, GPU active set) vs the GPU's
+   gradients -- the kernels' backward measured with the conditioning removed.
+
+Tolerances are stated per call (north star: 1e-4 relative on fp32).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from conftest import PKG, REPO
+
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def make_trainer(g, n, feats, pos, L, T, B, margin, seed=0, spread=False):
+    """PinSage with the reference's defaults except the BASELINE config's
+    (n_layers, T, batch); the model is rebuilt after construction because the
+    reference binds hyperparameters at construction (pinsage_training.py:139-148)."""
+    import pinsage_model as pm
+    import pinsage_training as pt
+    torch.manual_seed(seed)
+    tr = pt.PinSage(g, n, feats, pos, log=False, load_save=False)
+    tr.T, tr.n_layers = T, L
+    torch.manual_seed(seed + 1)
+    tr.model = pm.PinSageModel(g, tr.n, L, tr.dimensions, tr.n_hops, tr.alpha, T, tr.nbhds)
+    if spread:
+        with torch.no_grad():
+            for k, prm in tr.model.named_parameters():
+                prm.zero_() if k.endswith("bias") else prm.mul_(3.0)
+    tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+    tr.scheduler = torch.optim.lr_scheduler.ExponentialLR(tr.optimizer, tr.decay)
+    tr.batch_size = B
+    tr.margin = margin
+    return tr
+
+
+def step_outputs(tr, B):
+    """(Z [B, 3, out] f64, hinge [B] f64) of the last train_batch: the model
+    rows its loss kernel read and that kernel's per-triple hinge argument."""
+    import _native as nat
+    fs = tr._fused
+    e = fs.runner.engine
+    ws = fs.ws
+    out_dim = int(e.cfg.out)
+    z = torch.empty((3 * B, out_dim), dtype=torch.float32, device=ws.device)
+    nat.check(nat.lib().pinsage_engine_gather_output(e.h, nat.ptr(ws), 3 * B, nat.ptr(z),
+                                                     nat.stream_ptr()), "gather")
+    hinge = e.view(ws, int(e.off.hinge), torch.float32, B)
+    torch.cuda.synchronize()
+    return (z.view(B, 3, out_dim).cpu().double().numpy(), hinge.cpu().double().numpy())
+
+
+def _hinge_args(hq, hp, hn, margin):
+    hq, hp, hn = (F.normalize(x, dim=1) for x in (hq, hp, hn))
+    return (hq * hn).sum(1) - (hq * hp).sum(1) + margin
+
+
+def capture_step(tr, batch, run=None):
+    """Run tr.train_batch(batch) (or run(batch)); return what the oracle needs
+    to pin it: the parameters before the step, the batch, the GPU's gradients,
+    loss, output rows (Z) and hinge arguments, and the step's return value."""
+    b = np.asarray(batch.numpy() if torch.is_tensor(batch) else batch)
+    init = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()}
+    out = (run or tr.train_batch)(torch.from_numpy(b))
+    loss = out[0]
+    grads = {k: p.grad.detach().cpu().numpy().astype(np.float64) for k, p in tr.model.named_parameters()}
+    Z, hinge = step_outputs(tr, b.shape[0])
+    return dict(init=init, batch=b, grads=grads, loss=float(loss), Z=Z, hinge=hinge,
+                L=tr.n_layers, T=tr.T, margin=float(tr.margin), out_dim=tr.out_dim, out=out)
+
+
+def check_train_step(tr, feats, w, nb, batch, tol=1e-4, kink=1e-6, strict_a=True, report=None):
+    """Run tr.train_batch(batch) and pin it against the oracle in the five parts
+    above.  Returns a dict of the measured errors (also appended to `report`)."""
+    return check_record(capture_step(tr, batch), feats, w, nb, tol=tol, kink=kink, strict_a=strict_a,
+                        report=report)
+
+
+def check_record(rec, feats, w, nb, tol=1e-4, kink=1e-6, strict_a=True, report=None):
+    from oracle import oracle as orc
+    L, T, margin, out_dim = rec["L"], rec["T"], rec["margin"], rec["out_dim"]
+    init, b, gpu_grads, loss, Z, hinge = (rec[k] for k in ("init", "batch", "grads", "loss", "Z", "hinge"))
+    B = b.shape[0]
+    feats_cpu = feats.detach().cpu()
+    wn, nbn = np.asarray(w), np.asarray(nb)
+    p = {k: v.float().requires_grad_() for k, v in init.items()}
+    hs = [orc.model_forward(p, feats_cpu, b[:, c], L, T, wn, nbn, out_dim) for c in range(3)]
+    res = {}
+    # 1. forward rows, row-norm relative
+    ref_rows = np.stack([h.detach().double().numpy() for h in hs], 1)  # [B, 3, out]
+    row_err = np.linalg.norm(Z - ref_rows, axis=2) / np.maximum(np.linalg.norm(ref_rows, axis=2), 1e-30)
+    res["fwd_row_rel_max"] = float(row_err.max())
+    # 2. hinge arguments and activity
+    args_ref = _hinge_args(*(torch.from_numpy(ref_rows[:, c]) for c in range(3)), margin).numpy()
+    act_gpu, act_ref = hinge >= 0, args_ref >= 0
+    flip = act_gpu != act_ref
+    res["hinge_abs_max"] = float(np.abs(hinge - args_ref).max())
+    res["hinge_flips"] = int(flip.sum())
+    res["hinge_flip_arg_max"] = float(np.abs(args_ref[flip]).max()) if flip.any() else 0.0
+    res["active"] = int(act_gpu.sum())
+    # 3. loss
+    ref_loss = float(np.clip(args_ref, 0, None).mean())
+    res["loss_gpu"], res["loss_ref"] = loss, ref_loss
+    res["loss_rel"] = abs(loss - ref_loss) / max(abs(ref_loss), 1e-30)
+    # 4. (A) oracle forward, GPU active set
+    mask = torch.from_numpy(act_gpu.astype(np.float32))
+    lossA = (mask * _hinge_args(hs[0], hs[1], hs[2], margin)).sum() / B
+    gA = torch.autograd.grad(lossA, [p[k] for k in init], retain_graph=True, allow_unused=True)
+    # 5. (B) cotangent of the GPU's own outputs (f64), GPU active set
+    zt = torch.from_numpy(Z.copy()).requires_grad_()
+    lz = (mask.double() * _hinge_args(zt[:, 0], zt[:, 1], zt[:, 2], margin)).sum() / B
+    (dz,) = torch.autograd.grad(lz, [zt])
+    dz = dz.float()
+    lossB = sum((hs[c] * dz[:, c]).sum() for c in range(3))
+    gB = torch.autograd.grad(lossB, [p[k] for k in init], allow_unused=True)
+    errA, errB = {}, {}
+    for (k, ga), gb in zip(zip(init, gA), gB):
+        if k not in gpu_grads:
+            continue
+        ga = np.zeros(init[k].shape) if ga is None else ga.double().numpy()
+        gb = np.zeros(init[k].shape) if gb is None else gb.double().numpy()
+        errA[k] = rel(gpu_grads[k], ga) if np.linalg.norm(ga) > 0 else float(np.linalg.norm(gpu_grads[k]))
+        errB[k] = rel(gpu_grads[k], gb) if np.linalg.norm(gb) > 0 else float(np.linalg.norm(gpu_grads[k]))
+    res["grad_rel_A_max"] = max(errA.values())
+    res["grad_rel_B_max"] = max(errB.values())
+    res["grad_rel_A"], res["grad_rel_B"] = errA, errB
+    if report is not None:
+        report.append(res)
+    print({k: v for k, v in res.items() if not isinstance(v, dict)}, flush=True)
+    # the assertions
+    assert res["fwd_row_rel_max"] <= tol, res
+    assert res["hinge_flip_arg_max"] <= kink, res
+    assert abs(loss - ref_loss) <= tol * abs(ref_loss) + kink / B, res
+    assert res["grad_rel_B_max"] <= tol, res
+    if strict_a:
+        assert res["grad_rel_A_max"] <= tol, res
+    return res
+
+
+def fixed_cotangent_check(model, feats, ids, w, nb, L, T, seed=0, tol=1e-4):
+    """The autograd path (PinSageModel forward + HIP backward) under a fixed
+    random cotangent vs the oracle's forward/backward with the same cotangent:
+    output rows and every parameter gradient, norm-relative."""
+    from oracle import oracle as orc
+    init = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    rng = np.random.default_rng(seed)
+    c = torch.from_numpy(rng.standard_normal((len(ids), model.out_dim)).astype(np.float32))
+    for prm in model.parameters():
+        prm.grad = None
+    y = model(feats.cuda(), torch.from_numpy(np.asarray(ids, np.int64)))
+    (y * c.cuda()).sum().backward()
+    p = {k: v.float().requires_grad_() for k, v in init.items()}
+    yr = orc.model_forward(p, feats.detach().cpu(), np.asarray(ids, np.int64), L, T, np.asarray(w),
+                           np.asarray(nb), model.out_dim)
+    (yr * c).sum().backward()
+    fwd = rel(y.detach().cpu().numpy(), yr.detach().numpy())
+    errs = {k: rel(prm.grad.cpu().numpy(), p[k].grad.numpy()) for k, prm in model.named_parameters()}
+    print(f"L={L} T={T} fwd={fwd:.2e} grad max={max(errs.values()):.2e}", flush=True)
+    assert fwd <= tol, fwd
+    assert max(errs.values()) <= tol, errs
+    return fwd, errs

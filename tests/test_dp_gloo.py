@@ -47,7 +47,19 @@ def _worker(rank, world, port, tmp, out_q):
         state = torch.get_rng_state()
         flat = torch.full((10,), float(rank + 1))
         pt.average_gradients(flat)
-        out_q.put((rank, [s.numpy() for s in slices], state.numpy(), flat.numpy()))
+        # precompute exchange: equal contiguous shards (n not divisible by the
+        # world size), one all-gather per table
+        import pinsage_model as pm
+        n = 2001
+        lo, hi, per = pm._shard_range(n, rank, world)
+        full_w = torch.arange(n * 3, dtype=torch.float64).reshape(n, 3) / 7
+        full_nb = torch.arange(n * 3, dtype=torch.int64).reshape(n, 3) * 5
+        sw = torch.zeros((per, 3), dtype=torch.float64)
+        snb = torch.zeros((per, 3), dtype=torch.int64)
+        sw[:hi - lo], snb[:hi - lo] = full_w[lo:hi], full_nb[lo:hi]
+        gw, gnb = pm._gather_shards(sw, snb, n, per, None)
+        gathered_ok = torch.equal(gw, full_w) and torch.equal(gnb, full_nb)
+        out_q.put((rank, [s.numpy() for s in slices], state.numpy(), flat.numpy(), gathered_ok))
     finally:
         os.chdir(cwd)
         dist.destroy_process_group()
@@ -70,7 +82,7 @@ def test_dp_batch_slices_and_grad_average():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, tmp, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (sl, st, fl)) for r, sl, st, fl in (q.get(timeout=300) for _ in procs))
+    res = dict((r, (sl, st, fl, ok)) for r, sl, st, fl, ok in (q.get(timeout=300) for _ in procs))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -93,3 +105,4 @@ def test_dp_batch_slices_and_grad_average():
         assert (got == ref[s]).all()
     assert (res[0][1] == res[1][1]).all()  # RNG stays in lock-step across ranks
     assert np.allclose(res[0][2], 1.5) and np.allclose(res[1][2], 1.5)
+    assert res[0][3] and res[1][3]  # all-gathered precompute shards == the full table

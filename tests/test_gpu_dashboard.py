@@ -1,0 +1,115 @@
+"""BASELINE config C1 through the reference's own caller: the
+``dashboard.train_pinsage`` flow (/root/reference/dashboard.py:48-79)
+
+    dataset = SpotifyGraph(DATA_DIR, features_dir)
+    g, track_ids, col_ids, features = dataset.to_dgl_graph()
+    positives = dataset.load_positives(positives.json)
+    pinsage = PinSage(g, len(track_ids), features, positives)
+    setattr(pinsage, "run_name", ...)
+    pinsage.train()
+    pt.save_embeddings(pinsage, dataset)
+
+on a dataset_micro-shaped JSON triple that reuses the 4,324 real track ids of
+/root/reference/dataset_micro (held in tests/golden/dataset.npz), 512-d
+per-track feature files, 1 layer, T = 3, batch 32 (C1).  Every train step of
+the loop is pinned against the oracle (parity_util.check_record: forward rows,
+hinge arguments, loss, gradients), the batches against the oracle's sampler
+(reference RNG consumption), and every exported embedding file against the
+oracle's forward with the trained parameters (1e-4 row-relative).
+"""
+import json
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from parity_util import capture_step, check_record
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dashboard_train_pinsage_flow_c1():
+    import pinsage_model as pm
+    import pinsage_training as pt
+    import spotify_graph
+    import synthetic
+    from oracle import oracle as orc
+    d = golden("dataset")
+    ids = [str(x) for x in d["track_ids"]]
+    n = len(ids)
+    pg = synthetic.make_playlist_graph(n, int(d["n_cols"]), 12000, seed=5)
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            ds_dir = os.path.join(tmp, "dataset_micro")
+            synthetic.write_spotify_dataset(ds_dir, pg, track_ids=ids, seed=6)
+            fdir = os.path.join(ds_dir, "features_openl3")
+            os.makedirs(fdir)
+            raw = np.random.default_rng(7).standard_normal((n, 512)).astype(np.float32)
+            for i, tid in enumerate(ids):
+                torch.save(torch.from_numpy(raw[i].copy()), os.path.join(fdir, tid + ".pt"))
+            pairs = synthetic.make_positives(pg, 5 * n, seed=8)
+            with open(os.path.join(ds_dir, "positives_lfm.json"), "w") as f:
+                json.dump([{"a": ids[a], "b": ids[b]} for a, b in pairs], f)
+
+            # --- dashboard.py:62-70
+            pm.set_rng_mode("mt19937")
+            torch.manual_seed(0)
+            dataset = spotify_graph.SpotifyGraph(ds_dir, fdir)
+            g, track_ids, col_ids, features = dataset.to_dgl_graph()
+            positives = dataset.load_positives(os.path.join(ds_dir, "positives_lfm.json"))
+            pinsage = pt.PinSage(g, len(track_ids), features, positives)
+            setattr(pinsage, "run_name", "pinsage_openl3_ft")
+            # C1's hyperparameters (1 layer, fanout 3, batch 32): the reference binds
+            # them at construction (pinsage_training.py:127-152), so the model and its
+            # optimizer are rebuilt as an edited pinsage_training.py would build them
+            pinsage.n_layers, pinsage.T, pinsage.batch_size = 1, 3, 32
+            pinsage.epochs, pinsage.b_per_e = 2, 4
+            torch.manual_seed(1)
+            pinsage.model = pm.PinSageModel(g, pinsage.n, 1, pinsage.dimensions, pinsage.n_hops,
+                                            pinsage.alpha, 3, pinsage.nbhds)
+            pinsage.optimizer = torch.optim.Adam(pinsage.model.parameters(), lr=pinsage.lr)
+            pinsage.scheduler = torch.optim.lr_scheduler.ExponentialLR(pinsage.optimizer, pinsage.decay)
+            records = []
+            train_batch = pinsage.train_batch
+
+            def recording_train_batch(batch):
+                rec = capture_step(pinsage, batch, run=train_batch)
+                records.append(rec)
+                return rec["out"]
+
+            pinsage.train_batch = recording_train_batch
+            torch.manual_seed(2)
+            pinsage.train()
+            pt.save_embeddings(pinsage, dataset)
+
+            # --- batches: the reference's sampler consumption from seed 2
+            assert len(records) == pinsage.epochs * pinsage.b_per_e
+            mt = orc.MT(2)
+            for rec in records:
+                rb, _ = orc.sample_batch_easy(mt, positives.numpy(), n, 32)
+                assert np.array_equal(rec["batch"], rb)
+            # --- every step against the oracle
+            w, nb = pinsage.nbhds
+            for rec in records:
+                check_record(rec, features, w.numpy(), nb.numpy())
+            # --- state.pt written every batch, lr decayed per epoch
+            prog = torch.load(os.path.join("runs", "pinsage_openl3_ft", "state.pt"), weights_only=True)
+            assert prog["epochs_done"] == 1 and prog["batches_done"] == pinsage.b_per_e - 1
+            assert abs(pinsage.optimizer.param_groups[0]["lr"] - 1e-4 * 0.95 ** 2) < 1e-15
+            # --- exported embeddings vs the oracle's forward with the trained parameters
+            emb_dir = os.path.join("runs", "pinsage_openl3_ft", "emb")
+            assert sorted(os.listdir(emb_dir)) == sorted(t + ".pt" for t in ids)
+            got = np.stack([torch.load(os.path.join(emb_dir, t + ".pt"), weights_only=True).numpy()
+                            for t in ids])
+            params = {k: v.detach().cpu() for k, v in pinsage.model.state_dict().items()}
+            ref = orc.model_forward(params, features.cpu(), np.arange(n), 1, 3, w.numpy(), nb.numpy(),
+                                    128).numpy()
+            err = np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1)
+            assert err.max() <= 1e-4, err.max()
+        finally:
+            os.chdir(cwd)

@@ -138,7 +138,7 @@ def test_dp_two_ranks_match_oracle_dp():
         assert np.linalg.norm(diff) <= 1e-4 * np.linalg.norm(rv), k
 
 
-def _precompute_worker(rank, world, port, tmp, mode, out_q):
+def _precompute_worker(rank, world, port, tmp, mode, out_q, n_items=N_TRACKS):
     import sys
     for p in (PKG, REPO):
         if p not in sys.path:
@@ -153,16 +153,18 @@ def _precompute_worker(rank, world, port, tmp, mode, out_q):
         g, _, _ = _problem(tmp)
         pm.set_rng_mode(mode)
         torch.manual_seed(0)
-        w, nb = pm.precompute_neighborhoods_topt(g, N_TRACKS, 200, 0.85, 20, None)
+        w, nb = pm.precompute_neighborhoods_topt(g, n_items, 200, 0.85, 20, None)
         out_q.put((rank, w.numpy(), nb.numpy(), torch.get_rng_state().numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["mt19937", "philox"])
-def test_precompute_sharded_over_ranks_matches_single_process(mode):
-    """the precompute is dealt over the ranks by source chunk and
-    summed; table and the generator state afterwards are bitwise those of one
+@pytest.mark.parametrize("mode,n_items", [("mt19937", N_TRACKS), ("philox", N_TRACKS),
+                                          ("mt19937", N_TRACKS - 1), ("philox", N_TRACKS - 2)])
+def test_precompute_sharded_over_ranks_matches_single_process(mode, n_items):
+    """every rank walks an equal contiguous shard of the sources
+    (the last one shorter when n is not divisible by the world size) and the
+    shards are all-gathered; table and the generator state afterwards are bitwise those of one
     process computing everything (MT19937: exact jump-ahead to each chunk)."""
     import pinsage_model as pm
     tmp = tempfile.mkdtemp()
@@ -170,14 +172,14 @@ def test_precompute_sharded_over_ranks_matches_single_process(mode):
     pm.set_rng_mode(mode)
     try:
         torch.manual_seed(0)
-        w1, nb1 = pm.precompute_neighborhoods_topt(g, N_TRACKS, 200, 0.85, 20, None)
+        w1, nb1 = pm.precompute_neighborhoods_topt(g, n_items, 200, 0.85, 20, None)
         st1 = torch.get_rng_state().numpy()
     finally:
         pm.set_rng_mode("mt19937")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_precompute_worker, args=(r, 3, port, tmp, mode, q)) for r in range(3)]
+    procs = [ctx.Process(target=_precompute_worker, args=(r, 3, port, tmp, mode, q, n_items)) for r in range(3)]
     for p in procs:
         p.start()
     res = [q.get(timeout=100) for _ in procs]

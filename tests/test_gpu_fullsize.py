@@ -81,16 +81,16 @@ def test_frontier_full_batch(c2):
 
 @pytest.mark.parametrize("margin", [3.0, 1e-5])
 def test_train_step_full_size_vs_oracle(c2, margin):
-    """margin 3: every triple's hinge is active, so the gradient is a smooth
-    function of the forward and must match within 1e-4.  The reference's margin
-    1e-5 at initialisation puts triples within rounding of the hinge's kink
-    (embeddings start nearly collapsed: neg - pos ~ 0), where fp32-level
-    forward differences switch single triples on or off; there the loss must
-    still match within 1e-4 and the gradients within the share of the batch
-    that such flips can move."""
-    import pinsage_training as pt
+    """One train step on the full C2 problem against the oracle.  Margin 3:
+    every triple's hinge is active.  The reference's margin 1e-5 at
+    initialisation puts triples within rounding of the hinge's kink (embeddings
+    start nearly collapsed); parity_util.check_train_step pins that step in its
+    well-conditioned parts -- forward rows, per-triple hinge arguments (a
+    triple whose activity differs from the oracle's must sit within 1e-6 of the
+    kink), loss, the oracle's gradient over the GPU's active set, and the
+    oracle's backward under the GPU outputs' cotangent -- all at 1e-4."""
     import synthetic
-    from oracle import oracle as orc
+    from parity_util import check_train_step, make_trainer
     pg, g, indptr, indices, w, nb = c2
     feats = torch.from_numpy(np.random.default_rng(1).standard_normal((N_TRACKS, D_IN),
                                                                       dtype=np.float32))
@@ -101,30 +101,10 @@ def test_train_step_full_size_vs_oracle(c2, margin):
         try:
             g.nbhds_path = os.path.join(tmp, "nb.pt")
             torch.save((w, nb), g.nbhds_path)
-            torch.manual_seed(0)
-            tr = pt.PinSage(g, N_TRACKS, feats.cuda(), pos, log=False, load_save=False)
-            tr.T, tr.n_layers = T, 2
-            import pinsage_model as pm
-            torch.manual_seed(0)
-            tr.model = pm.PinSageModel(g, tr.n, 2, tr.dimensions, tr.n_hops, tr.alpha, T, tr.nbhds)
-            tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
-            tr.batch_size = B
-            init = {k: v.detach().cpu().numpy().copy() for k, v in tr.model.state_dict().items()}
-            tr.margin = margin
-            ref = orc.RefTrainer(init, feats, w.numpy(), nb.numpy(), n_layers=2, T=T, margin=margin)
+            tr = make_trainer(g, N_TRACKS, feats.cuda(), pos, 2, T, B, margin, seed=0)
             torch.manual_seed(3)
             batch, _ = tr.next_batch()
-            loss, _, _ = tr.train_batch(batch)
-            rl, _, _, rg = ref.step(batch.numpy())
-            assert abs(float(loss) - rl) <= 1e-4 * abs(rl) + 1e-7, (float(loss), rl)
-            errs = {}
-            for k, p in tr.model.named_parameters():
-                a = p.grad.detach().cpu().numpy().astype(np.float64)
-                b = rg[k].numpy().astype(np.float64)
-                errs[k] = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-30)
-            print("margin", margin, "grad rel errors", errs)
-            tol = 1e-4 if margin > 1 else 3e-2
-            assert all(e <= tol for e in errs.values()), errs
+            check_train_step(tr, feats, w.numpy(), nb.numpy(), batch)
         finally:
             os.chdir(cwd)
 

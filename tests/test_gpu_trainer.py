@@ -105,3 +105,30 @@ def test_embed_and_embedding_files():
             assert torch.allclose(allv, full, rtol=1e-5, atol=1e-6)
         finally:
             os.chdir(cwd)
+
+
+def test_train_after_large_forward_matches_oracle():
+    """A forward over more ids than the fused step's engine holds (embed() of
+    every track) replaces the runner's engine; the next train_batch must rebuild
+    its workspaces for it and still match the oracle's step
+    (parity_util.check_train_step, reference margin and init)."""
+    import pinsage_training as pt
+    from parity_util import check_train_step
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            tr.batch_size = 32
+            torch.manual_seed(2)
+            for it in range(3):
+                batch, _ = tr.next_batch()
+                check_train_step(tr, feats, tr.nbhds[0].numpy(), tr.nbhds[1].numpy(), batch)
+                if it == 0:
+                    e = tr.embed()  # all N ids: > 3 * batch_size, a larger engine
+                    assert e.shape == (N, 128) and torch.isfinite(e).all()
+                    tr.model.train()
+        finally:
+            os.chdir(cwd)
