@@ -34,8 +34,10 @@ CONFIGS = {
     "c3": dict(workload="synthetic dataset_large-scale playlist graph, 2-layer PinSAGE, fanout 25, "
                         "batch 2048", n_tracks=1_000_000, n_cols=250_000, memberships=10_000_000,
                d_in=512, n_layers=2, T=25, batch=2048),
+    # memberships are drawn with repeats and deduplicated: 53.6M draws leave 50.0M distinct
+    # track-collection pairs = 100.0M directed edges (tests/test_gpu_configs.py checks it)
     "c4": dict(workload="synthetic 10M nodes / 100M edges, 128-d features, 2-layer, per-GPU batch 512",
-               n_tracks=8_000_000, n_cols=2_000_000, memberships=50_000_000, d_in=128, n_layers=2,
+               n_tracks=8_000_000, n_cols=2_000_000, memberships=53_600_000, d_in=128, n_layers=2,
                T=10, batch=512, global_batch=4096),
 }
 # --scaling strong: the global batch stays fixed (C4 B_global 4096, per-GPU

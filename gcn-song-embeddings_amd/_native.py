@@ -61,6 +61,11 @@ _SIGS = {
     "pinsage_walk_philox": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, u64, u32, i64, vp, vp]),
     "pinsage_visit_topk_scratch": (i64, [i64, i64, i64]),
     "pinsage_visit_topk": (ctypes.c_int, [vp, vp, i64, i64, i64, i64, vp, vp, vp, vp, vp, i64, vp]),
+    "pinsage_ppr_topk_workspace": (i64, [i64, i64, ctypes.c_int]),
+    "pinsage_engine_set_gemm_choice": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_int]),
+    "pinsage_ppr_topk": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, i64, vp, u64, u32, i64, vp, i64,
+                                        vp, vp, vp, vp, i64, vp]),
     "pinsage_visit_dense": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, vp]),
     "pinsage_frontier_workspace": (i64, [i64]),
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),

@@ -25,6 +25,10 @@ int launch_visit_topk(const int32_t*, const int64_t*, int64_t, int64_t, int64_t,
                       double*, int64_t*, float*, int32_t*, int64_t, hipStream_t);
 int launch_visit_dense(const int32_t*, const int64_t*, int64_t, int64_t, int64_t, double*,
                        hipStream_t);
+int launch_walk_runs(const int64_t*, const int32_t*, const int64_t*, int64_t, int, float,
+                     const uint32_t*, uint64_t, uint32_t, int64_t, uint2*, int*, int*, hipStream_t);
+int launch_heap_topk(const uint2*, const int*, int64_t, int, int, double*, int64_t*, float*, int32_t*,
+                     int, hipStream_t);
 int64_t bitset_words(int64_t universe);
 int64_t bitset_blocks(int64_t universe);
 int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
@@ -259,6 +263,87 @@ int pinsage_walk_philox(const int64_t* indptr, const int32_t* indices, int64_t n
   }
   PS_CHECK_HIP(hipFreeAsync(err_dev, st));
   if (rc != kOk) return rc;
+  if (err != 0x7f7f7f7f) {
+    set_error("walk: zero-degree node met (the reference's torch.randint(0) raises here)");
+    return kErrGraph;
+  }
+  return kOk;
+}
+
+// ------------------------------------------------------------------ fused walk + top-k
+// Workspace: [MT chunk states | err | n_runs[R] | runs[R][n_hops] | MT raw words[R][3 n_hops]]
+// for R sources per round (R = all of them with pinsage_ppr_topk_workspace's size).
+static int64_t ppr_round_bytes(int64_t n_hops, bool mt) {
+  return 4 + n_hops * 8 + (mt ? 3 * n_hops * 4 : 0);
+}
+static constexpr int64_t kPprChunks = 1024;
+static int64_t ppr_fixed_bytes() {
+  return align_up(kPprChunks * (int64_t)sizeof(MTChunk), 256) + 256;
+}
+
+int64_t pinsage_ppr_topk_workspace(int64_t n_src, int64_t n_hops, int rng_mt) {
+  return ppr_fixed_bytes() + 3 * 256 + std::max<int64_t>(n_src, 1) * ppr_round_bytes(n_hops, rng_mt != 0);
+}
+
+int pinsage_ppr_topk(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                     const int64_t* sources, int64_t n_src, int64_t n_hops, float alpha, int64_t k,
+                     void* mt, uint64_t seed, uint32_t offset, int64_t src_base, void* ws,
+                     int64_t ws_bytes, double* w_out, int64_t* nb_out, float* wn_out,
+                     int32_t* nb32_out, int64_t t_norm, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  PS_REQUIRE(n_src >= 0 && n_hops > 0 && n_all > 0, kErrArg, "ppr_topk: bad sizes");
+  PS_REQUIRE(k >= 1 && k <= n_all, kErrArg, "ppr_topk: k out of range (torch: selected index k out of range)");
+  PS_REQUIRE(k * 64 <= n_all, kErrArg,
+             "ppr_topk: the nth_element regime (k * 64 > n_all) needs pinsage_visit_topk");
+  PS_REQUIRE(n_hops < 65536 && k + n_hops < 65536, kErrArg, "ppr_topk: n_hops / k too large");
+  PS_REQUIRE(n_hops <= 8192, kErrArg, "ppr_topk: n_hops too large for the LDS sort");
+  PS_REQUIRE(n_all < (int64_t)0xFFFFFFFF, kErrArg, "ppr_topk: n_all must fit 32 bits");
+  PS_REQUIRE(!wn_out || (t_norm >= 1 && t_norm <= k), kErrArg, "ppr_topk: t_norm must be in [1, k]");
+  if (n_src == 0) return kOk;
+  const bool use_mt = mt != nullptr;
+  char* base = static_cast<char*>(ws);
+  MTChunk* desc_dev = reinterpret_cast<MTChunk*>(base);
+  const int64_t fixed = ppr_fixed_bytes();
+  int* err_dev = reinterpret_cast<int*>(base + fixed - 256);
+  const int64_t room = (ws_bytes - fixed - 3 * 256) / ppr_round_bytes(n_hops, use_mt);
+  PS_REQUIRE(room >= 1, kErrWorkspace, "ppr_topk: workspace too small for one source");
+  const int64_t R = std::min(room, n_src);
+  int* nr_dev = reinterpret_cast<int*>(base + fixed);
+  uint2* runs_dev = reinterpret_cast<uint2*>(base + fixed + align_up(R * 4, 256));
+  uint32_t* raw = reinterpret_cast<uint32_t*>(base + fixed + align_up(R * 4, 256) +
+                                              align_up(R * n_hops * 8, 256));
+  PS_CHECK_HIP(hipMemsetAsync(err_dev, 0x7f, 4, st));
+  std::vector<MTChunk> desc(use_mt ? (size_t)kPprChunks : 0);
+  const int64_t per_src = 3 * n_hops;
+  for (int64_t r0 = 0; r0 < n_src; r0 += R) {
+    const int64_t nr = std::min(R, n_src - r0);
+    if (use_mt) {
+      MTState& g = *reinterpret_cast<MTState*>(mt);
+      const int64_t spc = (nr + kPprChunks - 1) / kPprChunks;
+      const int64_t n_chunks = (nr + spc - 1) / spc;
+      const int64_t wpc = spc * per_src;
+      for (int64_t c = 0; c < n_chunks; ++c) {
+        MTChunk& d = desc[(size_t)c];
+        std::memcpy(d.s, g.s, sizeof(d.s));
+        d.next = g.next;
+        d.avail = (uint32_t)g.avail();
+        g.skip(std::min(wpc, (nr - c * spc) * per_src));
+      }
+      PS_CHECK_HIP(hipMemcpyAsync(desc_dev, desc.data(), (size_t)n_chunks * sizeof(MTChunk),
+                                  hipMemcpyHostToDevice, st));
+      PS_TRY(launch_mt_expand(desc_dev, n_chunks, wpc, nr * per_src, raw, st));
+    }
+    PS_TRY(launch_walk_runs(indptr, indices, sources + r0, nr, (int)n_hops, alpha,
+                            use_mt ? raw : nullptr, seed, offset, src_base + r0, runs_dev, nr_dev,
+                            err_dev, st));
+    PS_TRY(launch_heap_topk(runs_dev, nr_dev, nr, (int)n_hops, (int)k, w_out ? w_out + r0 * k : nullptr,
+                            nb_out ? nb_out + r0 * k : nullptr, wn_out ? wn_out + r0 * t_norm : nullptr,
+                            nb32_out ? nb32_out + r0 * t_norm : nullptr, (int)t_norm, st));
+    if (use_mt && r0 + nr < n_src) PS_CHECK_HIP(hipStreamSynchronize(st));  // desc is reused
+  }
+  int err = 0;
+  PS_CHECK_HIP(hipMemcpyAsync(&err, err_dev, 4, hipMemcpyDeviceToHost, st));
+  PS_CHECK_HIP(hipStreamSynchronize(st));
   if (err != 0x7f7f7f7f) {
     set_error("walk: zero-degree node met (the reference's torch.randint(0) raises here)");
     return kErrGraph;

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -119,6 +120,12 @@ struct Engine {
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   std::vector<TimingSite> sites;
+  // per-site GEMM tile / stream-K / split-K choices (pinsage_engine_set_gemm_choice:
+  // set by the trainer's in-context tuner; absent = the launcher's size model)
+  struct GemmChoice {
+    int cfg = -1, stream_k = -1, splits = 0;
+  };
+  std::map<std::string, GemmChoice> choice;
   // pinsage_engine_set_fork: the next forward_layers call forks another
   // workspace's frontier onto `stream` right after the layer-0 Q projection
   struct Fork {
@@ -209,6 +216,14 @@ struct Timed {
 };
 
 static std::string lname(const char* base, int l) { return std::string(base) + ".l" + std::to_string(l); }
+
+// the tuner's choice for a GEMM site, if any
+static void apply_choice(const Engine& E, const std::string& site, GemmParams& p) {
+  auto it = E.choice.find(site);
+  if (it == E.choice.end()) return;
+  if (it->second.cfg >= 0) p.cfg = it->second.cfg;
+  if (it->second.stream_k >= 0) p.stream_k = it->second.stream_k;
+}
 
 static size_t carve(size_t& cur, int64_t bytes) {
   cur = (size_t)align_up((int64_t)cur, 256);
@@ -448,6 +463,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     {
       Timed tt(E, lname("fwd.q_gemm", l), st);
       with_sk(E, ws, q);
+      apply_choice(E, lname("fwd.q_gemm", l), q);
       PS_TRY(launch_gemm(q, st));
     }
     if (l == 0 && E.fork.stream) {  // the next batch's frontier beside the rest of the step
@@ -481,6 +497,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     w.norms = at<float>(ws, lb.nrm);
     Timed tw(E, lname("fwd.w_gemm", l), st);
     with_sk(E, ws, w);
+    apply_choice(E, lname("fwd.w_gemm", l), w);
     PS_TRY(launch_gemm(w, st));
   }
   // head: G2(lrelu(G1 y))
@@ -568,13 +585,20 @@ static AdamSlice adam_slice(const Engine& E, const AdamStep& a, int64_t w_off, i
 // waits for this event, recorded behind the main stream's last read of it
 // main: the launch runs on the main stream (its own slabs; the
 // weight-gradient stream may be using the others meanwhile)
-static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st,
+static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, const std::string& site,
                        const AdamSlice* adam = nullptr, hipEvent_t after_use = nullptr,
                        bool main = false, bool beside = false) {
   float* const slab = at<float>(ws, main ? E.slab_main : E.slab);
   float* const bslab = at<float>(ws, main ? E.bslab_main : E.bslab);
   int cfg = 0, S = 1;
   choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
+  {
+    auto it = E.choice.find(site);
+    if (it != E.choice.end()) {
+      if (it->second.cfg >= 0) cfg = it->second.cfg;
+      if (it->second.splits > 0) S = std::min(it->second.splits, kMaxSplits);
+    }
+  }
   GemmParams p;
   p.cfg = cfg;
   if (beside) p.grid_cap = E.side_grid;
@@ -654,7 +678,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   Timed t_hb(E, "bwd.head", st);
   PS_TRY(dep(E, st, s_wg));  // dZ, H1 ready: dG2 beside the head backward
   {
-    Timed tw(E, "bwd.wgrad.head", s_wg);
+    Timed tw(E, "bwd.wgrad.g2", s_wg);
     WGrad w;
     w.A = at<float>(ws, E.dZ);
     w.lda = o;
@@ -667,7 +691,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.K_hint = top.S.hint;
     w.dst = gr + E.pG2w;
     w.ld_dst = o;
-    PS_TRY(weight_grad(E, ws, w, s_wg, nullptr, nullptr, false, s_wg != st));
+    PS_TRY(weight_grad(E, ws, w, s_wg, "bwd.wgrad.g2", nullptr, nullptr, false, s_wg != st));
   }
   // dP1 = (dZ G2) * lrelu'(H1), dY_top = dP1 G1 and the top layer's
   // normalisation backward (dp_top) in one kernel, which also zeroes the
@@ -721,8 +745,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.dst = gr + E.pG1w;
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
-    Timed tw(E, "bwd.wgrad.head", s_wg);
-    PS_TRY(weight_grad(E, ws, w, s_wg, nullptr, nullptr, false, s_wg != st));
+    Timed tw(E, "bwd.wgrad.g1", s_wg);
+    PS_TRY(weight_grad(E, ws, w, s_wg, "bwd.wgrad.g1", nullptr, nullptr, false, s_wg != st));
   }
   t_hb.stop();
   for (int l = Lc - 1; l >= 0; --l) {
@@ -789,11 +813,14 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
         p.ldc = hd;
       }
       with_sk(E, ws, p);
+      apply_choice(E, lname("bwd.dcat", l), p);
+      Timed td(E, lname("bwd.dcat", l), st);
       PS_TRY(launch_gemm(p, st));
     }
     {
       Timed tw(E, lname("bwd.w_wgrad", l), s_w);
-      PS_TRY(weight_grad(E, ws, w_wgrad, s_w, nullptr, nullptr, false, s_w != st));
+      PS_TRY(weight_grad(E, ws, w_wgrad, s_w, lname("bwd.w_wgrad", l), nullptr, nullptr, false,
+                         s_w != st));
     }
     if (adam && l == 0) {  // every gradient but Q0's exists on s_w; W0 was read last
       PS_TRY(dep(E, st, s_w));
@@ -845,6 +872,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       p.c_idx = at<int32_t>(ws, lb.q_src);
       p.epi = kEpiAccum;
       with_sk(E, ws, p);
+      apply_choice(E, lname("bwd.dh", l), p);
+      Timed tdh(E, lname("bwd.dh", l), st);
       PS_TRY(launch_gemm(p, st));
     }
     {
@@ -852,7 +881,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       if (adam && l == 0) q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
       hipStream_t qs = l == 0 ? st : s_wg;
       Timed tq(E, lname("bwd.q_wgrad", l), qs);
-      PS_TRY(weight_grad(E, ws, q_wgrad, qs, adam && l == 0 ? &q0 : nullptr, nullptr, l == 0,
+      PS_TRY(weight_grad(E, ws, q_wgrad, qs, lname("bwd.q_wgrad", l), adam && l == 0 ? &q0 : nullptr,
+                         nullptr, l == 0,
                          qs != st));
     }
   }
@@ -1021,6 +1051,22 @@ int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, in
     PS_CHECK_HIP(hipMemcpy(&v, at<int>(ws, E->L[l].N.count), 4, hipMemcpyDeviceToHost));
     N[l] = v;
   }
+  return kOk;
+}
+
+int pinsage_engine_set_gemm_choice(pinsage_engine* e, const char* site, int cfg, int stream_k,
+                                   int splits) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  if (!E || !site) {
+    set_error("engine_set_gemm_choice: null argument");
+    return kErrArg;
+  }
+  if (cfg < -1 || cfg > 3 || stream_k < -1 || stream_k > 1 || splits < 0 || splits > kMaxSplits) {
+    set_error("engine_set_gemm_choice: cfg in [-1, 3], stream_k in [-1, 1], splits in [0, 64]");
+    return kErrArg;
+  }
+  if (cfg < 0 && stream_k < 0 && splits == 0) E->choice.erase(site);
+  else E->choice[site] = Engine::GemmChoice{cfg, stream_k, splits};
   return kOk;
 }
 

@@ -148,10 +148,66 @@ def _topk_device(src, trace, n_all, n_hops, T, t_norm=0):
     return w, nb, wn, nb32
 
 
+# fused walk + count + top-k (pinsage_ppr_topk): the trace never reaches HBM;
+# at most this many bytes of device scratch per call (more sources run in rounds)
+_PPR_WS_CAP = 1 << 30
+
+
+def _ppr_topk_device(g, nodeset, n_hops, alpha, T, t_norm=0, philox=None, want_ref=True):
+    """Top-T of visit_prob for each source (pinsage_model.py:32-53, 88-107) with
+    the fused kernel; same draws as _walk_device (+ _topk_device).  Returns
+    (w f64, nb i64, wn f32, nb32 i32) on the device (None where not asked).
+    Tiny graphs (T * 64 > N_all: torch's nth_element regime) take the walk +
+    visit_topk kernels."""
+    g = _as_csr(g)
+    n_all = g.number_of_nodes()
+    T = int(T)
+    if T * 64 > n_all or int(n_hops) + T >= 65536 or int(n_hops) > 8192:
+        src, trace = _walk_device(g, nodeset, n_hops, alpha, philox)
+        return _topk_device(src, trace, n_all, n_hops, T, t_norm=t_norm)
+    dev = nat.device()
+    indptr, indices = g.device_csr(dev)
+    src = torch.as_tensor(nodeset).reshape(-1).to(device=dev, dtype=torch.int64)
+    n = int(src.shape[0])
+    w = torch.empty((n, T), dtype=torch.float64, device=dev) if want_ref else None
+    nb = torch.empty((n, T), dtype=torch.int64, device=dev) if want_ref else None
+    wn = nb32 = None
+    if t_norm:
+        wn = torch.empty((n, t_norm), dtype=torch.float32, device=dev)
+        nb32 = torch.empty((n, t_norm), dtype=torch.int32, device=dev)
+    if n == 0:
+        return w, nb, wn, nb32
+    L = nat.lib()
+    alpha32 = float(np.float32(alpha))
+    mt_mode = _RNG_MODE == "mt19937" and philox is None
+    if mt_mode and g.max_degree() >= (1 << 28):
+        raise RuntimeError("degree >= 2^28: torch.randint switches to 64-bit draws; use rng mode 'philox'")
+    need = L.pinsage_ppr_topk_workspace(n, int(n_hops), 1 if mt_mode else 0)
+    ws = torch.empty(min(need, _PPR_WS_CAP), dtype=torch.uint8, device=dev)
+
+    def run(mt_p, seed, base):
+        nat.check(L.pinsage_ppr_topk(nat.ptr(indptr), nat.ptr(indices), n_all, nat.ptr(src), n,
+                                     int(n_hops), alpha32, T, mt_p, seed, 0, base, nat.ptr(ws),
+                                     ws.numel(), nat.ptr(w), nat.ptr(nb), nat.ptr(wn), nat.ptr(nb32),
+                                     int(t_norm), nat.stream_ptr()), "ppr_topk")
+
+    if mt_mode:
+        with nat.torch_rng() as mt:
+            run(mt.p, 0, 0)
+    else:
+        if philox is None:
+            with nat.torch_rng() as mt:
+                d = mt.draws(2)
+            seed, base = (int(d[0]) << 32) | int(d[1]), 0
+        else:
+            seed, base = philox
+        run(None, seed, int(base))
+    return w, nb, wn, nb32
+
+
 def sample_neighborhood_topt(g, n_items, nodeset, n_hops, alpha, T):
     """visit_prob.topk(T, 1) as a ``torch.return_types.topk`` (pinsage_model.py:103-107)."""
-    src, trace = _walk_device(g, nodeset, n_hops, alpha)
-    w, nb, _, _ = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T))
+    w, nb, _, _ = _ppr_topk_device(g, nodeset, n_hops, alpha, int(T))
     out_dev = torch.as_tensor(nodeset).device
     return torch.return_types.topk((w.to(out_dev), nb.to(out_dev)))
 
@@ -195,6 +251,7 @@ def _gather_shards(w_sh, nb_sh, n_items, per, dev):
             d.all_gather_into_tensor(full, x)
             out.append(full[:n_items].cpu())
         else:
+            t = t.cpu()
             parts = [torch.empty_like(t) for _ in range(world)]
             d.all_gather(parts, t)
             out.append(torch.cat(parts, 0)[:n_items].contiguous())
@@ -223,8 +280,10 @@ def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
     rank, world = _shard()
     lo, hi, per = _shard_range(n_items, rank, world)
     rows = per if world > 1 else n_items
-    sh_w = torch.zeros((rows, T), dtype=torch.float64)
-    sh_nb = torch.zeros((rows, T), dtype=torch.int64)
+    # the shard is assembled on the device (zero padding rows of a short last
+    # shard) and crosses to the host once
+    sh_w = torch.zeros((rows, T), dtype=torch.float64, device=dev)
+    sh_nb = torch.zeros((rows, T), dtype=torch.int64, device=dev)
     st0 = torch.get_rng_state().numpy().copy()
     mt_mode = _RNG_MODE == "mt19937"
     philox = None
@@ -239,17 +298,16 @@ def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
         if mt_mode:
             _set_stream_position(st0, 3 * int(n_hops) * i)
         ids = torch.arange(i, min(i + chunk, hi), dtype=torch.int64, device=dev)
-        src, trace = _walk_device(g, ids, n_hops, alpha, None if mt_mode else (philox, i))
-        w, nb, _, _ = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T))
-        sh_w[i - lo:i - lo + ids.shape[0]] = w.cpu()
-        sh_nb[i - lo:i - lo + ids.shape[0]] = nb.cpu()
+        w, nb, _, _ = _ppr_topk_device(g, ids, n_hops, alpha, int(T), philox=None if mt_mode else (philox, i))
+        sh_w[i - lo:i - lo + ids.shape[0]] = w
+        sh_nb[i - lo:i - lo + ids.shape[0]] = nb
         print(f"{min(i + chunk, hi)}/{n_items} done.")
     if mt_mode:
         _set_stream_position(st0, 3 * int(n_hops) * n_items)
     if world > 1:
         all_w, all_nb = _gather_shards(sh_w, sh_nb, n_items, per, dev)
     else:
-        all_w, all_nb = sh_w, sh_nb
+        all_w, all_nb = sh_w.cpu(), sh_nb.cpu()
     print(f"{time.time() - t0}s elapsed.")
     if path and rank == 0:
         torch.save((all_w, all_nb), path)
@@ -284,8 +342,7 @@ def relevant_nodes_per_layer(g, n_items, nodeset, n_layers, n_hops, alpha, T):
     S = []
     cur = torch.as_tensor(nodeset).to(dev, torch.int64)
     for _ in reversed(range(0, n_layers)):
-        src, trace = _walk_device(g, cur, n_hops, alpha)
-        w, nb, _, nb32 = _topk_device(src, trace, g.number_of_nodes(), n_hops, int(T), t_norm=int(T))
+        w, nb, _, nb32 = _ppr_topk_device(g, cur, n_hops, alpha, int(T), t_norm=int(T))
         S.insert(0, (cur.to(out_dev), w.to(out_dev), nb.to(out_dev)))
         # unique(cat(nb.flatten(), cur)): rows of nb belong to cur's positions
         table = torch.zeros((g.number_of_nodes(), int(T)), dtype=torch.int32, device=dev)

@@ -279,6 +279,9 @@ class _FusedStep:
         self.graph_B = None
         self.parity = 0
         self.ahead_hits = 0
+        # in-context GEMM tuner (see _autotune); PINSAGE_AUTOTUNE=0 keeps the size model
+        self.autotune = os.environ.get("PINSAGE_AUTOTUNE", "1") != "0"
+        self.tuned_choices = None
 
     def ensure(self, B):
         r = self.runner
@@ -317,6 +320,7 @@ class _FusedStep:
             self.parity = 0
             self.ws = self.wss[0]
             self._tuned = False
+            self.tuned_choices = None
             self.graphs = None
 
     def adopt_optimizer_state(self):
@@ -427,6 +431,77 @@ class _FusedStep:
         b1, b2 = g["betas"]
         nat.check(nat.lib().pinsage_engine_adam(self.runner.engine.h, self._coef_ptr(p), float(b1),
                                                 float(b2), float(g["eps"]), nat.stream_ptr()), "adam")
+
+    # per-site candidates: (cfg, stream_k, splits); a GEMM site takes a block-tile
+    # config with or without stream-K, a weight-gradient site a config and a split-K count
+    _GEMM_OPTS = [(c, k, 0) for c in (0, 1, 2, 3) for k in (0, 1) if not (c == 0 and k == 1)]
+    _WGRAD_OPTS = [(c, -1, sp) for c in (0, 1, 2) for sp in (1, 2, 4, 8, 16, 32)]
+
+    def _gemm_sites(self):
+        sites = []
+        for l in range(self.runner.model.n_layers):
+            sites += [(f"fwd.q_gemm.l{l}", self._GEMM_OPTS), (f"fwd.w_gemm.l{l}", self._GEMM_OPTS),
+                      (f"bwd.dcat.l{l}", self._GEMM_OPTS), (f"bwd.w_wgrad.l{l}", self._WGRAD_OPTS),
+                      (f"bwd.q_wgrad.l{l}", self._WGRAD_OPTS)]
+            if l > 0:
+                sites.append((f"bwd.dh.l{l}", self._GEMM_OPTS))
+        return sites + [("bwd.wgrad.g1", self._WGRAD_OPTS), ("bwd.wgrad.g2", self._WGRAD_OPTS)]
+
+    def _autotune(self, B, p, reps=3):
+        """In-context GEMM tuner: the size model picks tile configs from frontier
+        sizes alone, and measured in the step it is off by up to 2x on the small
+        projections (launch-latency bound, sensitive to the chip's state).  So on
+        the first step's frontier, every GEMM site is timed under each candidate
+        with HIP events on its launch stream (kernels back to back behind a
+        stream hold), and the fastest is kept (pinsage_engine_set_gemm_choice).
+        Probe k sets candidate k at every site at once (their interplay is second
+        order).  The probes rerun this step's frontier, layers, loss and
+        backward WITHOUT the optimizer: parameters and Adam state are untouched,
+        and every choice computes the same products (speed only)."""
+        e = self.runner.engine
+        L = nat.lib()
+        sites = self._gemm_sites()
+        n_probe = max(len(o) for _, o in sites)
+        best = {name: (float("inf"), None) for name, _ in sites}
+        hold = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        name = ctypes.create_string_buffer(128)
+        ms = ctypes.c_double()
+        calls = ctypes.c_int64()
+        for k in range(n_probe):
+            for site, opts in sites:
+                o = opts[k % len(opts)]
+                nat.check(L.pinsage_engine_set_gemm_choice(e.h, site.encode(), *o), "set_gemm_choice")
+            nat.check(L.pinsage_engine_timing(e.h, 1), "timing")
+            ok = True
+            try:
+                for _ in range(reps):
+                    L.pinsage_stream_hold(2000, hold)
+                    self._frontier(B, p)
+                    st = nat.stream_ptr()
+                    nat.check(L.pinsage_engine_forward_layers(e.h, nat.ptr(self.wss[p]), st), "forward_layers")
+                    nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.wss[p]), B, float(self.tr.margin), 1, st),
+                              "loss")
+                    nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.wss[p]), st), "backward")
+                torch.cuda.synchronize()
+            except RuntimeError:  # e.g. a split count whose slabs do not fit: not a candidate
+                ok = False
+                torch.cuda.synchronize()
+            L.pinsage_engine_timing_collect(e.h)
+            i = 0
+            while ok and L.pinsage_engine_timing_get(e.h, i, name, 128, ctypes.byref(ms), ctypes.byref(calls)) == 0:
+                nm = name.value.decode()
+                if nm in best and calls.value > 0:
+                    opts = dict(sites)[nm]
+                    t = ms.value / calls.value
+                    if t < best[nm][0]:
+                        best[nm] = (t, opts[k % len(opts)])
+                i += 1
+            L.pinsage_engine_timing(e.h, 0)
+        for site, _ in sites:
+            o = best[site][1]
+            nat.check(L.pinsage_engine_set_gemm_choice(e.h, site.encode(), *(o if o else (-1, -1, 0))),
+                      "set_gemm_choice")
+        self.tuned_choices = {k: {"us": v[0] * 1e3, "cfg": v[1]} for k, v in best.items()}
 
     def _signature(self, feats, table):
         return (self.runner.flat.data_ptr(), self.grads.data_ptr(), self.m.data_ptr(),
@@ -548,6 +623,8 @@ class _FusedStep:
             self._main(B, p, with_adam=not self.dist)
             self._publish(p)
             self.pending = [None, None]
+            if self.autotune and self._tuned and self.tuned_choices is None:
+                self._autotune(B, p)
             if self.use_graph and self._tuned:
                 self._capture(B, sig)
         if self.dist:

@@ -117,6 +117,25 @@ int pinsage_visit_topk(const int32_t* trace, const int64_t* sources, int64_t n_s
                        int64_t n_hops, int64_t n_all, int64_t k, void* dense_scratch,
                        double* w_out, int64_t* nb_out, float* wn_out, int32_t* nb32_out,
                        int64_t t_norm, void* stream);
+/* Fused walk + visit counting + top-k (the SURVEY's ppr_topk): replaces
+ * do_random_walks -> sample_neighborhood -> visit_prob.topk(k, 1)
+ * (pinsage_model.py:32-53, 88-107) in sample_neighborhood_topt and
+ * precompute_neighborhoods_topt (:103-132), and PersPageRank.knn
+ * (baselines.py:114-151).  The walk's trace stays in LDS (never in HBM); outputs
+ * as pinsage_visit_topk.  mt != null: MT19937 mode (host state advanced by
+ * 3*n_hops*n_src draws, exactly the reference's consumption); mt == null:
+ * Philox mode keyed by (seed, hop, src_base + i, offset), the same draws as
+ * pinsage_walk_philox.  Only the partial_sort regime (k * 64 <= n_all); the
+ * nth_element regime of tiny graphs goes through pinsage_visit_topk.
+ * ws: device bytes >= pinsage_ppr_topk_workspace(n_src, n_hops, mt != null)
+ * (smaller workspaces run in rounds).  Synchronises the stream (zero-degree
+ * check: the reference's torch.randint(0) raises). */
+int64_t pinsage_ppr_topk_workspace(int64_t n_src, int64_t n_hops, int rng_mt);
+int pinsage_ppr_topk(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                     const int64_t* sources, int64_t n_src, int64_t n_hops, float alpha, int64_t k,
+                     void* mt, uint64_t seed, uint32_t offset, int64_t src_base, void* ws,
+                     int64_t ws_bytes, double* w_out, int64_t* nb_out, float* wn_out,
+                     int32_t* nb32_out, int64_t t_norm, void* stream);
 /* sample_neighborhood (pinsage_model.py:88-101): dense f64 [n_src][n_all]. */
 int pinsage_visit_dense(const int32_t* trace, const int64_t* sources, int64_t n_src,
                         int64_t n_hops, int64_t n_all, double* dense, void* stream);
@@ -296,6 +315,15 @@ int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, in
 /* Expected frontier sizes (e.g. from read_counts): choose GEMM block tiles
  * that fill the chip; sizes stay device-side, hints only affect speed. */
 int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t* N);
+/* Per-site GEMM choice (a tuner measures the sites in context and fixes them):
+ * site names as the timing sites -- fwd.q_gemm.lN, fwd.w_gemm.lN, bwd.dcat.lN,
+ * bwd.dh.lN (block tile config cfg 0..3, stream_k 0/1), bwd.w_wgrad.lN,
+ * bwd.q_wgrad.lN, bwd.wgrad.g1, bwd.wgrad.g2 (cfg 0..3 and split-K count
+ * splits >= 1).  -1 / 0 leave a field to the launcher's size model; all three
+ * unset removes the site's entry.  Speed only: every choice computes the same
+ * GEMM (summation order may differ). */
+int pinsage_engine_set_gemm_choice(pinsage_engine* e, const char* site, int cfg, int stream_k,
+                                   int splits);
 
 /* Per-launch-site HIP-event timing on the launch stream (bench/profiling):
  * enable (also clears), collect after the work (synchronises the events), then

@@ -446,3 +446,37 @@ def test_train_step_three_layers_fanout_50_vs_oracle():
                     assert all(e < REL_TOL for e in errs.values()), errs
         finally:
             os.chdir(cwd)
+
+
+@pytest.mark.parametrize("mode", ["mt19937", "philox"])
+@pytest.mark.parametrize("k", [10, 100, 1000])
+def test_fused_ppr_topk_matches_walk_plus_topk(mode, k):
+    """pinsage_ppr_topk (walk + counts + heap replay in one pass, trace in LDS,
+    one lane per source for the heap) against do_random_walks' trace fed to the
+    visit_topk kernel and against the oracle: bit-exact, same RNG consumption,
+    including the normalised device-table outputs (t_norm)."""
+    import graph
+    import pinsage_model as pm
+    import synthetic
+    from oracle import oracle as orc
+    pg = synthetic.make_playlist_graph(70000, 10000, 300000, seed=31)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices)
+    src = torch.from_numpy(np.random.default_rng(k).integers(0, 70000, 700).astype(np.int64))
+    pm.set_rng_mode(mode)
+    try:
+        torch.manual_seed(99)
+        w, nb, wn, nb32 = pm._ppr_topk_device(g, src, 500, 0.85, k, t_norm=min(k, 25))
+        after_fused = torch.get_rng_state()
+        torch.manual_seed(99)
+        s2, trace = pm._walk_device(g, src, 500, 0.85)
+        w2, nb2, wn2, nb322 = pm._topk_device(s2, trace, pg.n_all, 500, k, t_norm=min(k, 25))
+        assert torch.equal(after_fused, torch.get_rng_state())
+    finally:
+        pm.set_rng_mode("mt19937")
+    assert torch.equal(w, w2) and torch.equal(nb, nb2)
+    assert torch.equal(wn, wn2) and torch.equal(nb32, nb322)
+    if mode == "mt19937":
+        rw, rn = orc.sample_neighborhood_topt(indptr, indices, pg.n_all, src.numpy()[:48], 500, 0.85, k,
+                                              orc.MT(99))
+        assert (w[:48].cpu().numpy() == rw).all() and (nb[:48].cpu().numpy() == rn).all()

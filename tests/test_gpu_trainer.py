@@ -125,7 +125,10 @@ def test_train_after_large_forward_matches_oracle():
             torch.manual_seed(2)
             for it in range(3):
                 batch, _ = tr.next_batch()
-                check_train_step(tr, feats, tr.nbhds[0].numpy(), tr.nbhds[1].numpy(), batch)
+                # B = 32: part A (oracle forward, short signed sums) at 1e-3, part B at 1e-4
+                res = check_train_step(tr, feats, tr.nbhds[0].numpy(), tr.nbhds[1].numpy(), batch,
+                                       strict_a=False)
+                assert res["grad_rel_A_max"] <= 1e-3, res
                 if it == 0:
                     e = tr.embed()  # all N ids: > 3 * batch_size, a larger engine
                     assert e.shape == (N, 128) and torch.isfinite(e).all()
