@@ -615,48 +615,68 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
 // backward hands the output row the SUM of the gradients of every position of
 // that call holding the same node (index_put backward, pinsage_model.py:29 then
 // :265), so G[c][rank] accumulates those sums and K[c][rank] the multiplicity;
-// loss_finish forms dZ = sum_c K[c] * G[c].
+// dZ = sum_c K[c] * G[c] is formed by the head backward as it loads its rows
+// (head.hip), or by dz_combine_kernel for the unfused head.
+//
+// Two memory round trips per wave: the triple's indices (pos_rank, batch ids),
+// then every Z and feature value it needs, into registers (ZPL / FPL values per
+// lane and row), before any arithmetic.  The variance monitor's per-block
+// column partials come from the query rows already in registers (via LDS);
+// loss_monitor_kernel reduces them beside the backward.
+template <int ZPL, int FPL>
 __global__ __launch_bounds__(256) void loss_triple_kernel(
     const float* __restrict__ Z, int d, const int32_t* __restrict__ pos_rank, int B, float margin,
     const float* __restrict__ feats, int64_t ld_f, int d_in, const int64_t* __restrict__ batch,
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ part,
     float* __restrict__ colpart, float* __restrict__ hinge) {
   __shared__ float red[4][4];  // per wave: loss, nfl, sum||h_q||^2, unused
-  // per-block column sum and sum of squared deviations from the block's own
-  // column mean over its (<= 4) query rows (variance monitor, merged by Chan's
-  // formula in loss_finish_kernel: no cancellation when the rows collapse)
-  {
-    const int b0 = blockIdx.x * 4;
-    const int nb = min(4, B - b0);
-    for (int c = threadIdx.x; c < d; c += blockDim.x) {
-      float x[4];
-      float s = 0.f;
-      for (int k = 0; k < 4; ++k) {
-        x[k] = k < nb ? Z[(int64_t)pos_rank[3 * (b0 + k)] * d + c] : 0.f;
-        s += x[k];
-      }
-      const float mb = s / (float)nb;
-      float m2 = 0.f;
-      for (int k = 0; k < 4; ++k)
-        if (k < nb) m2 += (x[k] - mb) * (x[k] - mb);
-      colpart[(int64_t)blockIdx.x * 2 * d + c] = s;
-      colpart[(int64_t)blockIdx.x * 2 * d + d + c] = m2;
+  __shared__ float qrow[4][64 * ZPL];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x * 4 + wv;
+  const bool valid = b < B;
+  // round 1: indices
+  int rq = 0, rp = 0, rn = 0;
+  int64_t iq = 0, ip = 0, in = 0;
+  if (valid) {
+    rq = pos_rank[3 * b];
+    rp = pos_rank[3 * b + 1];
+    rn = pos_rank[3 * b + 2];
+    if (feats) {
+      iq = batch[3 * b];
+      ip = batch[3 * b + 1];
+      in = batch[3 * b + 2];
     }
   }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + wv;
+  // round 2: rows into registers
+  float zq[ZPL], zp[ZPL], zn[ZPL];
+#pragma unroll
+  for (int i = 0; i < ZPL; ++i) {
+    const int c = lane + 64 * i;
+    const bool ok = valid && c < d;
+    zq[i] = ok ? Z[(int64_t)rq * d + c] : 0.f;
+    zp[i] = ok ? Z[(int64_t)rp * d + c] : 0.f;
+    zn[i] = ok ? Z[(int64_t)rn * d + c] : 0.f;
+  }
+  float fq[FPL], fp[FPL], fn[FPL];
+#pragma unroll
+  for (int i = 0; i < FPL; ++i) {
+    const int c = lane + 64 * i;
+    const bool ok = valid && feats && c < d_in;
+    fq[i] = ok ? feats[iq * ld_f + c] : 0.f;
+    fp[i] = ok ? feats[ip * ld_f + c] : 0.f;
+    fn[i] = ok ? feats[in * ld_f + c] : 0.f;
+  }
   float lossv = 0.f, nflv = 0.f, sq = 0.f;
-  if (b < B) {
-    const int rq = pos_rank[3 * b], rp = pos_rank[3 * b + 1], rn = pos_rank[3 * b + 2];
+  {
     // --- max_margin_loss on the model outputs
     float dq_ = 0.f, dp_ = 0.f, dn_ = 0.f, qp = 0.f, qn = 0.f;
-    for (int c = lane; c < d; c += 64) {
-      const float a = Z[(int64_t)rq * d + c], p = Z[(int64_t)rp * d + c], n = Z[(int64_t)rn * d + c];
-      dq_ += a * a;
-      dp_ += p * p;
-      dn_ += n * n;
-      qp += a * p;
-      qn += a * n;
+#pragma unroll
+    for (int i = 0; i < ZPL; ++i) {
+      dq_ += zq[i] * zq[i];
+      dp_ += zp[i] * zp[i];
+      dn_ += zn[i] * zn[i];
+      qp += zq[i] * zp[i];
+      qn += zq[i] * zn[i];
     }
     dq_ = wave_sum(dq_);
     dp_ = wave_sum(dp_);
@@ -668,16 +688,16 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
                 nn = fmaxf(sqrtf(dn_), 1e-12f);
     const float cqp = qp / (nq * np), cqn = qn / (nq * nn);
     const float ds = cqn - cqp + margin;
-    if (hinge && lane == 0) hinge[b] = ds;  // the hinge argument (parity tests read it)
-    lossv = ds >= 0.f ? ds : 0.f;
-    const float g = ds >= 0.f ? 1.f / (float)B : 0.f;
+    if (valid && hinge && lane == 0) hinge[b] = ds;  // the hinge argument (parity tests read it)
+    lossv = (valid && ds >= 0.f) ? ds : 0.f;
+    const float g = (valid && ds >= 0.f) ? 1.f / (float)B : 0.f;
     if (g != 0.f) {
       // d/d(normalised rows): q_hat <- g(n_hat - p_hat), p_hat <- -g q_hat,
       // n_hat <- g q_hat; then x_hat = x/||x||: dx = (g_hat - x_hat (x_hat.g_hat)) / ||x||
       float pq = 0.f, pp = 0.f, pn = 0.f;
-      for (int c = lane; c < d; c += 64) {
-        const float a = Z[(int64_t)rq * d + c] / nq, p = Z[(int64_t)rp * d + c] / np,
-                    n = Z[(int64_t)rn * d + c] / nn;
+#pragma unroll
+      for (int i = 0; i < ZPL; ++i) {
+        const float a = zq[i] / nq, p = zp[i] / np, n = zn[i] / nn;
         pq += a * (g * (n - p));
         pp += p * (-g * a);
         pn += n * (g * a);
@@ -685,24 +705,35 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
       pq = wave_sum(pq);
       pp = wave_sum(pp);
       pn = wave_sum(pn);
-      for (int c = lane; c < d; c += 64) {
-        const float a = Z[(int64_t)rq * d + c] / nq, p = Z[(int64_t)rp * d + c] / np,
-                    n = Z[(int64_t)rn * d + c] / nn;
-        atomicAdd(G + ((int64_t)0 * S_max + rq) * d + c, (g * (n - p) - a * pq) / nq);
-        atomicAdd(G + ((int64_t)1 * S_max + rp) * d + c, (-g * a - p * pp) / np);
-        atomicAdd(G + ((int64_t)2 * S_max + rn) * d + c, (g * a - n * pn) / nn);
+#pragma unroll
+      for (int i = 0; i < ZPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < d) {
+          const float a = zq[i] / nq, p = zp[i] / np, n = zn[i] / nn;
+          atomicAdd(G + ((int64_t)0 * S_max + rq) * d + c, (g * (n - p) - a * pq) / nq);
+          atomicAdd(G + ((int64_t)1 * S_max + rp) * d + c, (-g * a - p * pp) / np);
+          atomicAdd(G + ((int64_t)2 * S_max + rn) * d + c, (g * a - n * pn) / nn);
+        }
       }
     }
-    if (lane == 0) {
+    if (valid && lane == 0) {
       atomicAdd(Kc + 0 * S_max + rq, 1);
       atomicAdd(Kc + 1 * S_max + rp, 1);
       atomicAdd(Kc + 2 * S_max + rn, 1);
     }
     // --- monitor: cosine triplet loss on raw features (margin 1e-4)
     if (feats) {
-      const int64_t iq = batch[3 * b], ip = batch[3 * b + 1], in = batch[3 * b + 2];
       float fqq = 0.f, fpp = 0.f, fnn = 0.f, fqp = 0.f, fqn = 0.f;
-      for (int c = lane; c < d_in; c += 64) {
+#pragma unroll
+      for (int i = 0; i < FPL; ++i) {
+        fqq += fq[i] * fq[i];
+        fpp += fp[i] * fp[i];
+        fnn += fn[i] * fn[i];
+        fqp += fq[i] * fp[i];
+        fqn += fq[i] * fn[i];
+      }
+      // (d_in > 64 * FPL: the rest of the row, streamed)
+      for (int c = lane + 64 * FPL; valid && c < d_in; c += 64) {
         const float a = feats[iq * ld_f + c], p = feats[ip * ld_f + c], n = feats[in * ld_f + c];
         fqq += a * a;
         fpp += p * p;
@@ -722,51 +753,47 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
       const float cp = (fqp / (aq * ap)) / fmaxf(sqrtf(hq2 * hp2), 1e-8f);
       const float cn = (fqn / (aq * an)) / fmaxf(sqrtf(hq2 * hn2), 1e-8f);
       const float v = (1.f - cp) - (1.f - cn) + 1e-4f;
-      nflv = v > 0.f ? v : 0.f;
+      nflv = (valid && v > 0.f) ? v : 0.f;
     }
   }
+  // per-block column sum and sum of squared deviations from the block's own
+  // column mean over its (<= 4) query rows (variance monitor; Chan's merge below)
+#pragma unroll
+  for (int i = 0; i < ZPL; ++i) qrow[wv][lane + 64 * i] = zq[i];
   if (lane == 0) {
     red[wv][0] = lossv;
     red[wv][1] = nflv;
-    red[wv][2] = sq;
+    red[wv][2] = valid ? sq : 0.f;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  const int nb = min(4, B - (int)blockIdx.x * 4);
+  for (int c = tid; c < d; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < nb; ++k) s += qrow[k][c];
+    const float mb = s / (float)nb;
+    float m2 = 0.f;
+    for (int k = 0; k < nb; ++k) m2 += (qrow[k][c] - mb) * (qrow[k][c] - mb);
+    colpart[(int64_t)blockIdx.x * 2 * d + c] = s;
+    colpart[(int64_t)blockIdx.x * 2 * d + d + c] = m2;
+  }
+  if (tid == 0) {
     for (int k = 0; k < 3; ++k) part[(int64_t)blockIdx.x * 4 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
   }
 }
 
-// dZ[r] = sum_c K[c][r] * G[c][r], and G is zeroed behind the read so the next
-// step's atomics start from zero without a memset (Kc is zeroed by the first
-// backward kernel).  Block 0 also reduces, in a fixed order, the per-block loss
-// partials into scal[0] = loss, scal[1] = node-feature loss, and the variance
-// monitor (pinsage_training.py:99-103): sum((h - mean)^2)/(B-1) over the B query
-// rows, merged from the per-block (sum, M2) column partials by Chan's formula
-// M2 = sum_g M2_g + n_g (mean_g - mean)^2 (deviations, never |h|^2 - |mean|^2).
-__global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G,
-                                                           const int* __restrict__ Kc, int64_t S_max,
-                                                           const int* __restrict__ nS, int d,
-                                                           float* __restrict__ dZ,
-                                                           const float* __restrict__ part, int nparts,
-                                                           const float* __restrict__ colpart, int B,
-                                                           float* __restrict__ scal) {
-  const int64_t S = *nS;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / d;
-    float v = 0.f;
-    for (int c = 0; c < 3; ++c) {
-      const int k = Kc[c * S_max + r];
-      if (k) {
-        v += (float)k * G[c * S_max * d + e];
-        G[c * S_max * d + e] = 0.f;
-      }
-    }
-    dZ[e] = v;
-  }
-  if (blockIdx.x != 0) return;
-  // fixed-order reductions with every thread's loads in flight together
+// The step's monitors (pinsage_training.py:200-212): one block reduces, in a
+// fixed order, the per-block partials of the loss kernel into scal[0] = loss,
+// scal[1] = node-feature loss, scal[2] = sum |h_q|^2 and the variance
+// (pinsage_training.py:99-103) -- Chan's merge of the per-block (sum, M2)
+// column partials, M2 = sum_g M2_g + n_g (mean_g - mean)^2 (deviations, never
+// |h|^2 - |mean|^2).  Nothing in the backward reads these: the engine runs it
+// beside the backward.
+__global__ __launch_bounds__(1024) void loss_monitor_kernel(const float* __restrict__ part,
+                                                            int nparts,
+                                                            const float* __restrict__ colpart,
+                                                            int d, int B, float* __restrict__ scal) {
   __shared__ float cs[1024];
+  __shared__ float mean_s[1024];
   __shared__ float wred[16][3];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   float l = 0.f, nf = 0.f, sq = 0.f;
@@ -796,14 +823,12 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
     wred[wv][2] = sq;
   }
   __syncthreads();
-  __shared__ float mean_s[1024];
   if (t < d) {
     float tot = 0.f;
     for (int q = 0; q < ng; ++q) tot += cs[q * d + t];
     mean_s[t] = tot / (float)B;
   }
   __syncthreads();
-  // second pass: Chan's merge of the block partials around the batch mean
   float m2 = 0.f;
   if (grp < ng) {
     const float m = mean_s[c];
@@ -814,6 +839,7 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
     }
   }
   m2 = wave_sum(m2);
+  __syncthreads();
   if (lane == 0) cs[wv] = m2;
   __syncthreads();
   if (t == 0) {
@@ -828,6 +854,29 @@ __global__ __launch_bounds__(1024) void loss_finish_kernel(float* __restrict__ G
     scal[1] = nfs / (float)B;
     scal[2] = sqs;
     scal[3] = ms / (float)(B - 1);
+  }
+}
+
+// dZ[r] = sum_c K[c][r] * G[c][r], and G is zeroed behind the read (the unfused
+// head's path; the fused head backward forms dZ itself).  Kc is zeroed by the
+// first backward kernel.
+__global__ __launch_bounds__(1024) void dz_combine_kernel(float* __restrict__ G,
+                                                          const int* __restrict__ Kc, int64_t S_max,
+                                                          const int* __restrict__ nS, int d,
+                                                          float* __restrict__ dZ) {
+  const int64_t S = *nS;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < S * d;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / d;
+    float v = 0.f;
+    for (int c = 0; c < 3; ++c) {
+      const int k = Kc[c * S_max + r];
+      if (k) {
+        v += (float)k * G[c * S_max * d + e];
+        G[c * S_max * d + e] = 0.f;
+      }
+    }
+    dZ[e] = v;
   }
 }
 
@@ -995,14 +1044,19 @@ int launch_gather_out(const float* Z, int d, const int32_t* pr, int64_t n, float
   return kOk;
 }
 
+// autograd: the output rows' cotangents go into the loss's accumulators (G slab
+// 0, K slab 0); dZ = K * G is formed by the fused head backward (or here, for
+// the unfused head: scale = true)
 int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, const int* nS,
-                        int64_t S_max, float* G, int* Kc, float* dZ, hipStream_t st) {
+                        int64_t S_max, float* G, int* Kc, float* dZ, bool scale, hipStream_t st) {
   hipLaunchKernelGGL(dout_accum_kernel, dim3(grid_for(n * d, 256)), dim3(256), 0, st, dout, d, pr, n,
                      G, Kc);
   PS_CHECK_LAUNCH();
-  hipLaunchKernelGGL(dz_scale_kernel, dim3(grid_for(S_max * d, 256)), dim3(256), 0, st, G, Kc, d, nS,
-                     dZ);
-  PS_CHECK_LAUNCH();
+  if (scale) {
+    hipLaunchKernelGGL(dz_scale_kernel, dim3(grid_for(S_max * d, 256)), dim3(256), 0, st, G, Kc, d, nS,
+                       dZ);
+    PS_CHECK_LAUNCH();
+  }
   return kOk;
 }
 
@@ -1150,16 +1204,38 @@ int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int
 int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float margin,
                 const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
                 int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
-                float* hinge, hipStream_t st) {
-  // G and Kc are zero on entry (init_workspace; then loss_finish / the first
-  // backward kernel leave them zero)
+                float* hinge, bool combine_dz, hipStream_t st) {
+  // G and Kc are zero on entry (init_workspace; then the head backward (or
+  // dz_combine) and the first backward kernel leave them zero)
+  PS_REQUIRE(d <= 256, kErrArg, "loss: out_dim must be <= 256");
+  PS_REQUIRE(d <= 1024 && 1024 % d == 0, kErrArg, "loss: out_dim must divide 1024");
   const int nblk = ceil_div(B, 4);
-  hipLaunchKernelGGL(loss_triple_kernel, dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, margin,
-                     feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge);
+  const int fpl = d_in <= 128 ? 2 : d_in <= 256 ? 4 : 8;
+#define PS_LOSS(ZP, FP)                                                                           \
+  hipLaunchKernelGGL((loss_triple_kernel<ZP, FP>), dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, \
+                     margin, feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge)
+  if (d <= 128) {
+    if (fpl == 2) PS_LOSS(2, 2);
+    else if (fpl == 4) PS_LOSS(2, 4);
+    else PS_LOSS(2, 8);
+  } else {
+    if (fpl == 2) PS_LOSS(4, 2);
+    else if (fpl == 4) PS_LOSS(4, 4);
+    else PS_LOSS(4, 8);
+  }
+#undef PS_LOSS
   PS_CHECK_LAUNCH();
-  PS_REQUIRE(d <= 1024, kErrArg, "loss: out_dim must be <= 1024");
-  hipLaunchKernelGGL(loss_finish_kernel, dim3(grid_for(S_max * d, 1024, 256)), dim3(1024), 0, st, G,
-                     Kc, S_max, nS, d, dZ, part, nblk, colpart, B, scal);
+  if (combine_dz) {
+    hipLaunchKernelGGL(dz_combine_kernel, dim3(grid_for(S_max * d, 1024, 256)), dim3(1024), 0, st, G,
+                       Kc, S_max, nS, d, dZ);
+    PS_CHECK_LAUNCH();
+  }
+  return kOk;
+}
+
+int launch_loss_monitor(const float* part, int nparts, const float* colpart, int d, int B, float* scal,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(loss_monitor_kernel, dim3(1), dim3(1024), 0, st, part, nparts, colpart, d, B, scal);
   PS_CHECK_LAUNCH();
   return kOk;
 }

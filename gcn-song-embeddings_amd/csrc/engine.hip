@@ -53,7 +53,12 @@ int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const i
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
-                float*, hipStream_t);
+                float*, bool, hipStream_t);
+int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
+int agg_w_supported(int64_t, int64_t, int64_t, int64_t);
+int launch_agg_w(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*,
+                 const float*, int, const int*, int64_t, const float*, const float*, float*, float*,
+                 float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
                 hipStream_t);
 int csr_prepare();
@@ -62,11 +67,11 @@ int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t
 int launch_gather_out(const float*, int, const int32_t*, int64_t, float*, hipStream_t);
 int launch_head_fwd(const float*, int, const int*, int64_t, const float*, const float*,
                     const float*, float*, float*, hipStream_t);
-int launch_head_bwd(const float*, int, const int*, int64_t, const float*, const float*,
-                    const float*, const float*, const float*, float*, float*, float*, int,
-                    const int*, int*, int64_t, hipStream_t);
+int launch_head_bwd(float*, int*, int64_t, float*, int, const int*, int64_t, const float*,
+                    const float*, const float*, const float*, const float*, float*, float*,
+                    hipStream_t);
 int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
-                        int*, float*, hipStream_t);
+                        int*, float*, bool, hipStream_t);
 
 struct EngineConfig {
   int64_t n_items;   // rows of the feature table (track universe)
@@ -119,6 +124,8 @@ struct Engine {
   int side_grid = getenv("PINSAGE_SIDE_GRID") ? atoi(getenv("PINSAGE_SIDE_GRID")) : 0;
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
+  // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B)
+  bool fused_aggw = !getenv("PINSAGE_FUSED_AGGW") || atoi(getenv("PINSAGE_FUSED_AGGW")) != 0;
   std::vector<TimingSite> sites;
   // per-site GEMM tile / stream-K / split-K choices (pinsage_engine_set_gemm_choice:
   // set by the trainer's in-context tuner; absent = the launcher's size model)
@@ -431,6 +438,20 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
                              prev ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr, (int)c.out,
                              prev ? cnt(*prev) : nullptr, st));
   }
+  // the transposes of the neighbour slots (CSR of slot occurrences by q row,
+  // the aggregation backward's plan) depend only on the frontier: built here,
+  // on the frontier's stream -- for a trainer's look-ahead frontier that is
+  // beside the previous step, so the backward never waits for them
+  PS_TRY(csr_prepare());
+  for (int l = Lc - 1; l >= 0; --l) {
+    LayerBuf& lb = E.L[(size_t)l];
+    Timed tc(E, lname("fwd.csr", l), st);
+    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
+                            at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
+                            at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
+                            at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), at<int2>(ws, lb.split),
+                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, st));
+  }
   return kOk;
 }
 
@@ -470,6 +491,15 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(ensure_streams(E));
       PS_TRY(dep(E, st, E.fork.stream));
       PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
+    }
+    if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {
+      // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
+      Timed taw(E, lname("fwd.aggw", l), st);
+      PS_TRY(launch_agg_w(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q),
+                          (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S),
+                          lb.S.cap, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
+                          at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
+      continue;
     }
     Timed t_agg(E, lname("fwd.agg", l), st);
     PS_TRY(launch_agg(at<float>(ws, lb.q), (int)c.hid, at<int32_t>(ws, lb.loc),
@@ -658,26 +688,10 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   // Q0 go beside the chain's tail (the transposed aggregation and dQ0, which
   // do not need them); the other weight gradients stay on the chain
   hipStream_t s_wg0 = E.stream_mode == 4 ? E.side[1] : s_wg;
-  // the transposes of the neighbour slots depend only on the forward: build
-  // them beside the head backward; events mark each layer's CSR done
-  PS_TRY(dep(E, st, s_csr));
-  std::vector<hipEvent_t> csr_done((size_t)Lc);
-  for (int l = Lc - 1; l >= 0; --l) {
-    LayerBuf& lb = E.L[(size_t)l];
-    Timed tc(E, lname("bwd.csr", l), s_csr);
-    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
-                            at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
-                            at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
-                            at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), at<int2>(ws, lb.split),
-                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), hd, s_csr));
-    tc.stop();
-    csr_done[(size_t)l] = E.ev[(size_t)(E.ev_next++ % kEvents)];
-    PS_CHECK_HIP(hipEventRecord(csr_done[(size_t)l], s_csr));
-  }
+  // the CSR transposes were built with the frontier (engine_frontier)
   // weight gradients run on s_wg, each forked once its inputs exist on st
   Timed t_hb(E, "bwd.head", st);
-  PS_TRY(dep(E, st, s_wg));  // dZ, H1 ready: dG2 beside the head backward
-  {
+  auto wgrad_g2 = [&]() -> int {  // dG2 = dZ^T H1 beside the chain
     Timed tw(E, "bwd.wgrad.g2", s_wg);
     WGrad w;
     w.A = at<float>(ws, E.dZ);
@@ -691,17 +705,25 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.K_hint = top.S.hint;
     w.dst = gr + E.pG2w;
     w.ld_dst = o;
-    PS_TRY(weight_grad(E, ws, w, s_wg, "bwd.wgrad.g2", nullptr, nullptr, false, s_wg != st));
+    return weight_grad(E, ws, w, s_wg, "bwd.wgrad.g2", nullptr, nullptr, false, s_wg != st);
+  };
+  if (!E.fused_head) {  // dZ exists (dz_combine): fork dG2 before the head backward
+    PS_TRY(dep(E, st, s_wg));
+    PS_TRY(wgrad_g2());
   }
   // dP1 = (dZ G2) * lrelu'(H1), dY_top = dP1 G1 and the top layer's
   // normalisation backward (dp_top) in one kernel, which also zeroes the
   // loss's multiplicity counters (the dY scatter-add targets of the layers
   // below were zeroed by the forward's layer_prep)
   if (E.fused_head) {
-    PS_TRY(launch_head_bwd(at<float>(ws, E.dZ), o, cnt(top.S), top.S.cap, at<float>(ws, E.H1),
-                           E.params + E.pG1w, E.params + E.pG2w, at<float>(ws, top.y),
-                           at<float>(ws, top.nrm), at<float>(ws, E.dP1), at<float>(ws, top.dp),
-                           nullptr, o, nullptr, at<int>(ws, E.Kc), 3 * top.S.cap, st));
+    // the head backward forms dZ = sum_c K[c] G[c] from the loss's
+    // accumulators as it loads its rows (and zeroes them), writing dZ for dG2
+    PS_TRY(launch_head_bwd(at<float>(ws, E.G), at<int>(ws, E.Kc), top.S.cap, at<float>(ws, E.dZ), o,
+                           cnt(top.S), top.S.cap, at<float>(ws, E.H1), E.params + E.pG1w,
+                           E.params + E.pG2w, at<float>(ws, top.y), at<float>(ws, top.nrm),
+                           at<float>(ws, E.dP1), at<float>(ws, top.dp), st));
+    PS_TRY(dep(E, st, s_wg));
+    PS_TRY(wgrad_g2());
   } else {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
@@ -829,7 +851,6 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
                          E.n_params - l0.pWw, adam->coef, adam->beta1, adam->beta2, adam->eps,
                          s_w));
     }
-    PS_CHECK_HIP(hipStreamWaitEvent(st, csr_done[(size_t)l], 0));
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
                             at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
                             at<int>(ws, lb.off), at<int32_t>(ws, lb.occ), at<float>(ws, lb.wloc), T,
@@ -886,7 +907,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
                          qs != st));
     }
   }
-  // every gradient is written once the side streams drain into st
+  // every gradient is written once the side streams drain into st (side[0]
+  // also carries the loss monitors, pinsage_engine_loss)
+  PS_TRY(dep(E, E.side[0], st));
   PS_TRY(dep(E, s_csr, st));
   PS_TRY(dep(E, s_wg, st));
   if (s_wg0 != s_wg) PS_TRY(dep(E, s_wg0, st));
@@ -1128,13 +1151,23 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
     return kErrArg;
   }
   LayerBuf& top = E->L.back();
-  Timed t(*E, "loss", (hipStream_t)stream);
-  return launch_loss(at<float>(ws, E->Z), (int)c.out, at<int32_t>(ws, E->pos_rank), (int)batch_size,
-                     margin, with_monitors ? E->feats : nullptr, E->ld_f, (int)c.d_in,
-                     at<int64_t>(ws, E->ids), at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap,
-                     at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
-                     at<float>(ws, E->varpart), at<float>(ws, E->scal), at<float>(ws, E->hinge),
-                     (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  {
+    Timed t(*E, "loss", st);
+    PS_TRY(launch_loss(at<float>(ws, E->Z), (int)c.out, at<int32_t>(ws, E->pos_rank), (int)batch_size,
+                       margin, with_monitors ? E->feats : nullptr, E->ld_f, (int)c.d_in,
+                       at<int64_t>(ws, E->ids), at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap,
+                       at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
+                       at<float>(ws, E->varpart), at<float>(ws, E->scal), at<float>(ws, E->hinge),
+                       !E->fused_head, st));
+  }
+  // the monitors (loss, node-feature loss, variance scalars) beside the
+  // backward, on side stream 0, joined at the backward's end
+  PS_TRY(ensure_streams(*E));
+  PS_TRY(dep(*E, st, E->side[0]));
+  Timed tm(*E, "loss.monitor", E->side[0]);
+  return launch_loss_monitor(at<float>(ws, E->part), (int)ceil_div(batch_size, 4), at<float>(ws, E->varpart),
+                             (int)c.out, (int)batch_size, at<float>(ws, E->scal), E->side[0]);
 }
 
 int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,
@@ -1143,7 +1176,8 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
   LayerBuf& top = E->L.back();
   return launch_dz_from_dout(dout, (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
                              at<int>(ws, top.S.count), top.S.cap, at<float>(ws, E->G),
-                             at<int>(ws, E->Kc), at<float>(ws, E->dZ), (hipStream_t)stream);
+                             at<int>(ws, E->Kc), at<float>(ws, E->dZ), !E->fused_head,
+                             (hipStream_t)stream);
 }
 
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream) {

@@ -659,6 +659,8 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.epi != kEpiPartial || (!p.M_dev && !p.c_idx), kErrArg,
              "gemm: split-K partials need a static M");
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
+  PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
+             "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
   int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, Kmax, splits);

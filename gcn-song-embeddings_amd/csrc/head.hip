@@ -142,42 +142,69 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   }
 }
 
-// From dZ: dP1 = (dZ G2) * lrelu'(H1); dY = dP1 G1; then the top conv layer's
-// normalisation backward (y = u / ||u||, u = lrelu(pre)):
-//   dp = lrelu'(y) * (dY - y (y . dY)) / ||u||
-// Also zeroes z[0 .. *z_rows * z_n) (the next layer's scatter-add target) and
-// zi[0 .. zi_n) (the loss's multiplicity counters) grid-wide, as the unfused
-// normalisation backward did.
+// dZ rows r0 .. r0+31 formed from the loss's accumulators, dZ[r] = sum_c K[c][r]
+// G[c][r] (c = query / positive / negative call, pinsage_training.py:186-189
+// with put_embeddings' repeated-id semantics, conv.hip loss), staged in sA and
+// written out (the dG2 weight gradient reads them).  Every K and G value of the
+// block is loaded in one round; the block then zeroes what it read (the next
+// step's loss accumulates into zeros).  K[c][r] = 0 means G[c][r] is +0, so the
+// terms it adds change nothing (bitwise the old dZ = sum over k != 0).
+__device__ __forceinline__ void head_load_dz(float* sA, float* __restrict__ G, int* __restrict__ Kc,
+                                             int64_t S_max, float* __restrict__ dZ, int64_t r0, int64_t R,
+                                             int o, int tid) {
+  constexpr int NI = kHeadRows * (kHeadDim / 4) / 256;
+  float4 g[3][NI];
+  int k[3][NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
+    const bool ok = r0 + row < R && c < o;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      k[q][j] = ok ? Kc[q * S_max + r0 + row] : 0;
+      g[q][j] = ok ? *reinterpret_cast<const float4*>(G + ((int64_t)q * S_max + r0 + row) * o + c)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (k[q][j]) {
+        const float kf = (float)k[q][j];
+        v.x += kf * g[q][j].x;
+        v.y += kf * g[q][j].y;
+        v.z += kf * g[q][j].z;
+        v.w += kf * g[q][j].w;
+        *reinterpret_cast<float4*>(G + ((int64_t)q * S_max + r0 + row) * o + c) =
+            make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    *reinterpret_cast<float4*>(sA + row * kHeadLd + c) = v;
+    if (r0 + row < R && c < o) *reinterpret_cast<float4*>(dZ + (r0 + row) * o + c) = v;
+  }
+}
+
+// From the loss's accumulators: dZ (above); dP1 = (dZ G2) * lrelu'(H1); dY =
+// dP1 G1; then the top conv layer's normalisation backward (y = u / ||u||,
+// u = lrelu(pre)):  dp = lrelu'(y) * (dY - y (y . dY)) / ||u||.  The block
+// zeroes the multiplicity counters of its rows once every thread has read them.
 __global__ __launch_bounds__(256) void head_bwd_kernel(
-    const float* __restrict__ dZ, int o, const int* __restrict__ nrows, const float* __restrict__ H1,
-    const float* __restrict__ G1w, const float* __restrict__ G2w, const float* __restrict__ y,
-    const float* __restrict__ nrm, float* __restrict__ dP1, float* __restrict__ dp,
-    float* __restrict__ z, int z_n, const int* __restrict__ z_rows, int* __restrict__ zi,
-    int64_t zi_n) {
+    float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ dZ, int o,
+    const int* __restrict__ nrows, const float* __restrict__ H1, const float* __restrict__ G1w,
+    const float* __restrict__ G2w, const float* __restrict__ y, const float* __restrict__ nrm,
+    float* __restrict__ dP1, float* __restrict__ dp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* sA = lds;
   float* sW2 = sA + kHeadRows * kHeadLd;
   float* sW1 = sW2 + kHeadDim * kHeadLd;
   float* red = sW1 + kHeadDim * kHeadLd;  // [4 waves][32 rows] partial dots
   const int tid = threadIdx.x;
-  // z / zi zeroing (no consumer inside this kernel) comes last: the row chain
-  // is the critical path
-  auto zero_tail = [&]() {
-    const int64_t gt = (int64_t)blockIdx.x * 256 + tid, gs = (int64_t)gridDim.x * 256;
-    if (z) {
-      const int64_t zn4 = (int64_t)(*z_rows) * z_n / 4;
-      float4* z4 = reinterpret_cast<float4*>(z);
-      for (int64_t i = gt; i < zn4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (zi)
-      for (int64_t i = gt; i < zi_n; i += gs) zi[i] = 0;
-  };
   const int64_t R = *nrows;
   const int64_t r0 = (int64_t)blockIdx.x * kHeadRows;
-  if (r0 >= R) {
-    zero_tail();
-    return;
-  }
+  if (r0 >= R) return;
   const int lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = 32 * w, col = n0 + l32;
   // this lane's H1 (mask) and y values, fetched beside the staging loads
@@ -189,10 +216,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     hv[r] = ok ? H1[(r0 + row) * o + col] : 0.f;
     yv[r] = ok ? y[(r0 + row) * o + col] : 0.f;
   }
-  head_load_rows(sA, dZ, r0, R, o, tid);
+  head_load_dz(sA, G, Kc, S_max, dZ, r0, R, o, tid);
   head_load_weight(sW2, G2w, o, tid);
   head_load_weight(sW1, G1w, o, tid);
   __syncthreads();
+  if (tid < 3 * kHeadRows) {  // every K of the block's rows has been read
+    const int q = tid / kHeadRows, row = tid % kHeadRows;
+    if (r0 + row < R) Kc[q * S_max + r0 + row] = 0;
+  }
   f32x16 acc = head_mm<false>(sA, sW2, n0, l32, h);
   __syncthreads();  // every wave is done reading dZ from sA
 #pragma unroll
@@ -226,7 +257,6 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       dp[(r0 + row) * o + col] = lrelu_grad(yv[r]) * (acc[r] - yv[r] * dot) * inv;
     }
   }
-  zero_tail();
 }
 
 constexpr size_t kHeadFwdLds = (size_t)(kHeadRows + 2 * kHeadDim) * kHeadLd * 4;
@@ -258,17 +288,14 @@ int launch_head_fwd(const float* y, int o, const int* nrows, int64_t max_rows, c
   return kOk;
 }
 
-int launch_head_bwd(const float* dZ, int o, const int* nrows, int64_t max_rows, const float* H1,
-                    const float* G1w, const float* G2w, const float* y, const float* nrm,
-                    float* dP1, float* dp, float* z, int z_n, const int* z_rows, int* zi,
-                    int64_t zi_n, hipStream_t st) {
+int launch_head_bwd(float* G, int* Kc, int64_t S_max, float* dZ, int o, const int* nrows,
+                    int64_t max_rows, const float* H1, const float* G1w, const float* G2w,
+                    const float* y, const float* nrm, float* dP1, float* dp, hipStream_t st) {
   PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
-  PS_REQUIRE(!z || z_n % 4 == 0, kErrArg, "head: zeroed rows must be a multiple of 4 wide");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
   hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                     kHeadBwdLds, st, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp, z, z_n, z_rows, zi,
-                     zi_n);
+                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -455,9 +455,11 @@ class _FusedStep:
         with HIP events on its launch stream (kernels back to back behind a
         stream hold), and the fastest is kept (pinsage_engine_set_gemm_choice).
         Probe k sets candidate k at every site at once (their interplay is second
-        order).  The probes rerun this step's frontier, layers, loss and
-        backward WITHOUT the optimizer: parameters and Adam state are untouched,
-        and every choice computes the same products (speed only)."""
+        order).  The probes run before the step's own forward (the caller runs
+        the real step afterwards, so its outputs, gradients and workspace are
+        the step's): this step's frontier, layers, loss and backward WITHOUT
+        the optimizer -- parameters and Adam state are untouched, and every
+        choice computes the same products (speed only)."""
         e = self.runner.engine
         L = nat.lib()
         sites = self._gemm_sites()
@@ -620,11 +622,16 @@ class _FusedStep:
             self._slot_write_ids(k, self.slot_ids, batch, B)
             self._stage(B, self.slot_ids, p, p)
             self._frontier(B, p)
+            if self.autotune and self.tuned_choices is None:
+                # the size hints come from this batch's frontier, then the
+                # tuner's probes; the step itself runs after them
+                if not self._tuned:
+                    self.runner.engine.tune(self.wss[p])
+                    self._tuned = True
+                self._autotune(B, p)
             self._main(B, p, with_adam=not self.dist)
             self._publish(p)
             self.pending = [None, None]
-            if self.autotune and self._tuned and self.tuned_choices is None:
-                self._autotune(B, p)
             if self.use_graph and self._tuned:
                 self._capture(B, sig)
         if self.dist:

@@ -20,11 +20,11 @@ def _vp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def _gemm(M, N, K, ak, bk, A, a_idx, B, C, bias=None, act=0, epi=0, splits=1, cfg=-1, sk=0):
+def _gemm(M, N, K, ak, bk, A, a_idx, B, C, bias=None, act=0, epi=0, splits=1, cfg=-1, sk=0, b_idx=None):
     import _native as nat
     lib = nat.lib()
     rc = lib.pinsage_gemm_ex(M, N, K, ak, bk, _vp(A), A.shape[1], _vp(a_idx), _vp(B), B.shape[1],
-                             None, _vp(C), C.shape[-1], _vp(bias), act, epi, splits, cfg, sk,
+                             _vp(b_idx), _vp(C), C.shape[-1], _vp(bias), act, epi, splits, cfg, sk,
                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     nat.check(rc, "gemm_ex")
 
@@ -59,11 +59,20 @@ SHAPES = [  # M, N, K: ragged M / K tails, N = 128 and multi-tile N, long K
 
 
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("sk", [0, 1])
 def test_gemm_layouts_configs_schedules(ak, bk, cfg, sk):
+    """Every block-tile config (0: 128x128x16, 1: 64x128x32, 2: 32x128x32,
+    3: 64x128x16 three per CU, 4: four per CU -- K-major operands only, other
+    layouts are refused) under both schedules."""
     if sk and cfg == 0:
         pytest.skip("stream-K runs the 64- and 32-row tiles")
+    if cfg == 4 and not (ak and bk):
+        A = torch.randn(64, 64, device="cuda")
+        C = torch.empty(64, 64, device="cuda")
+        with pytest.raises(RuntimeError, match="cfg 4"):
+            _gemm(64, 64, 64, ak, bk, A, None, A, C, cfg=4, sk=sk)
+        return
     g = torch.Generator(device="cuda").manual_seed(1234 + 10 * cfg + sk)
     for M, N, K in SHAPES:
         if not ak and M % 4:
@@ -127,3 +136,25 @@ def test_split_k_partials():
     torch.cuda.synchronize()
     r = A.double().t() @ B.double()
     assert _rel(C.sum(0), r) < REL_TOL
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("S", [1, 2, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("shape", [(512, 512, 10552), (128, 640, 1500), (128, 128, 1536), (512, 128, 2600)])
+def test_weight_gradient_split_k_every_config(cfg, S, shape):
+    """The weight-gradient form the engine tunes over (pinsage_engine_set_gemm_choice):
+    M-major A (dpq / dp), N-major B with gathered k-rows (h[q_src], h[self]), split-K
+    slabs summed afterwards, for every config and split count (empty splits
+    included: S > K / BK)."""
+    M, N, K = shape
+    g = torch.Generator(device="cuda").manual_seed(17 + cfg + 10 * S)
+    A = torch.randn(K, M, device="cuda", generator=g)
+    rows = 3 * K
+    B = torch.randn(rows, N, device="cuda", generator=g)
+    b_idx = torch.randint(0, rows, (K,), device="cuda", generator=g, dtype=torch.int32)
+    C = torch.full((S, M, N), float("nan"), device="cuda")
+    _gemm(M, N, K, 0, 0, A, None, B, C, epi=3, splits=S, cfg=cfg, b_idx=b_idx)
+    torch.cuda.synchronize()
+    r = A.double().t() @ B.double()[b_idx.long()]
+    assert torch.isfinite(C).all()
+    assert _rel(C.sum(0), r) < REL_TOL, _rel(C.sum(0), r)
