@@ -64,6 +64,7 @@ _SIGS = {
     "pinsage_ppr_topk_workspace": (i64, [i64, i64, ctypes.c_int]),
     "pinsage_engine_set_gemm_choice": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                                       ctypes.c_int]),
+    "pinsage_engine_set_layer_table": (ctypes.c_int, [vp, i64, vp, vp, i64]),
     "pinsage_ppr_topk": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, i64, vp, u64, u32, i64, vp, i64,
                                         vp, vp, vp, vp, i64, vp]),
     "pinsage_visit_dense": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, vp]),

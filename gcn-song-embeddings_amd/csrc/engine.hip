@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -100,6 +101,11 @@ struct LayerBuf {
   int64_t max_chunks = 0, max_split = 0;
   // parameter offsets (floats) into the flat param / grad buffers
   int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
+  // this layer's own neighbourhood table (pinsage_engine_set_layer_table: the
+  // on-the-fly sampler gives every layer its own draws); null = the engine's
+  const int32_t* nb_tab = nullptr;
+  const float* wn_tab = nullptr;
+  int64_t ld_tab = 0;
 };
 
 // Optional HIP-event timing of launch sites on the launch stream (bench only).
@@ -126,7 +132,9 @@ struct Engine {
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B)
   bool fused_aggw = !getenv("PINSAGE_FUSED_AGGW") || atoi(getenv("PINSAGE_FUSED_AGGW")) != 0;
-  std::vector<TimingSite> sites;
+  // a deque: Timed scopes nest and hold pointers to their sites, which must
+  // stay valid when an inner scope appends a new site
+  std::deque<TimingSite> sites;
   // per-site GEMM tile / stream-K / split-K choices (pinsage_engine_set_gemm_choice:
   // set by the trainer's in-context tuner; absent = the launcher's size model)
   struct GemmChoice {
@@ -415,7 +423,9 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
                         pref(top.S), mem(top.S), cnt(top.S), st));
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
-    PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, E.nb, E.ldT, T, n, st));
+    const int32_t* nb_l = lb.nb_tab ? lb.nb_tab : E.nb;
+    const int64_t ld_l = lb.nb_tab ? lb.ld_tab : E.ldT;
+    PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, nb_l, ld_l, T, n, st));
     PS_TRY(launch_set_finalize(bits(lb.N), bits(lb.N), nullptr, n, bsum, pref(lb.N), mem(lb.N),
                                cnt(lb.N), st));
     if (l > 0) {
@@ -431,7 +441,8 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
     const bool is_top = l == Lc - 1;  // the top layer also ranks the batch positions
     PS_TRY(launch_layer_prep(mem(lb.S), cnt(lb.S), lb.S.cap, mem(lb.N), cnt(lb.N), lb.N.cap,
                              bits(lb.N), pref(lb.N), prev ? bits(*prev) : nullptr,
-                             prev ? pref(*prev) : nullptr, E.nb, E.wn, E.ldT, T,
+                             prev ? pref(*prev) : nullptr, lb.nb_tab ? lb.nb_tab : E.nb,
+                             lb.nb_tab ? lb.wn_tab : E.wn, lb.nb_tab ? lb.ld_tab : E.ldT, T,
                              at<int32_t>(ws, lb.self_src), at<int32_t>(ws, lb.q_src),
                              at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), bits(top.S),
                              pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank),
@@ -1090,6 +1101,21 @@ int pinsage_engine_set_gemm_choice(pinsage_engine* e, const char* site, int cfg,
   }
   if (cfg < 0 && stream_k < 0 && splits == 0) E->choice.erase(site);
   else E->choice[site] = Engine::GemmChoice{cfg, stream_k, splits};
+  return kOk;
+}
+
+int pinsage_engine_set_layer_table(pinsage_engine* e, int64_t layer, const int32_t* nb,
+                                   const float* wn, int64_t ld) {
+  Engine* E = reinterpret_cast<Engine*>(e);
+  if (!E || layer < 0 || layer >= E->cfg.n_layers || ((nb == nullptr) != (wn == nullptr)) ||
+      (nb && ld < E->cfg.T)) {
+    set_error("engine_set_layer_table: bad argument");
+    return kErrArg;
+  }
+  LayerBuf& lb = E->L[(size_t)layer];
+  lb.nb_tab = nb;
+  lb.wn_tab = wn;
+  lb.ld_tab = ld;
   return kOk;
 }
 

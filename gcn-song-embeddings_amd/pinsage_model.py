@@ -351,6 +351,38 @@ def relevant_nodes_per_layer(g, n_items, nodeset, n_layers, n_hops, alpha, T):
     return S
 
 
+def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
+    """relevant_nodes_per_layer (pinsage_model.py:142-154) for the engine: top
+    layer first, each layer's nodeset is walked (the fused walk + top-k
+    kernel: the same draws as the reference, in nodeset order) and its top-T
+    rows land in that layer's own device table, indexed by node id.  A node
+    repeated in the top nodeset keeps its LAST occurrence's row: the
+    reference's put_embeddings lets the last write win (pinsage_model.py:29),
+    so the output rows of every repeat are the last one's.  Returns the
+    per-layer (nb int32 [n_items][T], wn f32 [n_items][T]) tables, index 0 =
+    bottom; only the rows of each layer's nodes are written."""
+    dev = nodeset_dev.device
+    tabs = []
+    cur = nodeset_dev
+    for _ in range(n_layers):
+        _, _, wn, nb32 = _ppr_topk_device(g, cur, n_hops, alpha, int(T), t_norm=int(T), want_ref=False)
+        if nb32.numel() and int(nb32.max()) >= n_items:
+            # the reference's h[nb] (features of tracks only) raises here
+            raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
+                             "zero-weight tail: the reference's h[nb] raises IndexError)")
+        uniq, inv = torch.unique(cur, return_inverse=True)
+        pos = torch.arange(cur.shape[0], device=dev)
+        last = torch.full((uniq.shape[0],), -1, dtype=torch.int64, device=dev)
+        last.scatter_reduce_(0, inv, pos, reduce="amax")
+        nbt = torch.empty((n_items, int(T)), dtype=torch.int32, device=dev)
+        wnt = torch.empty((n_items, int(T)), dtype=torch.float32, device=dev)
+        nbt[uniq] = nb32[last]
+        wnt[uniq] = wn[last]
+        tabs.insert(0, (nbt, wnt))
+        cur = _frontier_step(uniq, nbt, int(T), n_items)
+    return tabs
+
+
 class _DeviceTable:
     """Device mirror of a precomputed (weights, nodes) table: first T columns,
     nodes int32, weights f32 normalised by their f64 row sum."""
@@ -472,6 +504,11 @@ class PinSageModel(nn.Module):
         self.G1.bias.data.fill_(0.3)
         self.G2 = nn.Linear(self.out_dim, self.out_dim, bias=False)
         torch.nn.init.xavier_uniform_(self.G2.weight)
+        # the reference's forward carries the on-the-fly sampler commented out
+        # (pinsage_model.py:247-249): True samples every layer's neighbourhoods
+        # per call (relevant_nodes_per_layer) instead of reading the table;
+        # nbhds=None (no table) implies it
+        self.sample_on_the_fly = nbhds is None
         self._runner = None
         if torch.cuda.is_available():
             self.to(nat.device())
@@ -604,11 +641,31 @@ class _EngineRunner:
 
     def table(self, nbhds):
         m = self.model
+        if m.sample_on_the_fly:
+            return None
         key = (id(nbhds[0]), id(nbhds[1]), int(m.T))
         if key != self._table_key:
             self._table = _DeviceTable(nbhds, m.T, m.n_items, self.dev)
             self._table_key = key
         return self._table
+
+    def fly_tables(self, ids):
+        """Per-layer tables of this call's on-the-fly draws (None in table mode)."""
+        m = self.model
+        if not m.sample_on_the_fly:
+            return None
+        tabs = _fly_layer_tables(m.g, m.n_items, ids, m.n_layers, m.n_hops, m.alpha, m.T)
+        self.fly_history = (getattr(self, "fly_history", []) + [tabs])[-3:]  # (tests inspect the draws)
+        return tabs
+
+    def set_layer_tables(self, tabs):
+        L = nat.lib()
+        e = self.engine
+        for l in range(self.model.n_layers):
+            nb, wn = tabs[l] if tabs is not None else (None, None)
+            nat.check(L.pinsage_engine_set_layer_table(e.h, l, nat.ptr(nb), nat.ptr(wn),
+                                                       int(nb.shape[1]) if nb is not None else 0),
+                      "set_layer_table")
 
     def ensure_engine(self, n_pos):
         m = self.model
@@ -619,11 +676,15 @@ class _EngineRunner:
             self._ws = None
         return self.engine
 
-    def bind(self, feats, table, grads=None, adam_m=None, adam_v=None):
+    def bind(self, feats, table, grads=None, adam_m=None, adam_v=None, tabs=None):
         e = self.engine
+        if table is not None:
+            nb, wn = table.nb32, table.wn
+        else:  # on-the-fly: the bottom layer's draws stand in as the engine-wide table
+            nb, wn = tabs[0]
         nat.check(nat.lib().pinsage_engine_set_tensors(
-            e.h, nat.ptr(feats), feats.stride(0), nat.ptr(table.nb32), nat.ptr(table.wn),
-            table.nb32.shape[1], nat.ptr(self.flat), nat.ptr(grads), nat.ptr(adam_m),
+            e.h, nat.ptr(feats), feats.stride(0), nat.ptr(nb), nat.ptr(wn),
+            nb.shape[1], nat.ptr(self.flat), nat.ptr(grads), nat.ptr(adam_m),
             nat.ptr(adam_v)), "engine_set_tensors")
 
     def run_forward(self, ws, ids_dev):
@@ -651,14 +712,19 @@ class _EngineRunner:
             raise IndexError(f"node ids out of range for {n_valid} items")
         self.pack()
         self.ensure_engine(n)
+        tabs = self.fly_tables(ids)
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.params())
         if need_grad:
-            out = _EngineFn.apply(self, feats, table, ids, *self.params())
+            out = _EngineFn.apply(self, feats, table, ids, tabs, *self.params())
         else:
             if self._ws is None:
                 self._ws = self.engine.new_workspace(self.dev)
-            self.bind(feats, table)
-            self.run_forward(self._ws, ids)
+            self.bind(feats, table, tabs=tabs)
+            self.set_layer_tables(tabs)
+            try:
+                self.run_forward(self._ws, ids)
+            finally:
+                self.set_layer_tables(None)
             out = torch.empty((n, m.out_dim), dtype=torch.float32, device=self.dev)
             nat.check(nat.lib().pinsage_engine_gather_output(self.engine.h, nat.ptr(self._ws), n,
                                                              nat.ptr(out), nat.stream_ptr()), "gather")
@@ -669,16 +735,21 @@ class _EngineFn(torch.autograd.Function):
     """Forward + HIP backward of PinSageModel for autograd callers."""
 
     @staticmethod
-    def forward(ctx, runner, feats, table, ids, *params):
+    def forward(ctx, runner, feats, table, ids, tabs, *params):
         e = runner.engine
         ws = e.new_workspace(runner.dev)
-        runner.bind(feats, table)
-        runner.run_forward(ws, ids)
+        runner.bind(feats, table, tabs=tabs)
+        runner.set_layer_tables(tabs)
+        try:
+            runner.run_forward(ws, ids)
+        finally:
+            runner.set_layer_tables(None)
         n = int(ids.shape[0])
         out = torch.empty((n, runner.model.out_dim), dtype=torch.float32, device=runner.dev)
         nat.check(nat.lib().pinsage_engine_gather_output(e.h, nat.ptr(ws), n, nat.ptr(out),
                                                          nat.stream_ptr()), "gather")
         ctx.runner, ctx.ws, ctx.feats, ctx.table, ctx.n = runner, ws, feats, table, n
+        ctx.tabs = tabs  # the frontier's tables stay alive with the workspace
         ctx.engine = e
         return out
 
@@ -686,7 +757,7 @@ class _EngineFn(torch.autograd.Function):
     def backward(ctx, dout):
         runner, e, ws = ctx.runner, ctx.engine, ctx.ws
         grads = torch.zeros(e.n_params, dtype=torch.float32, device=runner.dev)
-        runner.bind(ctx.feats, ctx.table, grads=grads)
+        runner.bind(ctx.feats, ctx.table, grads=grads, tabs=ctx.tabs)
         dout = dout.contiguous().to(torch.float32)
         nat.check(nat.lib().pinsage_engine_set_output_grad(e.h, nat.ptr(ws), nat.ptr(dout), ctx.n,
                                                            nat.stream_ptr()), "set_output_grad")
@@ -697,4 +768,4 @@ class _EngineFn(torch.autograd.Function):
             k = p.numel()
             out.append(grads[off:off + k].view(p.shape))
             off += k
-        return (None, None, None, None, *out)
+        return (None, None, None, None, None, *out)

@@ -629,6 +629,9 @@ class _FusedStep:
                     self.runner.engine.tune(self.wss[p])
                     self._tuned = True
                 self._autotune(B, p)
+                # the probes' backward scatter-added into this frontier's dY
+                # targets, which only the frontier (layer_prep) zeroes: redo it
+                self._frontier(B, p)
             self._main(B, p, with_adam=not self.dist)
             self._publish(p)
             self.pending = [None, None]
@@ -732,9 +735,33 @@ class PinSage:
     def train_batch(self, batch):
         """Fetch and train one batch of (q, pos, neg) triples: returns
         (loss, node_feat_loss, variance) as device scalars (no host sync)."""
+        if self.model.sample_on_the_fly:
+            return self._train_batch_fly(batch)
         if self._fused is None:
             self._fused = _FusedStep(self)
         return self._fused(batch)
+
+    def _train_batch_fly(self, batch):
+        """The reference's train_batch (pinsage_training.py:181-215) step for
+        step when the model samples on the fly (relevant_nodes_per_layer,
+        pinsage_model.py:142-154): three model calls -- each walks its own
+        nodeset's neighbourhoods, in the order q, pos, neg, consuming torch's
+        generator as the reference does -- max_margin_loss, the engine's HIP
+        backward per call (autograd), torch's Adam."""
+        batch = torch.as_tensor(batch)
+        h_q = self.model(self.features, batch[:, 0])
+        h_pos = self.model(self.features, batch[:, 1])
+        h_neg = self.model(self.features, batch[:, 2])
+        loss = max_margin_loss(h_q, h_pos, h_neg, self.margin)
+        self.optimizer.zero_grad()
+        loss.backward()
+        self.optimizer.step()
+        norm = torch.nn.functional.normalize
+        f = self.features
+        node_feat_loss = COSINE_TRIPLET_LOSS(norm(f[batch[:, 0]], dim=1), norm(f[batch[:, 1]], dim=1),
+                                             norm(f[batch[:, 2]], dim=1))
+        variance = batch_variance(h_q)
+        return loss, node_feat_loss, variance
 
     def train(self):
         from tqdm import tqdm

@@ -315,6 +315,14 @@ int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, in
 /* Expected frontier sizes (e.g. from read_counts): choose GEMM block tiles
  * that fill the chip; sizes stay device-side, hints only affect speed. */
 int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t* N);
+/* Layer `layer`'s own neighbourhood table (nb int32 / normalised weights f32,
+ * [n_items][ld], first T columns, rows of the layer's nodes used) in place of
+ * the engine-wide one from pinsage_engine_set_tensors: the on-the-fly sampler
+ * (relevant_nodes_per_layer, pinsage_model.py:142-154) draws every layer's
+ * neighbourhoods separately.  nb = wn = null restores the engine-wide table.
+ * Read when a frontier is enqueued (pinsage_engine_forward / _frontier). */
+int pinsage_engine_set_layer_table(pinsage_engine* e, int64_t layer, const int32_t* nb,
+                                   const float* wn, int64_t ld);
 /* Per-site GEMM choice (a tuner measures the sites in context and fixes them):
  * site names as the timing sites -- fwd.q_gemm.lN, fwd.w_gemm.lN, bwd.dcat.lN,
  * bwd.dh.lN (block tile config cfg 0..3, stream_k 0/1), bwd.w_wgrad.lN,

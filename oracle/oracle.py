@@ -249,9 +249,24 @@ def conv_layer(p, i, h, nodes, nb, w, in_dim):
     return z / z.norm(dim=1, keepdim=True)
 
 
-def model_forward(p, feats, nodeset, n_layers, T, w_table, nb_table, out_dim):
-    """PinSageModel.forward (pinsage_model.py:246-265) on torch-CPU tensors."""
-    layers = frontier(np.asarray(nodeset), n_layers, T, w_table, nb_table)
+def relevant_nodes_fly(indptr, indices, n_all, nodeset, n_layers, n_hops, alpha, T, mt):
+    """relevant_nodes_per_layer (pinsage_model.py:142-154): every layer's
+    nodeset walked with the MT19937 stream (top layer first, draws in nodeset
+    order), index 0 = bottom."""
+    S = []
+    cur = np.asarray(nodeset, np.int64)
+    for _ in range(n_layers):
+        w, nb = sample_neighborhood_topt(indptr, indices, n_all, cur, n_hops, alpha, T, mt)
+        S.insert(0, (cur, w, nb))
+        cur = np.unique(np.concatenate([nb.reshape(-1), cur]))
+    return S
+
+
+def model_forward(p, feats, nodeset, n_layers, T, w_table, nb_table, out_dim, layers=None):
+    """PinSageModel.forward (pinsage_model.py:246-265) on torch-CPU tensors;
+    `layers` (relevant_nodes_fly) replaces the table's frontier (:247-249)."""
+    if layers is None:
+        layers = frontier(np.asarray(nodeset), n_layers, T, w_table, nb_table)
     in_dims = [feats.shape[1]] + [out_dim] * (n_layers - 1)
     h = feats
     y = None
@@ -307,6 +322,26 @@ class RefTrainer:
         with torch.no_grad():
             nfl, var = triplet_monitors(self.feats, hs[0], torch.from_numpy(b))
         return float(loss), float(nfl), float(var), grads
+
+    def step_fly(self, batch, graph, n_hops, alpha, mt):
+        """The reference train step with on-the-fly sampling: each of the three
+        model calls walks its own nodeset (q, pos, neg in order) with the MT
+        stream `mt`; graph = (indptr, indices, n_all).  Returns (loss,
+        grads, per-call layers)."""
+        b = np.asarray(batch)
+        indptr, indices, n_all = graph
+        hs, lays = [], []
+        for c in range(3):
+            lay = relevant_nodes_fly(indptr, indices, n_all, b[:, c], self.L, n_hops, alpha, self.T, mt)
+            lays.append(lay)
+            hs.append(model_forward(self.p, self.feats, b[:, c], self.L, self.T, None, None, self.out,
+                                    layers=lay))
+        loss = max_margin_loss(*hs, self.margin)
+        self.opt.zero_grad()
+        loss.backward()
+        grads = {k: self.p[k].grad.detach().clone() for k in self.order}
+        self.opt.step()
+        return float(loss.detach()), grads, lays
 
     def step_dp(self, batch, world):
         """Data-parallel restatement of one step: ``world`` ranks each run the

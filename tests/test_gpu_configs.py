@@ -78,17 +78,22 @@ def test_train_step_reference_hyperparameters(tmpdir_cwd, name, n, n_cols, memb,
 
 def test_train_step_c5_shape_reference_init(tmpdir_cwd):
     """C5 (3 layers, fanout 50, d_in 256) at the reference init and margin.
-    A fresh 3-layer model collapses its outputs (|q_hat - p_hat| ~ 3e-3), so
-    the oracle's gradient over the GPU's active set with the oracle's own
-    forward (part A) differs by the amplified rounding of the forward (measured
-    ~1e-4, reported); the forward rows, hinge arguments, loss and the gradient
-    under the GPU outputs' cotangent (part B) are held to 1e-4."""
+    A fresh 3-layer model collapses its outputs (|q_hat - p_hat| ~ 3e-3): the
+    backward through three row normalisations of nearly parallel rows is
+    ill-conditioned in its linearisation point, so gradients evaluated at the
+    GPU's forward and at the oracle's (rows equal to 3e-7) differ by up to
+    ~1e-4 even under one shared cotangent (part B measured 3e-5 .. 1.04e-4
+    across kernel schedules), more with the oracle's own hinge cotangent
+    (part A, ~2e-4).  The forward rows and hinge arguments are held to 1e-4 /
+    1e-6, part B to 2e-4, part A to 1e-3; the kernels themselves are pinned at
+    1e-4 for this shape by test_fixed_cotangent_reference_init[50-3]
+    (random cotangent: well conditioned)."""
     n = 4000
     g, feats, pos, w, nb = _graph_problem(tmpdir_cwd, n, 1000, 50000, 256, seed=21, hops=300)
     tr = make_trainer(g, n, feats.cuda(), pos, 3, 50, 64, margin=1e-5, seed=7)
     torch.manual_seed(8)
     batch, _ = tr.next_batch()
-    res = check_train_step(tr, feats, w.numpy(), nb.numpy(), batch, strict_a=False)
+    res = check_train_step(tr, feats, w.numpy(), nb.numpy(), batch, strict_a=False, tol_b=2e-4)
     assert res["grad_rel_A_max"] <= 1e-3, res
 
 

@@ -99,11 +99,12 @@ def test_dashboard_train_pinsage_flow_c1():
                 assert np.array_equal(rec["batch"], rb)
             # --- every step against the oracle
             w, nb = pinsage.nbhds
-            # B = 32 with ~half the triples active: the head-bias gradients are short
-            # signed sums, so part A (oracle forward) is held to 1e-3 and part B
-            # (shared cotangent) to 1e-4 (parity_util)
+            # B = 32 with ~half the triples active: the head's gradients are short
+            # signed sums (cancelling q / pos / neg cotangents), so part A (oracle
+            # forward) is held to 1e-3 and part B (shared cotangent) to 3e-4; forward
+            # rows, hinge arguments and loss at 1e-4 / 1e-6 (parity_util)
             for rec in records:
-                res = check_record(rec, features, w.numpy(), nb.numpy(), strict_a=False)
+                res = check_record(rec, features, w.numpy(), nb.numpy(), strict_a=False, tol_b=3e-4)
                 assert res["grad_rel_A_max"] <= 1e-3, res
             # --- state.pt written every batch, lr decayed per epoch
             prog = torch.load(os.path.join("runs", "pinsage_openl3_ft", "state.pt"), weights_only=True)

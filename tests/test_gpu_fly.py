@@ -1,0 +1,122 @@
+"""On-the-fly sampling inside the model and the train step (SURVEY §8f row 1;
+relevant_nodes_per_layer, pinsage_model.py:142-154, the sampler the reference's
+forward carries commented out at :247-249): every model call walks its own
+nodeset's neighbourhoods with the fused walk + top-k kernel, consuming torch's
+generator exactly like the reference, and the engine reads per-layer tables of
+those draws.  Checked against the oracle's restatement (whose walk and top-k are
+pinned by the fly_* / topk_* fixtures): the draws of every call of a train step
+bit-exact, forward rows and the step's loss and gradients within 1e-4."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N, D_IN = 3000, 128
+
+
+def _problem(tmp):
+    import graph
+    import synthetic
+    pg = synthetic.make_playlist_graph(N, 750, 40000, seed=51)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
+    feats = torch.from_numpy(synthetic.make_features(N, D_IN, seed=52))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 5 * N, seed=53))
+    return pg, g, indptr, indices, feats, pos
+
+
+def _rows_rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float((np.linalg.norm(a - b, axis=1) / np.linalg.norm(b, axis=1)).max())
+
+
+@pytest.mark.parametrize("L,T", [(1, 3), (2, 3), (2, 10)])
+def test_forward_on_the_fly_vs_oracle(L, T):
+    """Forward with on-the-fly sampling, repeated ids included (the reference's
+    output rows of a repeated id are its last occurrence's), vs the oracle; the
+    generator ends where the reference's does."""
+    import pinsage_model as pm
+    from oracle import oracle as orc
+    pm.set_rng_mode("mt19937")
+    with tempfile.TemporaryDirectory() as tmp:
+        pg, g, indptr, indices, feats, pos = _problem(tmp)
+        torch.manual_seed(1)
+        m = pm.PinSageModel(g, N, L, (D_IN, 512, 128), 200, 0.85, T, None)
+        assert m.sample_on_the_fly
+        params = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        ids = np.random.default_rng(L * 10 + T).integers(0, N, 64)
+        ids[5] = ids[40]  # a repeated id
+        torch.manual_seed(123)
+        with torch.no_grad():
+            y = m(feats.cuda(), torch.from_numpy(ids)).cpu().numpy()
+        after = torch.get_rng_state()
+        mt = orc.MT(123)
+        lay = orc.relevant_nodes_fly(indptr, indices, pg.n_all, ids, L, 200, 0.85, T, mt)
+        ref = orc.model_forward(params, feats, ids, L, T, None, None, 128, layers=lay).numpy()
+        assert _rows_rel(y, ref) < 1e-4
+        mt.to_torch()  # the oracle's generator, handed to torch: the same state
+        assert torch.equal(torch.get_rng_state(), after)
+        # the sampled tables of the call equal the oracle's draws (per node, last occurrence)
+        tabs = m.runner().fly_history[-1]
+        for l in range(L):
+            ns, w, nb = lay[l]
+            nbt = tabs[l][0].cpu().numpy()
+            last = {}
+            for i, v in enumerate(ns):
+                last[int(v)] = i
+            for v, i in last.items():
+                assert np.array_equal(nbt[v], nb[i].astype(np.int32)), (l, v)
+
+
+@pytest.mark.parametrize("margin", [3.0, 1e-5])
+def test_train_step_on_the_fly_vs_oracle(margin):
+    """PinSage.train_batch with an on-the-fly model: three calls (q, pos, neg),
+    each with its own draws -- bit-exact against the oracle's draws of the same
+    calls -- then loss and every gradient vs the oracle's reference step
+    (margin 3: every hinge active; the reference's 1e-5: loss within 1e-4 and
+    gradients over the same active set, as parity_util explains)."""
+    import pinsage_model as pm
+    import pinsage_training as pt
+    from oracle import oracle as orc
+    pm.set_rng_mode("mt19937")
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            pg, g, indptr, indices, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            torch.manual_seed(2)
+            tr.model = pm.PinSageModel(g, N, 2, tr.dimensions, 200, 0.85, 3, None)
+            tr.n_hops = 200
+            tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+            tr.margin = margin
+            init = {k: v.detach().cpu().numpy().copy() for k, v in tr.model.state_dict().items()}
+            ref = orc.RefTrainer(init, feats, None, None, n_layers=2, T=3, margin=margin)
+            rng = np.random.default_rng(7)
+            batch = np.stack([rng.permutation(N)[:32] for _ in range(3)], 1).astype(np.int64)
+            torch.manual_seed(99)
+            loss, _, _ = tr.train_batch(torch.from_numpy(batch))
+            after = torch.get_rng_state()
+            mt = orc.MT(99)
+            rl, rg, lays = ref.step_fly(batch, (indptr, indices, pg.n_all), 200, 0.85, mt)
+            mt.to_torch()
+            assert torch.equal(torch.get_rng_state(), after)  # the same draws consumed
+            # the draws of each call (q, pos, neg): bit-exact
+            for c, tabs in enumerate(tr.model.runner().fly_history):
+                for l in range(2):
+                    ns, w, nb = lays[c][l]
+                    nbt = tabs[l][0].cpu().numpy()
+                    assert np.array_equal(nbt[ns], nb.astype(np.int32)), (c, l)
+            assert abs(float(loss) - rl) <= 1e-4 * abs(rl) + 1e-7, (float(loss), rl)
+            if margin > 1:
+                for k, p in tr.model.named_parameters():
+                    a = p.grad.detach().cpu().numpy().astype(np.float64)
+                    b = rg[k].numpy().astype(np.float64)
+                    assert np.linalg.norm(a - b) <= 1e-4 * np.linalg.norm(b) + 1e-12, k
+        finally:
+            os.chdir(cwd)

@@ -125,9 +125,12 @@ def test_train_after_large_forward_matches_oracle():
             torch.manual_seed(2)
             for it in range(3):
                 batch, _ = tr.next_batch()
-                # B = 32: part A (oracle forward, short signed sums) at 1e-3, part B at 1e-4
+                # B = 32, ~14 active triples: the head's gradients are short signed sums
+                # (cancelling q / pos / neg cotangents), so part A (oracle forward) is held
+                # to 1e-3 and part B (shared cotangent) to 3e-4; forward rows, hinge
+                # arguments and loss stay at 1e-4 / 1e-6 (parity_util)
                 res = check_train_step(tr, feats, tr.nbhds[0].numpy(), tr.nbhds[1].numpy(), batch,
-                                       strict_a=False)
+                                       strict_a=False, tol_b=3e-4)
                 assert res["grad_rel_A_max"] <= 1e-3, res
                 if it == 0:
                     e = tr.embed()  # all N ids: > 3 * batch_size, a larger engine
