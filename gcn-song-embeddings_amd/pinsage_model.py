@@ -351,36 +351,77 @@ def relevant_nodes_per_layer(g, n_items, nodeset, n_layers, n_hops, alpha, T):
     return S
 
 
+class _FlyDraws:
+    """One model call's on-the-fly draws, laid out for the engine.
+
+    ``tabs``: per-layer (nb int32 [n_items][T], wn f32 [n_items][T]) tables,
+    index 0 = bottom, rows of each layer's nodes written.  A node repeated in
+    the top nodeset keeps its LAST occurrence's row there: the reference's
+    put_embeddings lets the last write win (pinsage_model.py:29), so the output
+    rows of every repeat are the last one's.  ``uniq``/``inv``: the top
+    nodeset's distinct ids and each position's index into them.  ``repeats``:
+    for every earlier occurrence rank r = 1, 2, ... (counted from the last),
+    (index into uniq, ids, top-layer (nb, wn) table) of the positions holding
+    it.  Each occurrence walked its own neighbourhood, and index_put's backward
+    hands every occurrence's conv output the summed cotangent of its id
+    (pinsage_model.py:257-265), so their gradients are the reference's."""
+
+    def __init__(self, tabs, uniq, inv, repeats):
+        self.tabs, self.uniq, self.inv, self.repeats = tabs, uniq, inv, repeats
+
+    def with_top(self, top):
+        return self.tabs[:-1] + [top]
+
+
 def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
     """relevant_nodes_per_layer (pinsage_model.py:142-154) for the engine: top
     layer first, each layer's nodeset is walked (the fused walk + top-k
     kernel: the same draws as the reference, in nodeset order) and its top-T
-    rows land in that layer's own device table, indexed by node id.  A node
-    repeated in the top nodeset keeps its LAST occurrence's row: the
-    reference's put_embeddings lets the last write win (pinsage_model.py:29),
-    so the output rows of every repeat are the last one's.  Returns the
-    per-layer (nb int32 [n_items][T], wn f32 [n_items][T]) tables, index 0 =
-    bottom; only the rows of each layer's nodes are written."""
+    rows land in that layer's own device table, indexed by node id.  The next
+    layer's nodeset is unique(cat(nb.flatten(), cur)) over EVERY row drawn,
+    repeated nodes' earlier rows included (:152), so the draws of the layers
+    below follow the reference's stream.  Returns a _FlyDraws."""
     dev = nodeset_dev.device
+    T = int(T)
     tabs = []
     cur = nodeset_dev
-    for _ in range(n_layers):
-        _, _, wn, nb32 = _ppr_topk_device(g, cur, n_hops, alpha, int(T), t_norm=int(T), want_ref=False)
+    top_info = None
+    for layer in range(n_layers):
+        _, _, wn, nb32 = _ppr_topk_device(g, cur, n_hops, alpha, T, t_norm=T, want_ref=False)
         if nb32.numel() and int(nb32.max()) >= n_items:
             # the reference's h[nb] (features of tracks only) raises here
             raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
                              "zero-weight tail: the reference's h[nb] raises IndexError)")
+        n = int(cur.shape[0])
         uniq, inv = torch.unique(cur, return_inverse=True)
-        pos = torch.arange(cur.shape[0], device=dev)
-        last = torch.full((uniq.shape[0],), -1, dtype=torch.int64, device=dev)
-        last.scatter_reduce_(0, inv, pos, reduce="amax")
-        nbt = torch.empty((n_items, int(T)), dtype=torch.int32, device=dev)
-        wnt = torch.empty((n_items, int(T)), dtype=torch.float32, device=dev)
+        # occurrence rank of each position counted from its id's last one
+        order = torch.argsort(inv, stable=True)
+        ends = torch.cumsum(torch.bincount(inv, minlength=uniq.shape[0]), 0)
+        rank = torch.empty(n, dtype=torch.int64, device=dev)
+        rank[order] = ends[inv[order]] - 1 - torch.arange(n, device=dev)
+        last = torch.empty(uniq.shape[0], dtype=torch.int64, device=dev)
+        sel = rank == 0
+        last[inv[sel]] = torch.arange(n, device=dev)[sel]
+        nbt = torch.empty((n_items, T), dtype=torch.int32, device=dev)
+        wnt = torch.empty((n_items, T), dtype=torch.float32, device=dev)
         nbt[uniq] = nb32[last]
         wnt[uniq] = wn[last]
         tabs.insert(0, (nbt, wnt))
-        cur = _frontier_step(uniq, nbt, int(T), n_items)
-    return tabs
+        if layer == 0:
+            top_info = (uniq, inv, rank, nb32, wn)
+        cur = torch.unique(torch.cat([nb32.reshape(-1).to(torch.int64), cur]))
+    uniq, inv, rank, nb32, wn = top_info
+    repeats = []
+    n_rank = int(rank.max()) + 1 if rank.numel() else 1
+    for r in range(1, n_rank):
+        pos_r = torch.nonzero(rank == r).reshape(-1)
+        ids_r = nodeset_dev[pos_r]
+        nbt = torch.empty((n_items, T), dtype=torch.int32, device=dev)
+        wnt = torch.empty((n_items, T), dtype=torch.float32, device=dev)
+        nbt[ids_r] = nb32[pos_r]
+        wnt[ids_r] = wn[pos_r]
+        repeats.append((inv[pos_r], ids_r, (nbt, wnt)))
+    return _FlyDraws(tabs, uniq, inv, repeats)
 
 
 class _DeviceTable:
@@ -650,13 +691,14 @@ class _EngineRunner:
         return self._table
 
     def fly_tables(self, ids):
-        """Per-layer tables of this call's on-the-fly draws (None in table mode)."""
+        """This call's on-the-fly draws as a _FlyDraws (None in table mode)."""
         m = self.model
         if not m.sample_on_the_fly:
             return None
-        tabs = _fly_layer_tables(m.g, m.n_items, ids, m.n_layers, m.n_hops, m.alpha, m.T)
-        self.fly_history = (getattr(self, "fly_history", []) + [tabs])[-3:]  # (tests inspect the draws)
-        return tabs
+        draws = _fly_layer_tables(m.g, m.n_items, ids, m.n_layers, m.n_hops, m.alpha, m.T)
+        # (tests inspect the per-layer tables of the last calls)
+        self.fly_history = (getattr(self, "fly_history", []) + [draws.tabs])[-3:]
+        return draws
 
     def set_layer_tables(self, tabs):
         L = nat.lib()
@@ -712,9 +754,12 @@ class _EngineRunner:
             raise IndexError(f"node ids out of range for {n_valid} items")
         self.pack()
         self.ensure_engine(n)
-        tabs = self.fly_tables(ids)
+        draws = self.fly_tables(ids)
+        tabs = draws.tabs if draws is not None else None
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.params())
-        if need_grad:
+        if need_grad and draws is not None and draws.repeats:
+            out = self._fly_with_repeats(feats, draws)
+        elif need_grad:
             out = _EngineFn.apply(self, feats, table, ids, tabs, *self.params())
         else:
             if self._ws is None:
@@ -729,6 +774,21 @@ class _EngineRunner:
             nat.check(nat.lib().pinsage_engine_gather_output(self.engine.h, nat.ptr(self._ws), n,
                                                              nat.ptr(out), nat.stream_ptr()), "gather")
         return out.to(out_dev)
+
+
+    def _fly_with_repeats(self, feats, draws):
+        """Autograd forward of an on-the-fly call whose nodeset repeats ids.
+        The distinct ids run with their last occurrence's draws (the output
+        rows); every earlier occurrence rank runs again with its own top-layer
+        draws and enters the output as (o - o.detach()), an exact zero in the
+        forward through which each occurrence's conv output receives its id's
+        summed cotangent -- index_put's backward (pinsage_model.py:257-265)."""
+        ps = self.params()
+        out_u = _EngineFn.apply(self, feats, None, draws.uniq, draws.tabs, *ps)
+        for ui, ids_r, top in draws.repeats:
+            o = _EngineFn.apply(self, feats, None, ids_r, draws.with_top(top), *ps)
+            out_u = out_u.index_add(0, ui, o - o.detach())
+        return out_u[draws.inv]
 
 
 class _EngineFn(torch.autograd.Function):

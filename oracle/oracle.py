@@ -229,12 +229,35 @@ def param_names(n_layers):
     return names + ["G1.weight", "G1.bias", "G2.weight"]
 
 
+class _PutLast(torch.autograd.Function):
+    """``out[idx] = rows`` with the serial order's last write winning for a
+    repeated index.  torch-CPU's index_put_ gives no order for duplicates (it
+    becomes a parallel scatter: on a 16-thread host the winner changed from
+    run to run), the serial semantics are the last write; the backward is
+    index_put's: every row, winner or not, gets out's cotangent at its index."""
+
+    @staticmethod
+    def forward(ctx, h, idx, rows):
+        out = h.clone()
+        n = idx.shape[0]
+        _, first_rev = np.unique(idx.numpy()[::-1], return_index=True)
+        keep = torch.from_numpy(np.ascontiguousarray(n - 1 - first_rev))
+        out[idx[keep]] = rows[keep]
+        ctx.save_for_backward(idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        return None, None, g[idx]
+
+
 def _put(h, rows_idx, rows):
-    """put_embeddings semantics: detached copy, zero-padded row overwrite."""
-    out = h.detach().clone()
-    pad = out.shape[1] - rows.shape[1]
-    out[rows_idx, :] = torch.cat([rows, torch.zeros(rows.shape[0], pad, dtype=rows.dtype)], 1)
-    return out
+    """put_embeddings semantics (pinsage_model.py:24-30): detached copy,
+    zero-padded row overwrite, last write wins for repeated ids."""
+    pad = h.shape[1] - rows.shape[1]
+    padded = torch.cat([rows, torch.zeros(rows.shape[0], pad, dtype=rows.dtype)], 1)
+    return _PutLast.apply(h.detach(), rows_idx, padded)
 
 
 def conv_layer(p, i, h, nodes, nb, w, in_dim):

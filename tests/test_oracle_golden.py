@@ -214,3 +214,21 @@ def test_knn_from_emb_matches_reference():
     for k in (50, 1000):
         w, n = orc.knn_from_emb(d["emb"], d["q"], k)
         assert np.array_equal(w, d[f"w_{k}"]) and np.array_equal(n, d[f"n_{k}"]), k
+
+
+def test_put_repeated_ids_last_write_and_index_put_backward():
+    """The oracle's put_embeddings with repeated ids: the serial last write
+    wins (torch-CPU's parallel index_put leaves the winner unspecified), and
+    every occurrence's row gets the cotangent at its index (index_put's
+    backward), pinsage_model.py:24-30."""
+    import torch
+    from oracle import oracle as orc
+    h = torch.zeros(6, 3)
+    idx = torch.tensor([4, 1, 4, 2, 4])
+    rows = torch.arange(10, dtype=torch.float32).view(5, 2).requires_grad_()
+    out = orc._put(h, idx, rows)
+    assert out[4, :2].tolist() == [8.0, 9.0] and out[4, 2] == 0
+    assert out[1, :2].tolist() == [2.0, 3.0] and out[2, :2].tolist() == [6.0, 7.0]
+    g = torch.arange(18, dtype=torch.float32).view(6, 3)
+    (out * g).sum().backward()
+    assert torch.equal(rows.grad, g[idx, :2])
