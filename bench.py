@@ -39,6 +39,15 @@ CONFIGS = {
     "c4": dict(workload="synthetic 10M nodes / 100M edges, 128-d features, 2-layer, per-GPU batch 512",
                n_tracks=8_000_000, n_cols=2_000_000, memberships=53_600_000, d_in=128, n_layers=2,
                T=10, batch=512, global_batch=4096),
+    # BASELINE.json configs[4]: 100M nodes / 1B edges, d 256, 3 layers, fanout 50. Built
+    # on the device (a host build takes ~10 min); the [n, 100] host table would be 128 GB,
+    # so the model's T=50 table is made and kept in HBM (precompute_device_table); one
+    # 512-triple step reaches ~10^6 layer-0 nodes, so it runs in slices of `micro_batch`
+    # triples with recompute (PinSage.micro_batch)
+    "c5": dict(workload="synthetic 100M nodes / 1B edges, 256-d features, 3-layer fanout 50, "
+                        "per-GPU batch 512 in micro-batches of 16 triples", n_tracks=80_000_000,
+               n_cols=20_000_000, memberships=536_000_000, d_in=256, n_layers=3, T=50, batch=512,
+               global_batch=4096, micro_batch=16, device_build=True),
 }
 # --scaling strong: the global batch stays fixed (C4 B_global 4096, per-GPU
 # 4096/g); configs without a global_batch keep their batch as the global one
@@ -71,9 +80,46 @@ def setup_dist(n_gpus):
     return rank, world
 
 
+def build_problem_device(cfg, seed=0):
+    """C5-sized inputs drawn on the device (synthetic.make_playlist_graph_device):
+    graph, N(0,1) features z-scored per column, positives (host, for the sampler)."""
+    import graph
+    import synthetic
+    t0 = time.time()
+    dev = torch.device("cuda")
+    log(f"[bench] building synthetic graph on the device: {cfg['n_tracks']} tracks, "
+        f"{cfg['n_cols']} collections, {cfg['memberships']} memberships")
+    indptr, indices = synthetic.make_playlist_graph_device(cfg["n_tracks"], cfg["n_cols"], cfg["memberships"],
+                                                           seed=seed, device=dev)
+    g = graph.DeviceCSRGraph(indptr, indices)
+    log(f"[bench]   CSR built ({time.time()-t0:.1f}s): n_all={g.number_of_nodes()} edges={int(indices.shape[0])}")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed + 1)
+    feats = torch.empty((cfg["n_tracks"], cfg["d_in"]), dtype=torch.float32, device=dev)
+    for i in range(0, cfg["n_tracks"], 1 << 22):
+        feats[i:i + (1 << 22)].normal_(generator=gen)
+    # z-scored per column (spotify_graph.py:77-79) in row chunks: no full-size temporaries
+    ch = 1 << 20
+    n = cfg["n_tracks"]
+    mean = sum(feats[i:i + ch].sum(0, dtype=torch.float64) for i in range(0, n, ch)) / n
+    var = sum(((feats[i:i + ch].double() - mean) ** 2).sum(0) for i in range(0, n, ch)) / (n - 1)
+    std = var.sqrt() + 1e-12
+    for i in range(0, n, ch):
+        feats[i:i + ch] = ((feats[i:i + ch].double() - mean) / std).float()
+    pos = synthetic.make_positives_device(indptr, indices, cfg["n_tracks"], 5 * cfg["n_tracks"], seed=seed + 2)
+    log(f"[bench] features and {pos.shape[0]} positives in {time.time()-t0:.1f}s")
+
+    class _PG:
+        n_all = g.number_of_nodes()
+        n_edges = int(indices.shape[0])
+    return _PG(), g, feats, pos
+
+
 def build_problem(cfg, seed=0):
     import graph
     import synthetic
+    if cfg.get("device_build"):
+        return build_problem_device(cfg, seed)
     t0 = time.time()
     log(f"[bench] building synthetic graph: {cfg['n_tracks']} tracks, {cfg['n_cols']} collections, "
         f"{cfg['memberships']} memberships")
@@ -98,8 +144,12 @@ def precompute(g, cfg, mode):
     t0 = time.time()
     import contextlib
     with contextlib.redirect_stdout(sys.stderr):  # progress prints must not reach the JSON line
-        nb = pm.precompute_neighborhoods_topt(g, cfg["n_tracks"], pm.DEF_HOPS, pm.DEF_ALPHA,
-                                              pm.DEF_T_PRECOMP, None)
+        if cfg.get("device_build"):  # the model's T columns of the top-100, kept in HBM
+            nb = pm.precompute_device_table(g, cfg["n_tracks"], pm.DEF_HOPS, pm.DEF_ALPHA, cfg["T"],
+                                            pm.DEF_T_PRECOMP)
+        else:
+            nb = pm.precompute_neighborhoods_topt(g, cfg["n_tracks"], pm.DEF_HOPS, pm.DEF_ALPHA,
+                                                  pm.DEF_T_PRECOMP, None)
     torch.cuda.synchronize()
     dt = time.time() - t0
     pm.set_rng_mode("mt19937")
@@ -210,15 +260,26 @@ def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None, help="default 50 (c5: 3)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 5 (c5: 1)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scale", type=float, default=1.0,
+                    help="rehearsal only: scale the graph (tracks, collections, memberships)")
     ap.add_argument("--precompute-rng", default="philox", choices=["philox", "mt19937"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: per-GPU batch fixed; strong: global batch fixed (per-GPU = global / N)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
+    if args.scale != 1.0:
+        for k in ("n_tracks", "n_cols", "memberships"):
+            cfg[k] = max(1000, int(cfg[k] * args.scale))
+        cfg["workload"] += f" [REHEARSAL: graph scaled by {args.scale}]"
+    micro = cfg.get("micro_batch")
+    if args.steps is None:
+        args.steps = 3 if micro else 50
+    if args.warmup is None:
+        args.warmup = 1 if micro else 5
     rank, world = setup_dist(args.gpus)
     if args.scaling == "strong":
         gb = cfg.get("global_batch", cfg["batch"])
@@ -234,7 +295,7 @@ def main():
     hops = cfg["n_tracks"] * 500
     log(f"[bench] precompute ({args.precompute_rng}) {t_pre:.2f}s = {hops/t_pre/1e6:.1f} M hops/s")
     t_pre_warm = None
-    if t_pre < 2.0:  # the first call pays one-time costs (code objects, CSR upload): time it again
+    if t_pre < 2.0 and not micro:  # the first call pays one-time costs (code objects, CSR upload): time it again
         _, t_pre_warm = precompute(g, cfg, args.precompute_rng)
         log(f"[bench] precompute again (warm) {t_pre_warm * 1e3:.1f} ms")
 
@@ -242,9 +303,11 @@ def main():
         cwd = os.getcwd()
         os.chdir(tmp)
         g.nbhds_path = os.path.join(tmp, "nb.pt")
-        torch.save(nbhds, g.nbhds_path)
+        if not cfg.get("device_build"):
+            torch.save(nbhds, g.nbhds_path)
         torch.manual_seed(0)
-        tr = pt.PinSage(g, cfg["n_tracks"], feats.cuda(), pos, log=False, load_save=False)
+        tr = pt.PinSage(g, cfg["n_tracks"], feats.cuda(), pos, log=False, load_save=False,
+                        nbhds=nbhds if cfg.get("device_build") else None)
         # BASELINE config: n_layers / fanout / batch (bound before the model, as the reference does)
         if tr.T != cfg["T"] or tr.n_layers != cfg["n_layers"]:
             import pinsage_model as pm
@@ -254,6 +317,7 @@ def main():
             tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
             tr.scheduler = torch.optim.lr_scheduler.ExponentialLR(tr.optimizer, tr.decay)
         tr.batch_size = cfg["batch"]
+        tr.micro_batch = micro
         torch.manual_seed(1234)  # same global batches on every rank
 
         def step():
@@ -290,24 +354,27 @@ def main():
                 json.dumps({k: round(v / (args.steps + args.warmup) * 1e3, 4) for k, v in pt._HOST_T.items()}))
         value = 3 * cfg["batch"] * world * args.steps / elapsed
 
-        gemm_choices = tr._fused.tuned_choices
+        gemm_choices = tr._fused.tuned_choices if tr._fused is not None else None
         # per-kernel timing pass (HIP events on the launch stream), separate from the timed
         # loop; runs the same kernels eagerly (events are not recorded inside the graph)
-        tr._fused.use_graph = False
+        if tr._fused is not None:
+            tr._fused.use_graph = False
         eng = tr.model.runner().engine
         nat.lib().pinsage_engine_timing(eng.h, 1)
-        n_t = max(5, min(20, args.steps))
+        n_t = 1 if micro else max(5, min(20, args.steps))
         sizes = []
         hold_stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         for _ in range(n_t):
             # hold the stream while the host queues the step, so the events time the
             # kernels back to back (an eager step's host enqueue is ~0.5 ms: without
             # the hold, an idle GPU would charge each launch's host gap to its kernel)
-            nat.lib().pinsage_stream_hold(3000, hold_stream)
+            if not micro:
+                nat.lib().pinsage_stream_hold(3000, hold_stream)
             step()
             torch.cuda.synchronize()
             off = eng.off
-            ws = tr._fused.ws
+            # micro-batched: the frontier of the last slice's outputs-only forward
+            ws = tr._fused.ws if tr._fused is not None else tr.model.runner()._ws
             cN0 = int(eng.view(ws, int(off.count_N[0]), torch.int32, 1).item())
             cS0 = int(eng.view(ws, int(off.count_S[0]), torch.int32, 1).item())
             sizes.append((cN0, cS0))
@@ -322,15 +389,31 @@ def main():
     q_avg = q_ms / max(q_calls, 1)
     q_flops = 2.0 * U0 * d * hid
     achieved_tf = q_flops / (q_avg * 1e-3) / 1e12 if q_avg > 0 else 0.0
-    a_ms, a_calls = kt.get("fwd.agg.l0", (0.0, 1))
+    # the gather kernel: the fused aggregation + W projection (fwd.aggw.l0), or the
+    # aggregation alone when the engine runs them as two launches (PINSAGE_FUSED_AGGW=0)
+    fused = "fwd.aggw.l0" in kt
+    a_site = "fwd.aggw.l0" if fused else "fwd.agg.l0"
+    a_ms, a_calls = kt.get(a_site, (0.0, 1))
     a_avg = a_ms / max(a_calls, 1)
     # the aggregation reads each of the U0 distinct q rows from HBM at most once (repeats
     # of a popular row are L2/Infinity-Cache hits): unique bytes are the HBM bound;
     # logical bytes (every slot's row) are reported as the cache-served gather rate
     agg_bytes = U0 * hid * 4 + F0 * T * 8 + F0 * hid * 4
     agg_logical = F0 * T * hid * 4 + F0 * T * 8 + F0 * hid * 4
+    agg_flops = 0.0
+    if fused:
+        # + the gathered self rows, W, and the outputs y and row norms (agg is still
+        # written: the W weight gradient reads it)
+        extra = F0 * d * 4 + (d + hid) * 128 * 4 + F0 * 128 * 4 + F0 * 4
+        agg_bytes += extra
+        agg_logical += extra
+        agg_flops = 2.0 * F0 * (d + hid) * 128
+    # committed PMC summaries are keyed by config (+ the per-GPU batch when it is not the
+    # config's own, e.g. c4_b4096 = C4's global batch on one GPU)
+    pmc_key = args.config if cfg["batch"] == CONFIGS[args.config]["batch"] else f"{args.config}_b{cfg['batch']}"
+    a_traffic, a_traffic_src, _ = pmc_traffic(pmc_key, a_site)
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "calls": v[1]} for k, v in sorted(kt.items())}
-    traffic, traffic_src, mfma_busy = pmc_traffic(args.config, "fwd.q_gemm.l0")
+    traffic, traffic_src, mfma_busy = pmc_traffic(pmc_key, "fwd.q_gemm.l0")
     result = {
         "metric": "PinSAGE train-step nodes/sec (2-hop, batch 512) at 1/2/4/8 MI355X",
         "value": value,
@@ -355,15 +438,23 @@ def main():
                      "traffic_source": traffic_src, "mfma_busy_pmc": mfma_busy,
                      "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg,
                      "algorithmic_bytes_per_launch": 4.0 * (U0 * d + d * hid + U0 * hid)},
-        "gather_kernel": {"kernel": "fwd.agg.l0", "bound": "hbm", "avg_launch_ms": a_avg,
+        "gather_kernel": {"kernel": a_site + (" (weighted aggregation + [h_self || agg] W projection, "
+                                              "bias, lrelu, row L2 norm in one launch)" if fused else ""),
+                          "bound": "hbm", "avg_launch_ms": a_avg,
                           "achieved_GBs": agg_bytes / (a_avg * 1e-3) / 1e9 if a_avg > 0 else 0.0,
                           "peak_GBs": PEAK_HBM_GBS, "frac": (agg_bytes / (a_avg * 1e-3) / 1e9 / PEAK_HBM_GBS
                                                              if a_avg > 0 else 0.0),
                           "algorithmic_bytes": agg_bytes,
+                          "traffic": a_traffic, "traffic_source": a_traffic_src,
                           "logical_bytes": agg_logical,
                           "logical_GBs": agg_logical / (a_avg * 1e-3) / 1e9 if a_avg > 0 else 0.0,
-                          "note": "algorithmic = unique q rows + index/weight + output; logical counts "
-                                  "every (row, slot) read, most served by L2 / Infinity Cache"},
+                          "mfma_flops": agg_flops,
+                          "mfma_frac": (agg_flops / (a_avg * 1e-3) / 1e12 / PEAK_FP32_TFLOPS
+                                        if a_avg > 0 else 0.0),
+                          "note": "algorithmic = unique q rows + index/weight + agg"
+                                  + (" + self rows + W + y/norm outputs" if fused else "")
+                                  + "; logical counts every (row, slot) read, most served by L2 / "
+                                    "Infinity Cache"},
         "frontier": {"U0_mean": U0, "F0_mean": F0},
         "host_ms_per_step": {"sample_batch": t_sample / args.steps * 1e3,
                              "train_batch_enqueue": t_enqueue / args.steps * 1e3},
@@ -377,7 +468,19 @@ def main():
         "kernels": kernels,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if micro:
+        result["config"]["micro_batch"] = micro
+        result["frontier"]["note"] = "U0/F0 of one micro-batch slice (the last outputs-only forward)"
+    if cfg.get("device_build"):
+        result["data"] += "; graph, features and positives drawn on the device"
+        result["precompute"]["note"] = ("precompute_device_table: the model's T=50 columns of the top-100, "
+                                        "built and kept in HBM")
+    if rank == 0 and world == 1 and micro:
+        # the reference's put_embeddings clones (n x d_in x 4 = 82 GB each)
+        # and its dense [256, N_all] f64 visit matrix (205 GB) exceed the host: not run
+        result["cpu_baseline"] = {"value": None, "note": "not run: the reference's per-layer put_embeddings "
+                                  "clones (82 GB each) and dense visit matrices do not fit host memory"}
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(cfg, pg, feats, pos, nbhds)
         except Exception as ex:  # report, never fail the bench line

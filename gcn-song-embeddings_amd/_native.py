@@ -152,9 +152,13 @@ def stream_ptr():
 
 
 def ptr(t):
-    """Device/host pointer of a tensor (None -> NULL)."""
+    """Device/host pointer of a tensor (None -> NULL).  The C-ABI reads plain
+    arrays: a strided 1-D view (e.g. a column of a [3, B] batch reshaped) would
+    be read as if contiguous, so it is refused."""
     if t is None:
         return None
+    if t.dim() == 1 and t.numel() > 1 and t.stride(0) != 1:
+        raise ValueError("C-ABI pointer of a strided 1-D tensor (call .contiguous())")
     return ctypes.c_void_p(t.data_ptr())
 
 

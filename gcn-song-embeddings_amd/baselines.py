@@ -65,7 +65,7 @@ def _knn_cosine(emb, q, k_total, eps=1e-16):
     e = torch.as_tensor(emb)
     out_dev = e.device
     e = e.to(device="cuda", dtype=torch.float32).contiguous()
-    qs = torch.as_tensor(q).reshape(-1).to(torch.int64)
+    qs = torch.as_tensor(q).reshape(-1).to(torch.int64).contiguous()
     n, d = int(e.shape[0]), int(e.shape[1])
     if qs.numel() and (int(qs.min()) < 0 or int(qs.max()) >= n):
         raise IndexError(f"knn: query ids out of range for {n} rows")

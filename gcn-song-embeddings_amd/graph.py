@@ -122,3 +122,32 @@ class CSRGraph:
 
     def max_degree(self) -> int:
         return int(np.diff(self.indptr).max()) if self._n else 0
+
+
+class DeviceCSRGraph(CSRGraph):
+    """A CSRGraph whose CSR was built on the device (synthetic.make_playlist_graph_device):
+    the HBM mirror is the primary copy; ``indptr`` is kept on the host (degrees,
+    max_degree) and ``indices`` crosses to the host only if a host-side caller
+    (successors, edges, adj) asks for it."""
+
+    def __init__(self, indptr_dev, indices_dev, base_dir=".", nbhds_path="neighborhoods.pt"):
+        self._dev = (indptr_dev.to(torch.int64).contiguous(), indices_dev.to(torch.int32).contiguous())
+        self.indptr = self._dev[0].cpu().numpy()
+        self._indices = None
+        self._n = int(self.indptr.shape[0] - 1)
+        self._src = None
+        self._dst = None
+        self._rev = None
+        self.base_dir = base_dir
+        self.nbhds_path = nbhds_path
+
+    @property
+    def indices(self):
+        if self._indices is None:
+            self._indices = self._dev[1].cpu().numpy()
+        return self._indices
+
+    def device_csr(self, dev):
+        if self._dev[0].device != dev:
+            self._dev = (self._dev[0].to(dev), self._dev[1].to(dev))
+        return self._dev

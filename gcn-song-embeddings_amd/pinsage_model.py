@@ -79,7 +79,7 @@ def _walk_device(g, nodeset, n_hops, alpha, philox=None):
     g = _as_csr(g)
     dev = nat.device()
     indptr, indices = g.device_csr(dev)
-    src = torch.as_tensor(nodeset).reshape(-1).to(device=dev, dtype=torch.int64)
+    src = torch.as_tensor(nodeset).reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
     n = int(src.shape[0])
     n_all = g.number_of_nodes()
     trace = torch.empty((n, int(n_hops)), dtype=torch.int32, device=dev)
@@ -167,7 +167,7 @@ def _ppr_topk_device(g, nodeset, n_hops, alpha, T, t_norm=0, philox=None, want_r
         return _topk_device(src, trace, n_all, n_hops, T, t_norm=t_norm)
     dev = nat.device()
     indptr, indices = g.device_csr(dev)
-    src = torch.as_tensor(nodeset).reshape(-1).to(device=dev, dtype=torch.int64)
+    src = torch.as_tensor(nodeset).reshape(-1).to(device=dev, dtype=torch.int64).contiguous()
     n = int(src.shape[0])
     w = torch.empty((n, T), dtype=torch.float64, device=dev) if want_ref else None
     nb = torch.empty((n, T), dtype=torch.int64, device=dev) if want_ref else None
@@ -314,6 +314,43 @@ def precompute_neighborhoods_topt(g, n_items, n_hops, alpha, T, path):
     return (all_w, all_nb)
 
 
+def precompute_device_table(g, n_items, n_hops, alpha, T, T_precomp=DEF_T_PRECOMP, chunk=1 << 18):
+    """The model's neighbourhood table built and kept on the device: for every
+    item, the first T of its top-T_precomp PPR neighbours (the rows
+    precompute_neighborhoods_topt returns, cut to [:, :T] as the model reads
+    them, pinsage_model.py:164) with the weights normalised over those T
+    (pinsage_model.py:202).  Same draws and positions as
+    precompute_neighborhoods_topt (one process), but the [n, T_precomp] f64 + i64
+    table never exists: at 80M items it would be 128 GB of host memory.  Returns
+    a device table PinSageModel / PinSage accept as ``nbhds``."""
+    dev = nat.device()
+    T, T_precomp = int(T), int(T_precomp)
+    if T > T_precomp:
+        raise ValueError("T > T_precomp")
+    nb32 = torch.empty((n_items, T), dtype=torch.int32, device=dev)
+    wn = torch.empty((n_items, T), dtype=torch.float32, device=dev)
+    st0 = torch.get_rng_state().numpy().copy()
+    mt_mode = _RNG_MODE == "mt19937"
+    philox = None
+    if not mt_mode:
+        with nat.torch_rng() as mt:
+            d = mt.draws(2)
+        philox = (int(d[0]) << 32) | int(d[1])
+    for i in range(0, n_items, chunk):
+        if mt_mode:
+            _set_stream_position(st0, 3 * int(n_hops) * i)
+        ids = torch.arange(i, min(i + chunk, n_items), dtype=torch.int64, device=dev)
+        _, _, w_c, nb_c = _ppr_topk_device(g, ids, n_hops, alpha, T_precomp, t_norm=T,
+                                           philox=None if mt_mode else (philox, i), want_ref=False)
+        nb32[i:i + ids.shape[0]] = nb_c
+        wn[i:i + ids.shape[0]] = w_c
+    if mt_mode:
+        _set_stream_position(st0, 3 * int(n_hops) * n_items)
+    if n_items and int(nb32.max()) >= n_items:
+        raise IndexError("neighbourhood table references ids >= n_items")
+    return _DeviceTable.resident(nb32, wn)
+
+
 def sample_hard_negatives(g, n_items, visit_prob, hn_per_query, min_rank, max_rank):
     """(NOT USED in the reference either; pinsage_model.py:135-140)"""
     rng = visit_prob.topk(max_rank, 1)[1][:, min_rank:]
@@ -428,6 +465,16 @@ class _DeviceTable:
     """Device mirror of a precomputed (weights, nodes) table: first T columns,
     nodes int32, weights f32 normalised by their f64 row sum."""
 
+    @classmethod
+    def resident(cls, nb32, wn, src=None):
+        """A table already on the device (precompute_device_table): nb int32
+        [n][T], wn f32 [n][T] normalised over the T columns."""
+        t = cls.__new__(cls)
+        t.src = src
+        t.T = int(nb32.shape[1])
+        t.nb32, t.wn = nb32, wn
+        return t
+
     def __init__(self, nbhds, T, n_items, dev):
         w, nb = nbhds
         self.src = (w, nb)
@@ -490,7 +537,7 @@ class ConvLayer(nn.Module):
 
 def _conv_layer_forward(layer, h, nodeset, nb_nodes, nb_weights):
     dev = nat.device()
-    ns = torch.as_tensor(nodeset).reshape(-1).to(torch.int64)
+    ns = torch.as_tensor(nodeset).reshape(-1).to(torch.int64).contiguous()
     n_items = int(h.shape[0])
     T = int(nb_nodes.shape[1])
     # a table indexed by node id holding this call's rows
@@ -684,6 +731,19 @@ class _EngineRunner:
         m = self.model
         if m.sample_on_the_fly:
             return None
+        if isinstance(nbhds, _DeviceTable):  # device-resident (precompute_device_table)
+            if nbhds.T < int(m.T) or nbhds.nb32.shape[0] < m.n_items:
+                raise ValueError("device table narrower than T or shorter than n_items")
+            if nbhds.T == int(m.T):
+                return nbhds
+            key = (id(nbhds), int(m.T))
+            if key != self._table_key:
+                # the first T columns of a wider resident table, renormalised in f64
+                w = nbhds.wn[:, :m.T].to(torch.float64)
+                self._table = _DeviceTable.resident(nbhds.nb32[:, :m.T].contiguous(),
+                                                    (w / w.sum(1, keepdim=True)).float().contiguous())
+                self._table_key = key
+            return self._table
         key = (id(nbhds[0]), id(nbhds[1]), int(m.T))
         if key != self._table_key:
             self._table = _DeviceTable(nbhds, m.T, m.n_items, self.dev)
@@ -744,7 +804,7 @@ class _EngineRunner:
             raise RuntimeError("zeros: Dimension size must be non-negative (out_dim > feature dim, "
                                "as the reference's put_embeddings)")
         table = self.table(nbhds)
-        ids = torch.as_tensor(nodeset).reshape(-1).to(self.dev, torch.int64)
+        ids = torch.as_tensor(nodeset).reshape(-1).to(self.dev, torch.int64).contiguous()
         n = int(ids.shape[0])
         if n == 0:
             return torch.empty((0, m.out_dim), device=out_dev)

@@ -191,3 +191,93 @@ def write_spotify_dataset(dirpath: str, g: PlaylistGraph, track_ids=None, col_id
         with open(os.path.join(dirpath, name), "w", encoding="utf-8") as f:
             json.dump(obj, f)
     return track_ids, col_ids
+
+
+def make_playlist_graph_device(n_tracks: int, n_cols: int, n_memberships: int, seed: int = 0,
+                               zipf_a: float = 1.0, size_sigma: float = 1.0, device="cuda",
+                               chunk: int = 1 << 26):
+    """make_playlist_graph's distribution drawn on the device (torch, seeded
+    device generator), for graphs whose host build takes minutes (the C5 shape:
+    100M nodes / 1B edges).  Same layout and guarantees -- tracks first, rows in
+    edge-insertion order, every track in >= 1 collection, every collection with
+    >= 2 distinct tracks -- but a different random stream than the host
+    builder.  Returns (indptr int64 [N+1], indices int32 [E]) on the device."""
+    import torch
+    if n_tracks < 2 or n_cols < 1:
+        raise ValueError("need at least 2 tracks and 1 collection")
+    n_memberships = max(int(n_memberships), n_tracks + n_cols)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    f64 = torch.float64
+    ranks = torch.randperm(n_tracks, generator=gen, device=device).to(f64) + 1.0
+    cdf_t = torch.cumsum(ranks.pow_(-zipf_a), 0)
+    del ranks
+    cdf_t /= cdf_t[-1].clone()
+    raw = torch.empty(n_cols, dtype=f64, device=device).log_normal_(0.0, size_sigma, generator=gen)
+    sizes = torch.clamp(torch.round(raw / raw.mean() * (n_memberships / n_cols)), min=2)
+    cdf_c = torch.cumsum(sizes, 0)
+    cdf_c /= cdf_c[-1].clone()
+    del raw, sizes
+
+    def draw(cdf, n):
+        u = torch.rand(n, dtype=f64, device=device, generator=gen)
+        return torch.clamp(torch.searchsorted(cdf, u), max=cdf.shape[0] - 1)
+
+    parts = [draw(cdf_c, n_tracks) * n_tracks + torch.arange(n_tracks, device=device)]
+    extra = max(0, n_memberships - n_tracks)
+    for i in range(0, extra, chunk):
+        k = min(chunk, extra - i)
+        parts.append(draw(cdf_c, k) * n_tracks + draw(cdf_t, k))
+    key = torch.unique(torch.cat(parts))
+    del parts, cdf_t, cdf_c
+    # every collection gets >= 2 distinct tracks
+    cnt = torch.bincount(key // n_tracks, minlength=n_cols)
+    while bool((cnt < 2).any()):  # one random track more per short collection per round
+        bad = torch.nonzero(cnt < 2).reshape(-1)
+        add = torch.randint(0, n_tracks, (bad.numel(),), device=device, generator=gen)
+        key = torch.unique(torch.cat([key, bad * n_tracks + add]))
+        cnt = torch.bincount(key // n_tracks, minlength=n_cols)
+    cols = key // n_tracks
+    tracks = key - cols * n_tracks
+    del key
+    n_all = n_tracks + n_cols
+    deg = torch.cat([torch.bincount(tracks, minlength=n_tracks), cnt])
+    indptr = torch.zeros(n_all + 1, dtype=torch.int64, device=device)
+    torch.cumsum(deg, 0, out=indptr[1:])
+    del deg, cnt
+    m = tracks.shape[0]
+    indices = torch.empty(2 * m, dtype=torch.int32, device=device)
+    # collection rows: members ascending (the pairs are collection-major)
+    indices[m:] = tracks.to(torch.int32)
+    # track rows: collections in edge order = a stable sort of the pairs by track
+    _, order = torch.sort(tracks, stable=True)
+    del tracks
+    indices[:m] = (cols[order] + n_tracks).to(torch.int32)
+    return indptr, indices
+
+
+def make_positives_device(indptr, indices, n_tracks: int, n_pairs: int, seed: int = 3,
+                          chunk: int = 1 << 26):
+    """make_positives' co-membership pairs drawn on the device ([P, 2] int64 on
+    the host, where the batch sampler reads them)."""
+    import torch
+    dev = indptr.device
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    out = torch.empty((n_pairs, 2), dtype=torch.int64)
+    for i in range(0, n_pairs, chunk):
+        k = min(chunk, n_pairs - i)
+        a = torch.randint(0, n_tracks, (k,), device=dev, generator=gen)
+        da = indptr[a + 1] - indptr[a]
+        u = torch.rand(k, dtype=torch.float64, device=dev, generator=gen)
+        c = indices[indptr[a] + (u * da).to(torch.int64)].to(torch.int64)
+        dc = indptr[c + 1] - indptr[c]
+        u = torch.rand(k, dtype=torch.float64, device=dev, generator=gen)
+        kk = (u * dc).to(torch.int64)
+        b = indices[indptr[c] + kk].to(torch.int64)
+        same = b == a
+        kk = torch.where(same, (kk + 1) % dc, kk)
+        b = torch.where(same, indices[indptr[c] + kk].to(torch.int64), b)
+        out[i:i + k, 0] = a.cpu()
+        out[i:i + k, 1] = b.cpu()
+    return out

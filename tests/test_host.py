@@ -338,3 +338,29 @@ def test_randperm_prefix_long_matches_torch():
     ref = torch.randperm(n)[:k].numpy()
     assert (got == ref).all()
     assert int(torch.randint(1000, ())) == after
+
+
+def test_device_graph_generator_properties():
+    """synthetic.make_playlist_graph_device (the C5 bench's graph builder) on the
+    CPU device: bipartite and symmetric, rows in edge-insertion order, every
+    track in >= 1 collection and every collection with >= 2 distinct tracks;
+    positives are co-members and never self-pairs."""
+    import numpy as np
+    import torch
+    import synthetic
+    n, nc = 3000, 700
+    ip, ix = synthetic.make_playlist_graph_device(n, nc, 30000, seed=1, device="cpu")
+    ip, ix = ip.numpy(), ix.numpy()
+    deg = np.diff(ip)
+    assert deg[:n].min() >= 1 and deg[n:].min() >= 2
+    src = np.repeat(np.arange(n + nc), deg)
+    assert ((src < n) != (ix < n)).all()
+    fwd = set(zip(src.tolist(), ix.tolist()))
+    assert fwd == set(zip(ix.tolist(), src.tolist())) and len(fwd) == ix.shape[0]
+    for v in list(range(0, n, 97)) + list(range(n, n + nc, 13)):
+        row = ix[ip[v]:ip[v + 1]]
+        assert (np.diff(row) > 0).all()  # collection-major pairs: both row kinds ascend
+    pos = synthetic.make_positives_device(torch.from_numpy(ip), torch.from_numpy(ix), n, 4000, seed=3).numpy()
+    assert (pos[:, 0] != pos[:, 1]).all() and pos.max() < n
+    cols_of = {v: set(ix[ip[v]:ip[v + 1]].tolist()) for v in np.unique(pos[:200]).tolist()}
+    assert all(cols_of[a] & cols_of[b] for a, b in pos[:200].tolist())

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--match", default="gemm_f32_kernel")
     ap.add_argument("--simds", type=int, default=1024)
     ap.add_argument("--xcds", type=int, default=8)
+    ap.add_argument("--last", type=int, default=0, help="keep each group's last N dispatches")
     a = ap.parse_args()
     cnt = collections.defaultdict(dict)
     meta = {}
@@ -31,7 +32,7 @@ def main():
         meta[k] = (r["Kernel_Name"].split("(")[0].replace("void ", ""), int(r["Grid_Size"]),
                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     groups = collections.defaultdict(list)
-    for k, c in cnt.items():
+    for k, c in sorted(cnt.items()):
         name, grid, dur = meta[k]
         cyc = c["GRBM_GUI_ACTIVE"] / a.xcds
         groups[(name, grid)].append((dur, c["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * a.simds), cyc / dur / 1e9,
@@ -39,6 +40,8 @@ def main():
     print(f"# {a.csv}: per kernel/grid, mean over launches")
     print(f"{'kernel':60s} {'grid':>8s} {'n':>3s} {'us':>8s} {'mfma_busy':>9s} {'GHz':>5s} {'mfma_insts':>11s}")
     for (name, grid), v in sorted(groups.items()):
+        if a.last > 0:
+            v = v[-a.last:]
         n = len(v)
         m = [sum(x[i] for x in v) / n for i in range(4)]
         print(f"{name:60s} {grid:8d} {n:3d} {m[0] * 1e6:8.1f} {m[1]:9.3f} {m[2]:5.2f} {m[3]:11.0f}")

@@ -16,13 +16,19 @@ import csv
 import json
 
 
-def mean_counter(path, kernel, counter):
+def mean_counter(path, kernel, counter, grid=None, last=0):
+    """Mean per dispatch of `counter` over the dispatches of `kernel` (and grid
+    size); last > 0 keeps the last `last` dispatches only (bench.py's eager
+    timing pass runs each site once per step at the end of the run, after the
+    tuner's probe launches of the same templates)."""
     vals = {}
     for r in csv.DictReader(open(path)):
-        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            key = r.get("Dispatch_Id") or r.get("Correlation_Id") or len(vals)
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter and \
+                (grid is None or int(r["Grid_Size"]) == grid):
+            key = int(r["Dispatch_Id"])
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    return (sum(vals.values()) / len(vals), len(vals)) if vals else (None, 0)
+    keys = sorted(vals)[-last:] if last > 0 else sorted(vals)
+    return (sum(vals[k] for k in keys) / len(keys), len(keys)) if keys else (None, 0)
 
 
 def main():
@@ -32,14 +38,21 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--last", type=int, default=0)
+    ap.add_argument("--algorithmic", type=float, default=None,
+                    help="algorithmic bytes per launch (bench.py), for the traffic ratio")
     a = ap.parse_args()
-    f, nf = mean_counter(a.fetch, a.kernel, "FETCH_SIZE")
-    w, nw = mean_counter(a.write, a.kernel, "WRITE_SIZE")
-    out = {"config": a.config, "site": a.site, "kernel": a.kernel, "launches": min(nf, nw),
+    f, nf = mean_counter(a.fetch, a.kernel, "FETCH_SIZE", a.grid, a.last)
+    w, nw = mean_counter(a.write, a.kernel, "WRITE_SIZE", a.grid, a.last)
+    out = {"config": a.config, "site": a.site, "kernel": a.kernel, "grid": a.grid, "launches": min(nf, nw),
            "fetch_size_kb": f, "write_size_kb": w,
            "hbm_bytes_per_launch": (2 * f + w) * 1024 if f is not None and w is not None else None,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "FETCH_SIZE doubled (gfx950 counts half of wide coalesced reads); KB = 1024 B"}
+    if a.algorithmic and out["hbm_bytes_per_launch"]:
+        out["algorithmic_bytes_per_launch"] = a.algorithmic
+        out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / a.algorithmic
     print(json.dumps(out, indent=1))
 
 
