@@ -16,7 +16,7 @@ import csv
 import json
 
 
-def mean_counter(path, kernel, counter, grid=None, last=0):
+def mean_counter(path, kernel, counter, grid=None, last=0, stride=1, offset=0):
     """Mean per dispatch of `counter` over the dispatches of `kernel` (and grid
     size); last > 0 keeps the last `last` dispatches only (bench.py's eager
     timing pass runs each site once per step at the end of the run, after the
@@ -27,7 +27,10 @@ def mean_counter(path, kernel, counter, grid=None, last=0):
                 (grid is None or int(r["Grid_Size"]) == grid):
             key = int(r["Dispatch_Id"])
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
-    keys = sorted(vals)[-last:] if last > 0 else sorted(vals)
+    keys = sorted(vals)[-last * stride:] if last > 0 else sorted(vals)
+    # a template + grid launched `stride` times per step: this site is the
+    # `offset`-th of them in dispatch order
+    keys = keys[offset::stride]
     return (sum(vals[k] for k in keys) / len(keys), len(keys)) if keys else (None, 0)
 
 
@@ -40,11 +43,13 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--last", type=int, default=0)
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--offset", type=int, default=0)
     ap.add_argument("--algorithmic", type=float, default=None,
                     help="algorithmic bytes per launch (bench.py), for the traffic ratio")
     a = ap.parse_args()
-    f, nf = mean_counter(a.fetch, a.kernel, "FETCH_SIZE", a.grid, a.last)
-    w, nw = mean_counter(a.write, a.kernel, "WRITE_SIZE", a.grid, a.last)
+    f, nf = mean_counter(a.fetch, a.kernel, "FETCH_SIZE", a.grid, a.last, a.stride, a.offset)
+    w, nw = mean_counter(a.write, a.kernel, "WRITE_SIZE", a.grid, a.last, a.stride, a.offset)
     out = {"config": a.config, "site": a.site, "kernel": a.kernel, "grid": a.grid, "launches": min(nf, nw),
            "fetch_size_kb": f, "write_size_kb": w,
            "hbm_bytes_per_launch": (2 * f + w) * 1024 if f is not None and w is not None else None,

@@ -1,0 +1,41 @@
+"""(kernel, grid, duration) of the main bench sites in the last eager step of a
+rocprofv3 kernel trace of bench.py (the per-kernel timing pass runs each step
+eagerly behind a stream hold, after the timed graph replays):
+
+    python tools/site_kernels.py gpurun_out/prof_c2/stats/run_kernel_trace.csv
+
+fwd.q_gemm.l0 = the step's first gemm_f32_kernel<true, true, ...> (gathered
+rows x Q^T), fwd.aggw.l0 = its first agg_w_kernel, bwd.q_wgrad.l0 = the last
+gemm_f32_kernel<false, false, ...> before the publish kernel (dQ0 closes the
+backward on the main stream, pinsage engine_backward)."""
+import csv
+import json
+import sys
+
+
+def main(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    holds = [i for i, r in enumerate(rows) if "stream_hold" in r["Kernel_Name"]]
+    step = rows[holds[-1] + 1:]
+    end = next((i for i, r in enumerate(step) if "step_publish" in r["Kernel_Name"]), len(step))
+    step = step[:end]
+
+    def rec(r):
+        name = r["Kernel_Name"].replace("void ", "").split("(")[0]
+        return {"kernel": name, "grid": int(r["Grid_Size_X"]),
+                "us": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3}
+    out = {}
+    for r in step:
+        n = r["Kernel_Name"]
+        if "fwd.q_gemm.l0" not in out and "gemm_f32_kernel<true, true" in n:
+            out["fwd.q_gemm.l0"] = rec(r)
+        if "fwd.aggw.l0" not in out and "agg_w_kernel" in n:
+            out["fwd.aggw.l0"] = rec(r)
+        if "gemm_f32_kernel<false, false" in n:
+            out["bwd.q_wgrad.l0"] = rec(r)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
