@@ -90,6 +90,7 @@ _SIGS = {
     "pinsage_engine_offsets": (ctypes.c_int, [vp, ctypes.POINTER(EngineOffsets)]),
     "pinsage_engine_set_tensors": (ctypes.c_int, [vp, vp, i64, vp, vp, i64, vp, vp, vp, vp]),
     "pinsage_engine_forward": (ctypes.c_int, [vp, vp, vp, i64, vp]),
+    "pinsage_engine_forward_inference": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_frontier": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_forward_layers": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_set_fork": (ctypes.c_int, [vp, vp, vp, i64, vp]),

@@ -394,7 +394,8 @@ static inline void with_sk(const Engine& E, void* ws, GemmParams& p) {
 // scatter targets).  engine_layers runs the projections, aggregations and the
 // head.  A trainer with two workspaces runs step i+1's frontier beside step
 // i's backward (pinsage_training._FusedStep).
-int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st) {
+int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st,
+                    bool with_csr = true) {
   const EngineConfig& c = E.cfg;
   PS_REQUIRE(E.feats && E.nb && E.wn && E.params, kErrArg, "engine: pointers not set");
   PS_REQUIRE(n_pos > 0 && n_pos <= c.max_pos, kErrArg, "engine: n_pos out of range");
@@ -452,7 +453,9 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
   // the transposes of the neighbour slots (CSR of slot occurrences by q row,
   // the aggregation backward's plan) depend only on the frontier: built here,
   // on the frontier's stream -- for a trainer's look-ahead frontier that is
-  // beside the previous step, so the backward never waits for them
+  // beside the previous step, so the backward never waits for them.  An
+  // inference forward (no backward will follow) skips them.
+  if (!with_csr) return kOk;
   PS_TRY(csr_prepare());
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
@@ -571,8 +574,9 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   return launch_gemm(g2, st);
 }
 
-int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st) {
-  PS_TRY(engine_frontier(E, ws, ids_dev, n_pos, st));
+int engine_forward(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, hipStream_t st,
+                   bool with_csr = true) {
+  PS_TRY(engine_frontier(E, ws, ids_dev, n_pos, st, with_csr));
   return engine_layers(E, ws, st);
 }
 
@@ -1139,6 +1143,11 @@ int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream) {
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                            void* stream) {
   return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
+}
+
+int pinsage_engine_forward_inference(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
+                                     void* stream) {
+  return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream, false);
 }
 
 int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,

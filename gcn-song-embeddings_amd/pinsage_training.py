@@ -954,6 +954,41 @@ def save_embeddings(trainer, dataset, base_run_dir=BASE_RUN_DIR, override_run_na
             torch.save(emb[j, :].clone(), save_path)
 
 
+def save_embeddings_tensor(trainer, dataset, base_run_dir=BASE_RUN_DIR, override_run_name=None,
+                           bsize=1 << 16):
+    """The embeddings of every track as ONE file (an extension beside the
+    reference's per-track files): ``runs/<run>/emb.pt``
+    holds ``{"ids": [track ids in dataset order], "emb": f32 [n, out]}``, the
+    rows save_embeddings writes one file each, computed in ``bsize`` batches
+    on the device.  Returns the path."""
+    track_ids = list(dataset.tracks)
+    n = len(track_ids)
+    run_name = override_run_name if override_run_name else trainer.run_name
+    run_dir = os.path.join(base_run_dir, run_name)
+    os.makedirs(run_dir, exist_ok=True)
+    emb = torch.empty((n, trainer.out_dim), dtype=torch.float32)
+    trainer.model.eval()
+    with torch.no_grad():
+        for i in range(0, n, bsize):
+            ids = torch.arange(i, min(i + bsize, n))
+            emb[i:i + ids.shape[0]] = trainer.model(trainer.features, ids).cpu()
+    path = os.path.join(run_dir, "emb.pt")
+    torch.save({"ids": track_ids, "emb": emb}, path)
+    return path
+
+
+def load_embeddings_tensor(trainer, dataset=None, base_run_dir=BASE_RUN_DIR):
+    """(ids, emb) of save_embeddings_tensor's file; rows reordered to
+    ``dataset.tracks`` when a dataset is given."""
+    d = torch.load(os.path.join(base_run_dir, trainer.run_name, "emb.pt"), weights_only=True)
+    ids, emb = d["ids"], d["emb"]
+    if dataset is not None:
+        pos = {t: i for i, t in enumerate(ids)}
+        order = torch.tensor([pos[t] for t in dataset.tracks], dtype=torch.int64)
+        ids, emb = list(dataset.tracks), emb[order]
+    return ids, emb
+
+
 def load_embeddings(trainer, dataset, base_run_dir=BASE_RUN_DIR):
     emb_dir = os.path.join(base_run_dir, trainer.run_name, "emb")
     return torch.stack([torch.load(os.path.join(emb_dir, t + ".pt"), weights_only=True)

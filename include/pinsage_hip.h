@@ -275,6 +275,11 @@ int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int6
  * table -- no parameters -- so a trainer with two workspaces runs the next
  * step's frontier on a side stream while this step's layers and backward run
  * in the other workspace. */
+/* pinsage_engine_forward without the backward's plan (the CSR transposes of the
+ * neighbour slots): for outputs only (PinSage.embed, evaluation, the first pass
+ * of the micro-batched step); no backward may follow on this workspace. */
+int pinsage_engine_forward_inference(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
+                                     void* stream);
 int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                             void* stream);
 int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream);

@@ -480,3 +480,36 @@ def test_fused_ppr_topk_matches_walk_plus_topk(mode, k):
         rw, rn = orc.sample_neighborhood_topt(indptr, indices, pg.n_all, src.numpy()[:48], 500, 0.85, k,
                                               orc.MT(99))
         assert (w[:48].cpu().numpy() == rw).all() and (nb[:48].cpu().numpy() == rn).all()
+
+
+@pytest.mark.parametrize("dims,T,n", [((24, 16, 32), 4, 300), ((128, 128, 512), 10, 700), ((256, 128, 512), 50, 200)])
+def test_conv_layer_autograd_vs_oracle(dims, T, n):
+    """Standalone ConvLayer (pinsage_model.py:171-212) trained through autograd:
+    output, every parameter gradient and the gradient of h (a wider h than
+    in_dim; repeated nodeset rows) vs the oracle's ConvLayer under a fixed
+    random cotangent, at the reference init (xavier, bias 0.3)."""
+    import pinsage_model as pm
+    from oracle import oracle as orc
+    d_in, out, hid = dims
+    rng = np.random.default_rng(d_in + T)
+    n_items = 5000
+    torch.manual_seed(d_in)
+    conv = pm.ConvLayer(d_in, out, hid).cuda()
+    h = torch.from_numpy(rng.standard_normal((n_items, d_in + 8)).astype(np.float32))
+    ns = rng.integers(0, n_items, n)
+    ns[3] = ns[7]
+    nb = rng.integers(0, n_items, (n, T))
+    w = rng.integers(1, 60, (n, T)).astype(np.float64) / 500.0
+    c = torch.from_numpy(rng.standard_normal((n, out)).astype(np.float32))
+    hg = h.cuda().requires_grad_()
+    y = conv(hg, torch.from_numpy(ns), torch.from_numpy(nb), torch.from_numpy(w))
+    (y * c.cuda()).sum().backward()
+    p = {f"conv_layers.0.{k}": v.detach().cpu().clone().requires_grad_() for k, v in conv.state_dict().items()}
+    hr = h.clone().requires_grad_()
+    yr = orc.conv_layer(p, 0, hr, torch.from_numpy(ns), torch.from_numpy(nb), torch.from_numpy(w), d_in)
+    (yr * c).sum().backward()
+    assert _rel(y.detach().cpu().numpy(), yr.detach().numpy()) < REL_TOL
+    for k, prm in conv.named_parameters():
+        assert _rel(prm.grad.cpu().numpy(), p[f"conv_layers.0.{k}"].grad.numpy()) < REL_TOL, k
+    assert _rel(hg.grad.cpu().numpy(), hr.grad.numpy()) < REL_TOL
+    assert float(hg.grad[:, d_in:].abs().max()) == 0.0

@@ -103,6 +103,20 @@ def test_embed_and_embedding_files():
             allv = pt.load_embeddings(tr, ds, base_run_dir=os.path.join(tmp, "runs"))
             full = tr.embed().detach().cpu()
             assert torch.allclose(allv, full, rtol=1e-5, atol=1e-6)
+            # the exported embeddings vs the oracle's reference forward over every track
+            from oracle import oracle as orc
+            params = {k: v.detach().cpu() for k, v in tr.model.state_dict().items()}
+            w, nb = tr.nbhds
+            ref = orc.model_forward(params, feats.cpu(), np.arange(N), tr.n_layers, tr.T, np.asarray(w),
+                                    np.asarray(nb), tr.out_dim).detach().numpy()
+            err = np.linalg.norm(allv.numpy() - ref, axis=1) / np.linalg.norm(ref, axis=1)
+            assert err.max() < 1e-4, err.max()
+            # one-tensor export: the same rows, dataset order
+            path = pt.save_embeddings_tensor(tr, ds, base_run_dir=os.path.join(tmp, "runs"), bsize=1000)
+            assert os.path.isfile(path)
+            ids_t, emb_t = pt.load_embeddings_tensor(tr, ds, base_run_dir=os.path.join(tmp, "runs"))
+            assert ids_t == list(ds.tracks)
+            assert torch.allclose(emb_t, allv, rtol=1e-5, atol=1e-6)
         finally:
             os.chdir(cwd)
 
