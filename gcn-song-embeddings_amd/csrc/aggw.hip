@@ -5,37 +5,39 @@
 //             pre-normalised by their f64 row sum = sum(w*q)/sum(w))
 //   y[f]    = normalize(lrelu([h[self f] || agg[f]] W^T + b))   (:208-211)
 //
-// One workgroup (16 waves) per 32 rows.  It stages the 32 rows' A operand
+// One workgroup (8 waves) per 16 rows, two workgroups per CU, so one
+// workgroup's gather overlaps the other's projection (a 32-row tile at one
+// workgroup per CU ran gather, then MFMA, then epilogue back to back: 38 us at
+// C2, 55 us at C4).  The workgroup stages the 16 rows' A operand
 // [h_self || agg] in LDS -- the self rows gathered from h, the aggregate formed
 // right there from the T gathered q rows (fma in slot order t = 0, 1, ..., the
 // same arithmetic as agg_kernel) and also written out for the backward's
-// weight gradient -- so agg is never read back from memory and the launch
-// between the two disappears.  The projection then runs on fp32 MFMA
-// (v_mfma_f32_32x32x2_f32) with the K dimension split four ways across the
-// waves: wave (kq, cg) owns output columns 32 cg .. 32 cg + 31 over the k
-// quarter kq, so a 32-row tile's dependent MFMA chain is K / 8 long instead of
-// K / 2 (the unfused 32 x 128 tile ran one chain per SIMD over all of K and was
-// latency-bound).  B fragments (W rows, K-major) stream from global / L2 with a
-// one-chunk register double buffer.  The four quarters' partial tiles are
-// summed in LDS in a fixed order, then bias, LeakyReLU and the row L2 norm.
+// weight gradient -- so agg is never read back from memory.  The projection
+// runs on fp32 MFMA v_mfma_f32_16x16x4_f32: wave w owns output columns
+// 16 w .. 16 w + 15 over all of K, two accumulators alternating (its 40-cycle
+// dependent latency over a 32-cycle issue); A fragments are ds_read_b128 of
+// the tile, B fragments (W rows, K-major) stream from global / L2 with a
+// one-chunk register double buffer.  Then bias, LeakyReLU and the row L2 norm
+// through a [16][128] LDS image.
 #include <algorithm>
 
 #include "common.h"
 
 namespace ps {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kAwRows = 32;     // rows per workgroup
-constexpr int kAwOut = 128;     // out_dim (4 column groups of 32)
-constexpr int kAwThreads = 1024;
+constexpr int kAwRows = 16;     // rows per workgroup
+constexpr int kAwOut = 128;     // out_dim (8 column groups of 16)
+constexpr int kAwThreads = 512;
 constexpr int kAwTMax = 64;     // fanout held in LDS per row
 
-// LDS: A tile [32][K + 4] floats (row stride = 4 mod 64 banks: b128 fragment
-// reads of 16 consecutive rows hit distinct banks), then the tile's slot lists.
+// LDS: A tile [16][K + 4] floats (row stride = 4 mod 64 banks: the b128
+// fragment reads of 16 rows x 4 k-quads hit distinct banks), then the tile's
+// slot lists.
 __device__ __forceinline__ int aw_lda(int K) { return K + 4; }
 
-__global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
+__global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
     const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
     const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
     const float* __restrict__ wloc, int T, const int* __restrict__ nS,
@@ -43,10 +45,10 @@ __global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
     float* __restrict__ nrm_out, float* __restrict__ agg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int K = d + hid, lda = aw_lda(K);
-  float* sA = lds;                                          // [32][lda]
-  int* sLoc = reinterpret_cast<int*>(lds + kAwRows * lda);  // [32][T]
-  float* sW = reinterpret_cast<float*>(sLoc + kAwRows * kAwTMax);  // [32][T]
-  int* sSelf = reinterpret_cast<int*>(sW + kAwRows * kAwTMax);     // [32]
+  float* sA = lds;                                          // [16][lda]
+  int* sLoc = reinterpret_cast<int*>(lds + kAwRows * lda);  // [16][T]
+  float* sW = reinterpret_cast<float*>(sLoc + kAwRows * kAwTMax);  // [16][T]
+  int* sSelf = reinterpret_cast<int*>(sW + kAwRows * kAwTMax);     // [16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t F = *nS;
   const int64_t tiles = (F + kAwRows - 1) / kAwRows;
@@ -131,13 +133,186 @@ __global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
       }
     }
     __syncthreads();
+    // ---- projection: wave w, columns 16 w .. 16 w + 15, all of K.
+    // v_mfma_f32_16x16x4_f32: lane l supplies A[row l & 15][k] and B[k][col l & 15]
+    // for k = (l >> 4) (+4 per instruction); a float4 of k-quad g = l >> 4 feeds
+    // four instructions, the r-th taking k = 16 s + 4 g + r (a bijection onto the
+    // 16 k of chunk s)
+    const int l16 = lane & 15, g = lane >> 4;
+    const float* wrow = W + (int64_t)(wave * 16 + l16) * K;
+    const float* arow = sA + l16 * lda;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    // chunks of 4 k-sixteens (64 k); B fragments of chunk c+1 load while c runs
+    const int nch = K / 64;
+    float4 bcur[4], bnxt[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) bcur[s2] = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 4 * g);
+    for (int ch = 0; ch < nch; ++ch) {
+      const int k0 = 64 * ch;
+      if (ch + 1 < nch) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+          bnxt[s2] = *reinterpret_cast<const float4*>(wrow + k0 + 64 + 16 * s2 + 4 * g);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const float4 av = *reinterpret_cast<const float4*>(arow + k0 + 16 * s2 + 4 * g);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bcur[s2].x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bcur[s2].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bcur[s2].z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bcur[s2].w, acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) bcur[s2] = bnxt[s2];
+    }
+    __syncthreads();  // every wave is done reading the A tile
+    // ---- the [16][128] output tile -> LDS, then bias, lrelu, row L2 norm
+    float* red = sA;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(4 * g + r) * kAwOut + wave * 16 + l16] = acc0[r] + acc1[r];
+    __syncthreads();
+    {
+      const int row = tid >> 5, c4 = tid & 31;  // 4 columns 4 c4 .. 4 c4 + 3
+      float v[4];
+      float s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = 4 * c4 + e;
+        const float x = lrelu(red[row * kAwOut + col] + bias[col]);
+        v[e] = x;
+        s2 += x * x;
+      }
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+      const float nrm = sqrtf(s2);
+      if (row < nrows) {
+        *reinterpret_cast<float4*>(y + (r0 + row) * kAwOut + 4 * c4) =
+            make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
+        if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
+      }
+    }
+    __syncthreads();  // LDS is reused by the next tile
+  }
+}
+
+typedef float aw_f32x16 __attribute__((ext_vector_type(16)));
+
+// The 32-row variant (one 1024-thread workgroup per CU, K split four ways
+// over the waves, v_mfma_f32_32x32x2_f32): reads W once per 32 rows instead
+// of per 16, which wins at K = d + hid = 1024 (C2/C3 layer 0: 41.6 vs 54.9 us
+// at C2); the 16-row kernel above wins at K = 640 (C2 layer 1: 22.5 vs 29.9 us).
+constexpr int kAw32Rows = 32;     // rows per workgroup
+constexpr int kAw32Out = 128;     // out_dim (4 column groups of 32)
+constexpr int kAw32Threads = 1024;
+constexpr int kAw32TMax = 64;     // fanout held in LDS per row
+
+// LDS: A tile [32][K + 4] floats (row stride = 4 mod 64 banks: b128 fragment
+// reads of 16 consecutive rows hit distinct banks), then the tile's slot lists.
+__device__ __forceinline__ int aw32_lda(int K) { return K + 4; }
+
+__global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
+    const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
+    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
+    const float* __restrict__ wloc, int T, const int* __restrict__ nS,
+    const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y,
+    float* __restrict__ nrm_out, float* __restrict__ agg) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int K = d + hid, lda = aw32_lda(K);
+  float* sA = lds;                                          // [32][lda]
+  int* sLoc = reinterpret_cast<int*>(lds + kAw32Rows * lda);  // [32][T]
+  float* sW = reinterpret_cast<float*>(sLoc + kAw32Rows * kAw32TMax);  // [32][T]
+  int* sSelf = reinterpret_cast<int*>(sW + kAw32Rows * kAw32TMax);     // [32]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t F = *nS;
+  const int64_t tiles = (F + kAw32Rows - 1) / kAw32Rows;
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * kAw32Rows;
+    const int nrows = (int)min((int64_t)kAw32Rows, F - r0);
+    // ---- slot lists and self-row indices of the tile
+    for (int i = tid; i < kAw32Rows * T; i += kAw32Threads) {
+      const int row = i / T, t = i - row * T;
+      const bool ok = row < nrows;
+      sLoc[row * kAw32TMax + t] = ok ? loc[(r0 + row) * T + t] : 0;
+      sW[row * kAw32TMax + t] = ok ? wloc[(r0 + row) * T + t] : 0.f;
+    }
+    if (tid < kAw32Rows) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : 0;
+    __syncthreads();
+    // ---- self rows -> A[:, 0:d)
+    {
+      const int d4 = d >> 2;
+      for (int i = tid; i < kAw32Rows * d4; i += kAw32Threads) {
+        const int row = i / d4, c4 = i - row * d4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nrows) v = *reinterpret_cast<const float4*>(h + (int64_t)sSelf[row] * ldh + 4 * c4);
+        *reinterpret_cast<float4*>(sA + row * lda + 4 * c4) = v;
+      }
+    }
+    // ---- aggregate -> A[:, d:K) and agg (thread: row tid / 32, float4 columns
+    //      (tid % 32) + 32 j); four slots' rows in flight per round
+    {
+      const int row = tid >> 5, c0 = tid & 31, h4 = hid >> 2;
+      const int nj = (h4 + 31) / 32;
+      for (int j0 = 0; j0 < nj; j0 += 4) {
+        float4 a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nrows) {
+          int t = 0;
+          for (; t + 4 <= T; t += 4) {
+            float4 x[4][4];
+            float w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sLoc[row * kAw32TMax + t + u] * hid);
+              w[u] = sW[row * kAw32TMax + t + u];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int c = min(c0 + 32 * (j0 + j), h4 - 1);
+                x[u][j] = qr[c];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                a[j].x = fmaf(w[u], x[u][j].x, a[j].x);
+                a[j].y = fmaf(w[u], x[u][j].y, a[j].y);
+                a[j].z = fmaf(w[u], x[u][j].z, a[j].z);
+                a[j].w = fmaf(w[u], x[u][j].w, a[j].w);
+              }
+          }
+          for (; t < T; ++t) {
+            const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sLoc[row * kAw32TMax + t] * hid);
+            const float w = sW[row * kAw32TMax + t];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int c = min(c0 + 32 * (j0 + j), h4 - 1);
+              const float4 x = qr[c];
+              a[j].x = fmaf(w, x.x, a[j].x);
+              a[j].y = fmaf(w, x.y, a[j].y);
+              a[j].z = fmaf(w, x.z, a[j].z);
+              a[j].w = fmaf(w, x.w, a[j].w);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = c0 + 32 * (j0 + j);
+          if (c < h4) {
+            *reinterpret_cast<float4*>(sA + row * lda + d + 4 * c) = a[j];
+            if (row < nrows) *reinterpret_cast<float4*>(agg + (r0 + row) * hid + 4 * c) = a[j];
+          }
+        }
+      }
+    }
+    __syncthreads();
     // ---- projection: wave (kq, cg), k quarter kq, columns 32 cg ..
     const int cg = wave & 3, kq = wave >> 2;
     const int l32 = lane & 31, hh = lane >> 5;
     const int kspan = K >> 2, kb = kq * kspan;
     const float* wrow = W + (int64_t)(cg * 32 + l32) * K;
     const float* arow = sA + l32 * lda;
-    f32x16 acc;
+    aw_f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     // chunks of 4 k-octets (32 k); B fragments of chunk c+1 load while c runs
@@ -169,7 +344,7 @@ __global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
-      red[(kq * kAwRows + row) * kAwOut + cg * 32 + l32] = acc[r];
+      red[(kq * kAw32Rows + row) * kAw32Out + cg * 32 + l32] = acc[r];
     }
     __syncthreads();
     {
@@ -179,10 +354,10 @@ __global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int col = 4 * c4 + e;
-        float x = red[(0 * kAwRows + row) * kAwOut + col];
-        x += red[(1 * kAwRows + row) * kAwOut + col];
-        x += red[(2 * kAwRows + row) * kAwOut + col];
-        x += red[(3 * kAwRows + row) * kAwOut + col];
+        float x = red[(0 * kAw32Rows + row) * kAw32Out + col];
+        x += red[(1 * kAw32Rows + row) * kAw32Out + col];
+        x += red[(2 * kAw32Rows + row) * kAw32Out + col];
+        x += red[(3 * kAw32Rows + row) * kAw32Out + col];
         x = lrelu(x + bias[col]);
         v[e] = x;
         s2 += x * x;
@@ -191,7 +366,7 @@ __global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
       for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
       const float nrm = sqrtf(s2);
       if (row < nrows) {
-        *reinterpret_cast<float4*>(y + (r0 + row) * kAwOut + 4 * c4) =
+        *reinterpret_cast<float4*>(y + (r0 + row) * kAw32Out + 4 * c4) =
             make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
         if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
       }
@@ -200,12 +375,19 @@ __global__ __launch_bounds__(kAwThreads) void agg_w_kernel(
   }
 }
 
+static int agg_w32_supported(int64_t d, int64_t hid, int64_t T) {
+  const int64_t K = d + hid;
+  const int64_t lds = (int64_t)kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
+  return K % 128 == 0 && K + 4 >= 4 * kAw32Out && T <= kAw32TMax && lds <= 160 * 1024;
+}
+
 int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
   const int64_t K = d + hid;
   const int64_t lds = (int64_t)kAwRows * (K + 4) * 4 + 2 * kAwRows * kAwTMax * 4 + kAwRows * 4;
-  // the A tile's LDS is reused for the four partial 32 x 128 tiles: K + 4 >= 512
-  return out == kAwOut && K % 128 == 0 && K + 4 >= 4 * kAwOut && hid % 4 == 0 && d % 4 == 0 &&
-         T >= 1 && T <= kAwTMax && lds <= 160 * 1024;
+  // the A tile's LDS is reused for the [16][128] output tile (K + 4 >= 128);
+  // two workgroups per CU; the aggregation pass covers hid in passes of 512
+  return out == kAwOut && K % 64 == 0 && K + 4 >= kAwOut && hid % 4 == 0 && d % 4 == 0 &&
+         T >= 1 && T <= kAwTMax && 2 * lds <= 160 * 1024;
 }
 
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
@@ -226,9 +408,22 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int64_t tiles = (S_max + kAwRows - 1) / kAwRows;
-  const int grid = (int)std::min<int64_t>(tiles, cus);
-  hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
-                     loc, wloc, T, nS, W, bias, y, nrm, agg);
+  const int grid = (int)std::min<int64_t>(tiles, 2 * (int64_t)cus);
+  if (K >= 1024 && agg_w32_supported(d, hid, T)) {
+    const int lds32 = kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
+    static bool prepared32 = false;
+    if (!prepared32) {
+      PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      prepared32 = true;
+    }
+    const int64_t tiles32 = (S_max + kAw32Rows - 1) / kAw32Rows;
+    hipLaunchKernelGGL(agg_w32_kernel, dim3((int)std::min<int64_t>(tiles32, cus)), dim3(kAw32Threads), lds32,
+                       st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, W, bias, y, nrm, agg);
+  } else {
+    hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
+                       loc, wloc, T, nS, W, bias, y, nrm, agg);
+  }
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -477,6 +477,17 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
   return launch_gemm(p, (hipStream_t)stream);
 }
 
+int pinsage_gemm_set_prec(int prec) {
+  if (prec < 0 || prec > 1) {
+    set_error("gemm_set_prec: 0 (fp32 MFMA) or 1 (split bf16)");
+    return kErrArg;
+  }
+  gemm_set_default_prec(prec);
+  return kOk;
+}
+
+int pinsage_gemm_get_prec(void) { return gemm_default_prec(); }
+
 int64_t pinsage_knn_scratch_bytes(int64_t n, int64_t batch_rows) {
   return knn_scratch_bytes(n, batch_rows < 1 ? 1 : batch_rows);
 }

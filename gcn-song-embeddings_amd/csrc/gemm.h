@@ -74,7 +74,17 @@ struct GemmParams {
                                   // the critical chain leaves the other CUs to it)
   int stream_k = -1;              // -1 choose by size, 0 off, 1 on (when allowed)
   int sk_min_units = 4;           // k-steps per block at least
+  // product arithmetic: 0 = v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains);
+  // 1 = split bf16 (each fp32 operand = hi + mid + lo bf16 exactly to 2^-26,
+  // six v_mfma_f32_32x32x16_bf16 products per 16-k step, fp32 accumulation:
+  // fp32-level error at 2.67x the f32 MFMA rate); K-major A and B only;
+  // -1 = the library default (PINSAGE_GEMM_PREC, else 1 where allowed)
+  int prec = -1;
 };
+
+// default product arithmetic (GemmParams::prec = -1): 0 fp32 MFMA, 1 split bf16
+int gemm_default_prec();
+void gemm_set_default_prec(int prec);
 
 // slab floats a stream-K launch may use (two partial tiles per resident block)
 int64_t gemm_sk_slab_floats();

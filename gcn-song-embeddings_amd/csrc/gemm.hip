@@ -24,6 +24,24 @@
 namespace ps {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// x = H + M + L with H, M, L bf16: H = RN(x), M = RN(x - H), L = RN(x - H - M);
+// both differences are exact in fp32, so |x - (H + M + L)| <= 2^-9 |x - H - M|
+// <= 2^-26 |x| (the pieces have the exponent range of fp32).
+__device__ __forceinline__ void split3(const float4& a, const float4& b, bf16x8& H, bf16x8& M, bf16x8& L) {
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)x[j];
+    const float r = x[j] - (float)h;
+    const __bf16 m = (__bf16)r;
+    const float s = r - (float)m;
+    H[j] = h;
+    M[j] = m;
+    L[j] = (__bf16)s;
+  }
+}
 
 constexpr int kLdsBudget = 81920;  // bytes per workgroup: two workgroups per CU
 constexpr int kLdsBudget3 = 54272;  // three workgroups per CU (cfg 3)
@@ -189,8 +207,10 @@ __device__ __forceinline__ void wait_stage(int younger) {
 
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK; at most
 // NSMAX stage buffers in the ring.
-template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2>
+template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2,
+          bool BF = false>
 __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
+  static_assert(!BF || (AK && BKM && BK % 16 == 0), "split-bf16 products: K-major operands, 16-k steps");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
   using OpB = typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type;
@@ -300,6 +320,39 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
           }
       };
+      if constexpr (BF) {
+        // 16-k steps: lane (row l32, half h) holds k = 16 t + 8 h + j, j = 0..7
+        // (two float4 of the swizzled K-major image), split into hi / mid / lo;
+        // the products whose magnitude is >= 2^-18 of hi*hi, smallest first
+#pragma unroll
+        for (int t = 0; t < BK / 16; ++t) {
+          bf16x8 aH[TM], aM[TM], aL[TM], bH[TN], bM[TN], bL[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const int r = (wm * TM + i) * 32 + l32;
+            split3(OpA::frag(As, r, 16 * t + 8 * h), OpA::frag(As, r, 16 * t + 8 * h + 4), aH[i], aM[i],
+                   aL[i]);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int c = (wn * TN + j) * 32 + l32;
+            split3(OpB::frag(Bs, c, 16 * t + 8 * h), OpB::frag(Bs, c, 16 * t + 8 * h + 4), bH[j], bM[j],
+                   bL[j]);
+          }
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[i], bH[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[i], bL[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM[i], bM[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM[i], bH[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[i], bM[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[i], bH[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        return;
+      }
       static_assert((BK / 8) % 2 == 0, "octets are processed in pairs");
       // sched_barrier pins the prefetch distance (the scheduler otherwise
       // sinks each read next to its MFMAs and exposes the LDS latency)
@@ -575,6 +628,15 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
 
 constexpr int kCfgBM[5] = {128, 64, 32, 64, 64};
 
+// the product arithmetic of GEMMs that do not choose (GemmParams::prec < 0):
+// PINSAGE_GEMM_PREC at load, then pinsage_gemm_set_prec
+static int g_prec = -1;
+int gemm_default_prec() {
+  if (g_prec < 0) g_prec = getenv("PINSAGE_GEMM_PREC") ? atoi(getenv("PINSAGE_GEMM_PREC")) : 1;
+  return g_prec;
+}
+void gemm_set_default_prec(int prec) { g_prec = prec; }
+
 int gemm_slots() {
   static const int slots = [] {
     int dev = 0, cus = 0;
@@ -621,6 +683,21 @@ int gemm_pick_config(int M, int N, int K, int splits) {
 
 template <bool AK, bool BKM>
 static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
+  if constexpr (AK && BKM) {
+    if (p.prec == 1) {  // split-bf16 products
+      if (cfg == 0)
+        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 2, 2, 16, 4, 2, true>), g, dim3(256), 0, st, p);
+      else if (cfg == 1)
+        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 1, 2, 32, 4, 2, true>), g, dim3(256), 0, st, p);
+      else if (cfg == 2)
+        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 1, 4, 1, 1, 32, 4, 2, true>), g, dim3(256), 0, st, p);
+      else if (cfg == 3)
+        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 1, 2, 16, 4, 3, true>), g, dim3(256), 0, st, p);
+      else
+        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 1, 2, 16, 3, 4, true>), g, dim3(256), 0, st, p);
+      return;
+    }
+  }
   if (cfg == 0)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16>), g, dim3(256), 0, st, p);
   else if (cfg == 1)
@@ -661,6 +738,8 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
   PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
              "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
+  if (p.prec < 0) p.prec = gemm_default_prec();
+  if (!(p.a_kmajor && p.b_kmajor)) p.prec = 0;
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
   int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, Kmax, splits);

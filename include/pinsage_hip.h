@@ -170,6 +170,15 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
                     int64_t lda, const int32_t* a_idx, const float* B, int64_t ldb,
                     const int32_t* b_idx, float* C, int64_t ldc, const float* bias, int act,
                     int epi, int splits, int cfg, int stream_k, void* stream);
+/* Product arithmetic of the fp32 GEMMs with K-major operands (the Q / W
+ * projections of the forward, the kNN dot products): 0 = v_mfma_f32_32x32x2_f32
+ * (exact fp32 FMA chains); 1 (default; PINSAGE_GEMM_PREC overrides at load) =
+ * each fp32 operand split exactly into hi + mid + lo bf16 (|residual| <= 2^-26
+ * |x|), the six products down to 2^-18 of hi*hi on v_mfma_f32_32x32x16_bf16
+ * with fp32 accumulation: fp32-level error at 2.67x the fp32 MFMA rate.
+ * Process-wide; other GEMMs always use fp32 MFMA. */
+int pinsage_gemm_set_prec(int prec);
+int pinsage_gemm_get_prec(void);
 /* agg[f] = sum_t w[f][t] * q[loc[f][t]]  (weights already normalised;
  * pinsage_model.py:202). */
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,

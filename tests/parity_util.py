@@ -12,7 +12,8 @@ each one well conditioned:
    row-norm relative;
 2. hinge arguments: the engine's per-triple value (written by its loss kernel)
    vs the oracle's; a triple whose activity differs must have |arg| <= 1e-6;
-3. loss within 1e-4 relative;
+3. loss within 1e-4 relative, plus what the hinge arguments' own fp32 error
+   (|arg| <= 1e-5 absolute) contributes to their clamped mean;
 4. (A) the oracle's gradient over the GPU's active set, with the oracle's own
    forward, vs the GPU's gradients;
 5. (B) the oracle's backward driven by the cotangent of the GPU's own outputs
@@ -160,7 +161,14 @@ def check_record(rec, feats, w, nb, tol=1e-4, kink=1e-6, strict_a=True, report=N
     # the assertions
     assert res["fwd_row_rel_max"] <= tol, res
     assert res["hinge_flip_arg_max"] <= kink, res
-    assert abs(loss - ref_loss) <= tol * abs(ref_loss) + kink / B, res
+    # the hinge arguments are differences of cosines of unit rows (O(1) values):
+    # fp32 holds them to a few 1e-7 absolute
+    assert res["hinge_abs_max"] <= 1e-5, res
+    # the loss is their clamped mean: at the reference's margin it is ~1e-5, a
+    # cancellation of O(1) cosines, so its error is bounded by the arguments'
+    # (mean absolute error over the active triples), not by 1e-4 of itself
+    assert abs(loss - ref_loss) <= tol * abs(ref_loss) + (kink * res["hinge_flips"]
+                                                           + res["hinge_abs_max"] * res["active"]) / B, res
     assert res["grad_rel_B_max"] <= (tol if tol_b is None else tol_b), res
     if strict_a:
         assert res["grad_rel_A_max"] <= tol, res

@@ -148,9 +148,36 @@ def test_train_step_on_the_fly_vs_oracle(margin, repeats):
             (dz,) = torch.autograd.grad((mask * args).sum() / batch.shape[0], [zt])
             lossB = sum((hs[c] * dz[:, c].float()).sum() for c in range(3))
             gB = torch.autograd.grad(lossB, [p[k] for k in init], allow_unused=True)
+            # at the reference init the 2-layer, T = 3 model's outputs are nearly
+            # collapsed: gradients of the head (G1.bias: per-row terms that almost
+            # cancel) sit at ~1e-4 even under one shared cotangent, so part B holds
+            # 2e-4 here; the kernels are pinned at 1e-4 under a random cotangent below
             for k, gb in zip(init, gB):
                 gb = np.zeros(init[k].shape) if gb is None else gb.double().numpy()
                 a = gpu_grads[k]
-                assert np.linalg.norm(a - gb) <= 1e-4 * np.linalg.norm(gb) + 1e-12, (k, parity_util.rel(a, gb))
+                assert np.linalg.norm(a - gb) <= 2e-4 * np.linalg.norm(gb) + 1e-12, (k, parity_util.rel(a, gb))
+            # the same three calls' draws under a random cotangent (well conditioned),
+            # at the parameters after the step
+            init_after = {k: v.detach().cpu().numpy().copy() for k, v in tr.model.state_dict().items()}
+            mt2 = orc.MT(99)
+            states = []
+            for c in range(3):
+                mt2.to_torch()
+                states.append(torch.get_rng_state())
+                orc.relevant_nodes_fly(indptr, indices, pg.n_all, batch[:, c], 2, 200, 0.85, 3, mt2)
+            rng_c = np.random.default_rng(3)
+            for c in range(3):
+                ct = torch.from_numpy(rng_c.standard_normal(Z[:, c].shape).astype(np.float32))
+                for prm in tr.model.parameters():
+                    prm.grad = None
+                # replay call c with its own draws
+                torch.set_rng_state(states[c])
+                yc = tr.model(tr.features, torch.from_numpy(batch[:, c]))
+                (yc * ct.to(yc.device)).sum().backward()
+                pc = {k: torch.from_numpy(v).float().requires_grad_() for k, v in init_after.items()}
+                hr = orc.model_forward(pc, feats, batch[:, c], 2, 3, None, None, 128, layers=lays[c])
+                (hr * ct).sum().backward()
+                for k, prm in tr.model.named_parameters():
+                    assert parity_util.rel(prm.grad.cpu().numpy(), pc[k].grad.numpy()) <= 1e-4, (c, k)
         finally:
             os.chdir(cwd)

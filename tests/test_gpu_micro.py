@@ -59,8 +59,10 @@ def _record(tr, b, run):
     init = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()}
     loss, _, _ = run(b)
     grads = {k: p.grad.detach().cpu().numpy().astype(np.float64) for k, p in tr.model.named_parameters()}
-    Z = tr.last_outputs.permute(1, 0, 2).cpu().double()
-    hinge = parity_util._hinge_args(Z[:, 0], Z[:, 1], Z[:, 2], tr.margin).numpy()
+    Zd = tr.last_outputs.permute(1, 0, 2)
+    Z = Zd.cpu().double()
+    # the arguments as the sliced step's loss evaluated them (torch fp32 on the device)
+    hinge = parity_util._hinge_args(Zd[:, 0], Zd[:, 1], Zd[:, 2], tr.margin).double().cpu().numpy()
     return dict(init=init, batch=b.numpy(), grads=grads, loss=float(loss), Z=Z.numpy(), hinge=hinge,
                 L=tr.n_layers, T=tr.T, margin=float(tr.margin), out_dim=tr.out_dim)
 

@@ -57,11 +57,11 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_
     rc = lib.pinsage_gemm_ex(*args)
     if rc != 0:
         raise RuntimeError(lib.pinsage_last_error().decode())
-    ref = (A[a_idx.long()] if a_idx is not None else A) if ak else A.t()
-    ref = ref @ ((B.t() if bk else (B[b_idx.long()] if b_idx is not None else B)))
+    ref = ((A[a_idx.long()] if a_idx is not None else A) if ak else A.t()).double()
+    ref = ref @ ((B.t() if bk else (B[b_idx.long()] if b_idx is not None else B))).double()
     if bias_act:
-        ref = torch.nn.functional.leaky_relu(ref + bias)
-    err = ((C.sum(0) - ref).abs().max() / ref.abs().max()).item()
+        ref = torch.nn.functional.leaky_relu(ref + bias.double())
+    err = ((C.sum(0).double() - ref).norm() / ref.norm()).item()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
         lib.pinsage_gemm_ex(*args)
@@ -86,16 +86,19 @@ def main():
     ap.add_argument("--sets", type=int, default=1, help="row sets cycled over repetitions")
     ap.add_argument("--bias-act", action="store_true", help="bias + LeakyReLU epilogue (the Q projection)")
     ap.add_argument("--sorted", action="store_true", help="gathered rows in ascending order")
+    ap.add_argument("--prec", default="1", help="product arithmetic(s) of K-major GEMMs: 0 fp32 MFMA, 1 split bf16")
     a = ap.parse_args()
     lib = nat.lib()
     stream = torch.cuda.current_stream()
     for s in a.shapes:
+      for prec in [int(x) for x in a.prec.split(",")]:
+        lib.pinsage_gemm_set_prec(prec)
         for cfg in [int(c) for c in a.cfgs.split(",")]:
             for sk in [int(c) for c in a.sk.split(",")]:
                 if sk == 1 and cfg == 0:
                     continue
                 us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets, a.bias_act, a.sorted)
-                print(f"{s:24s} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
+                print(f"{s:24s} prec={prec} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
                       flush=True)
 
 
