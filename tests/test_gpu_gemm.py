@@ -158,3 +158,37 @@ def test_weight_gradient_split_k_every_config(cfg, S, shape):
     r = A.double().t() @ B.double()[b_idx.long()]
     assert torch.isfinite(C).all()
     assert _rel(C.sum(0), r) < REL_TOL, _rel(C.sum(0), r)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+def test_split_bf16_products_are_fp32_accurate(cfg):
+    """The split-bf16 product path (K-major operands: x = hi + mid + lo bf16,
+    six 32x32x16 bf16 MFMAs per 16-k step, fp32 accumulation) against float64,
+    next to the exact-fp32 MFMA path on the same data: its error is the fp32
+    path's order (measured below it), with ragged M / K tails, gathered rows,
+    wide-range magnitudes and both schedules."""
+    import _native as nat
+    lib = nat.lib()
+    g = torch.Generator(device="cuda").manual_seed(99 + cfg)
+    old = lib.pinsage_gemm_get_prec()
+    try:
+        for M, N, K in SHAPES:
+            A = torch.randn((M, K), device="cuda", generator=g)
+            A *= torch.exp2(torch.randint(-20, 20, (M, 1), device="cuda", generator=g).float())
+            B = torch.randn((N, K), device="cuda", generator=g)
+            a_idx = torch.randint(0, M, (M,), device="cuda", generator=g, dtype=torch.int32) if M > 1 else None
+            bias = torch.randn(N, device="cuda", generator=g)
+            r = _ref(M, N, K, 1, 1, A, a_idx, B, bias, 1)
+            errs = {}
+            for prec in (0, 1):
+                assert lib.pinsage_gemm_set_prec(prec) == 0
+                for sk in ((0, 1) if cfg else (0,)):
+                    C = torch.full((M, N), float("nan"), device="cuda")
+                    _gemm(M, N, K, 1, 1, A, a_idx, B, C, bias=bias, act=1, cfg=cfg, sk=sk)
+                    torch.cuda.synchronize()
+                    assert torch.isfinite(C).all()
+                    errs[(prec, sk)] = _rel(C, r)
+            assert max(errs[k] for k in errs if k[0] == 1) <= 2.0 * max(errs[k] for k in errs if k[0] == 0) + 1e-9, errs
+            assert max(errs.values()) < 2e-6, errs
+    finally:
+        lib.pinsage_gemm_set_prec(old)
