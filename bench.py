@@ -414,6 +414,12 @@ def main():
     a_traffic, a_traffic_src, _ = pmc_traffic(pmc_key, a_site)
     kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "calls": v[1]} for k, v in sorted(kt.items())}
     traffic, traffic_src, mfma_busy = pmc_traffic(pmc_key, "fwd.q_gemm.l0")
+    prec = nat.lib().pinsage_gemm_get_prec()
+    gemm_arith = ("split bf16: each fp32 operand = hi + mid + lo bf16 (exact to 2^-26), six "
+                  "v_mfma_f32_32x32x16_bf16 products per 16-k step, fp32 accumulation; achieved/peak are "
+                  "algorithmic fp32 FLOP against the fp32 MFMA peak, executed bf16 MFMA work is 6x "
+                  "(mfma_busy_pmc counts those cycles)" if prec == 1 else
+                  "v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains)")
     result = {
         "metric": "PinSAGE train-step nodes/sec (2-hop, batch 512) at 1/2/4/8 MI355X",
         "value": value,
@@ -432,7 +438,8 @@ def main():
                    "n_layers": cfg["n_layers"], "fanout": T, "batch_per_gpu": cfg["batch"],
                    "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
                    "batch_rng": "mt19937 (reference-exact)"},
-        "roofline": {"bound": "mfma", "kernel": "fwd.q_gemm.l0 (gather + fp32 MFMA Q projection)",
+        "roofline": {"bound": "mfma", "kernel": "fwd.q_gemm.l0 (gather + Q projection on MFMA)",
+                     "arithmetic": gemm_arith,
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "mfma_busy_pmc": mfma_busy,

@@ -5,7 +5,7 @@ eagerly behind a stream hold, after the timed graph replays):
     python tools/site_kernels.py gpurun_out/prof_c2/stats/run_kernel_trace.csv
 
 fwd.q_gemm.l0 = the step's first gemm_f32_kernel<true, true, ...> (gathered
-rows x Q^T), fwd.aggw.l0 = its first agg_w_kernel, bwd.q_wgrad.l0 = the last
+rows x Q^T), fwd.aggw.l0 = its first agg_w*_kernel, bwd.q_wgrad.l0 = the last
 gemm_f32_kernel<false, false, ...> before the publish kernel (dQ0 closes the
 backward on the main stream, pinsage engine_backward)."""
 import csv
@@ -30,7 +30,7 @@ def main(path):
         n = r["Kernel_Name"]
         if "fwd.q_gemm.l0" not in out and "gemm_f32_kernel<true, true" in n:
             out["fwd.q_gemm.l0"] = rec(r)
-        if "fwd.aggw.l0" not in out and "agg_w_kernel" in n:
+        if "fwd.aggw.l0" not in out and "agg_w" in n:  # agg_w_kernel or agg_w32_kernel
             out["fwd.aggw.l0"] = rec(r)
         if "gemm_f32_kernel<false, false" in n:
             out["bwd.q_wgrad.l0"] = rec(r)
