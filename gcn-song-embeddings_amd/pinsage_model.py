@@ -528,134 +528,11 @@ class ConvLayer(nn.Module):
     def forward(self, h, nodeset, nb_nodes, nb_weights):
         """Standalone call (inside PinSageModel the fused engine runs all
         layers): the layer's rows for ``nodeset`` from the given neighbourhood
-        rows, differentiable in the parameters and in ``h`` (_ConvLayerFn)."""
-        return _ConvLayerFn.apply(h, nodeset, nb_nodes, nb_weights, self.Q.weight, self.Q.bias,
-                                  self.W.weight, self.W.bias)
-
-
-def _gemm(M, N, K, a_kmajor, b_kmajor, A, lda, B, ldb, C, ldc, a_idx=None, b_idx=None):
-    """C[M][N] = op(A) op(B) on the fp32 MFMA GEMM (pinsage_gemm_ex, plain store)."""
-    nat.check(nat.lib().pinsage_gemm_ex(M, N, K, a_kmajor, b_kmajor, nat.ptr(A), lda, nat.ptr(a_idx),
-                                        nat.ptr(B), ldb, nat.ptr(b_idx), nat.ptr(C), ldc, None, 0, 0, 1,
-                                        -1, 0, nat.stream_ptr()), "gemm_ex")
-
-
-def _pad_rows(x, mult=4):
-    r = (-x.shape[0]) % mult
-    return x if r == 0 else torch.cat([x, x.new_zeros((r,) + tuple(x.shape[1:]))])
-
-
-class _ConvLayerFn(torch.autograd.Function):
-    """ConvLayer.forward (pinsage_model.py:189-212) on the C-ABI kernels:
-
-        q   = lrelu(h[u] Q^T + b_Q)          u = distinct neighbours  (pinsage_linear, gathered rows)
-        agg = sum_t w[f,t] q[loc[f,t]]       w normalised by sum_t    (pinsage_weighted_agg)
-        z   = lrelu([h[f] || agg] W^T + b_W) (pinsage_linear)
-        y   = z / |z|
-
-    and the backward: dW = dz^T [h_self || agg], d[h_self || agg] = dz W,
-    dq = the transposed aggregation (pinsage_segment_wmean over the CSR of the
-    slots by neighbour) times lrelu', dQ = dq^T h[u], dh[u] += dq Q,
-    dh[f] += d h_self -- the GEMMs on pinsage_gemm_ex.  Gathers, the
-    concatenation, the row norm and the scatter of dh into h's rows are torch
-    glue on the device."""
-
-    @staticmethod
-    def forward(ctx, h, nodeset, nb_nodes, nb_weights, Qw, Qb, Ww, Wb):
-        dev = nat.device()
-        hid, d = Qw.shape
-        out = Ww.shape[0]
-        hd = h.detach()
-        if hd.device != dev or hd.dtype != torch.float32 or hd.stride(1) != 1:
-            hd = hd.to(dev, torch.float32).contiguous()
-        ns = torch.as_tensor(nodeset).reshape(-1).to(dev, torch.int64)
-        nb = torch.as_tensor(nb_nodes).to(dev, torch.int64)
-        n, T = nb.shape
-        if ns.shape[0] != n:
-            raise ValueError("nodeset and nb_nodes rows differ")
-        if n and (int(torch.cat([ns, nb.reshape(-1)]).min()) < 0 or
-                  int(torch.cat([ns, nb.reshape(-1)]).max()) >= hd.shape[0]):
-            raise IndexError("node ids out of range of h")
-        w64 = torch.as_tensor(nb_weights).to(dev, torch.float64)
-        wn = (w64 / w64.sum(1, keepdim=True)).to(torch.float32).contiguous()
-        uniq, inv = torch.unique(nb.reshape(-1), return_inverse=True)
-        loc = inv.view(n, T).to(torch.int32).contiguous()
-        u32 = uniq.to(torch.int32).contiguous()
-        U = int(uniq.shape[0])
-        q = torch.empty((U, hid), dtype=torch.float32, device=dev)
-        params = [x.detach().to(dev, torch.float32).contiguous() for x in (Qw, Qb, Ww, Wb)]
-        Qw_, Qb_, Ww_, Wb_ = params
-        L = nat.lib()
-        if U:
-            nat.check(L.pinsage_linear(nat.ptr(hd), hd.stride(0), nat.ptr(u32), U, d, nat.ptr(Qw_),
-                                       nat.ptr(Qb_), hid, 1, nat.ptr(q), hid, nat.stream_ptr()), "linear")
-        agg = torch.empty((n, hid), dtype=torch.float32, device=dev)
-        if n:
-            nat.check(L.pinsage_weighted_agg(nat.ptr(q), hid, nat.ptr(loc), nat.ptr(wn), n, T, nat.ptr(agg),
-                                             nat.stream_ptr()), "weighted_agg")
-        cat = torch.cat([hd[ns, :d], agg], 1).contiguous()
-        z = torch.empty((n, out), dtype=torch.float32, device=dev)
-        if n:
-            nat.check(L.pinsage_linear(nat.ptr(cat), d + hid, None, n, d + hid, nat.ptr(Ww_), nat.ptr(Wb_),
-                                       out, 1, nat.ptr(z), out, nat.stream_ptr()), "linear")
-        nrm = z.norm(dim=1, keepdim=True)
-        y = z / nrm
-        ctx.save_for_backward(hd, ns, uniq, u32, loc, wn, q, cat, z, nrm, y, *params)
-        ctx.h_meta = (h.shape, h.dtype, h.device, d)
-        ctx.param_meta = tuple(x.device for x in (Qw, Qb, Ww, Wb))
-        return y.to(h.device)
-
-    @staticmethod
-    def backward(ctx, dy):
-        hd, ns, uniq, u32, loc, wn, q, cat, z, nrm, y, Qw_, Qb_, Ww_, Wb_ = ctx.saved_tensors
-        h_shape, h_dtype, h_device, d = ctx.h_meta
-        dev = y.device
-        n, T = loc.shape
-        hid = Qw_.shape[0]
-        out = Ww_.shape[0]
-        U = int(uniq.shape[0])
-        dy = dy.to(dev, torch.float32)
-        # through the row norm and LeakyReLU (slope 0.01)
-        dz = (dy - y * (y * dy).sum(1, keepdim=True)) / nrm
-        dpre = (dz * torch.where(z > 0, 1.0, 0.01)).contiguous()
-        gW = torch.empty((out, d + hid), dtype=torch.float32, device=dev)
-        dcat = torch.empty((n, d + hid), dtype=torch.float32, device=dev)
-        dq = torch.zeros((U, hid), dtype=torch.float32, device=dev)
-        gQ = torch.empty((hid, d), dtype=torch.float32, device=dev)
-        dh_nb = torch.empty((U, d), dtype=torch.float32, device=dev)
-        if n:
-            dp4, cat4 = _pad_rows(dpre), _pad_rows(cat)
-            _gemm(out, d + hid, dp4.shape[0], 0, 0, dp4, out, cat4, d + hid, gW, d + hid)
-            _gemm(n, d + hid, out, 1, 0, dpre, out, Ww_, d + hid, dcat, d + hid)
-            # transposed aggregation: slots sorted by neighbour row
-            flat = loc.reshape(-1).to(torch.int64)
-            order = torch.argsort(flat, stable=True)
-            seg = torch.zeros(U + 1, dtype=torch.int64, device=dev)
-            seg[1:] = torch.cumsum(torch.bincount(flat, minlength=U), 0)
-            rows = (order // T).to(torch.int32).contiguous()
-            wT = wn.reshape(-1)[order].contiguous()
-            dagg = dcat[:, d:].contiguous()
-            nat.check(nat.lib().pinsage_segment_wmean(nat.ptr(dagg), hid, n, hid, nat.ptr(seg), nat.ptr(rows),
-                                                      nat.ptr(wT), U, 0, nat.ptr(dq), hid, nat.stream_ptr()),
-                      "segment_wmean")
-            dq.mul_(torch.where(q > 0, 1.0, 0.01))
-            dq4 = _pad_rows(dq)
-            u4 = _pad_rows(u32)
-            _gemm(hid, d, dq4.shape[0], 0, 0, dq4, hid, hd, hd.stride(0), gQ, d, b_idx=u4)
-            _gemm(U, d, hid, 1, 0, dq, hid, Qw_, d, dh_nb, d)
-        else:
-            gW.zero_()
-            gQ.zero_()
-        gWb = dpre.sum(0)
-        gQb = dq.sum(0)
-        dh = None
-        if ctx.needs_input_grad[0]:
-            dh = torch.zeros(h_shape, dtype=torch.float32, device=dev)
-            dh[:, :d].index_add_(0, ns, dcat[:, :d])
-            dh[:, :d].index_add_(0, uniq, dh_nb)
-            dh = dh.to(h_device, h_dtype)
-        pq, pqb, pw, pwb = ctx.param_meta
-        return (dh, None, None, None, gQ.to(pq), gQb.to(pqb), gW.to(pw), gWb.to(pwb))
+        rows on torch.ops.pinsage (pinsage_ops.conv_layer), differentiable in
+        the parameters and in ``h``."""
+        import pinsage_ops
+        return pinsage_ops.conv_layer(h, nodeset, nb_nodes, nb_weights, self.Q.weight, self.Q.bias,
+                                      self.W.weight, self.W.bias)
 
 
 class PinSageModel(nn.Module):

@@ -364,3 +364,20 @@ def test_device_graph_generator_properties():
     assert (pos[:, 0] != pos[:, 1]).all() and pos.max() < n
     cols_of = {v: set(ix[ip[v]:ip[v + 1]].tolist()) for v in np.unique(pos[:200]).tolist()}
     assert all(cols_of[a] & cols_of[b] for a, b in pos[:200].tolist())
+
+
+def test_torch_operator_library_registers_every_op():
+    """libpinsage_torch.so (csrc/torch_ops.cpp) loads and registers the
+    torch.ops.pinsage schemas of SURVEY.md §8(b2), with autograd formulas for
+    the differentiable ones; no compute (there is no CPU implementation)."""
+    import torch
+    import pinsage_ops
+    pinsage_ops.load()
+    for name in ("ppr_topk", "frontier", "linear", "gemm", "weighted_agg", "weighted_agg_backward",
+                 "segment_wmean"):
+        assert hasattr(torch.ops.pinsage, name), name
+    x = torch.zeros(4, 8)
+    W = torch.zeros(4, 8)
+    import pytest
+    with pytest.raises(NotImplementedError, match="CPU"):  # HIP dispatch only: fails loudly
+        torch.ops.pinsage.linear(x, None, W, None, True)
