@@ -29,18 +29,31 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // x = H + M + L with H, M, L bf16: H = RN(x), M = RN(x - H), L = RN(x - H - M);
 // both differences are exact in fp32, so |x - (H + M + L)| <= 2^-9 |x - H - M|
 // <= 2^-26 |x| (the pieces have the exponent range of fp32).
+// Per pair of elements: three v_cvt_pk_bf16_f32, two packed fp32 subtractions
+// (v_pk_add_f32) and four shifts / masks back to fp32 (nine VALU issues for
+// two elements; the scalar form compiled to ~11.7).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x2 bf2_to_f2(unsigned p) {
+  return f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+__device__ __forceinline__ void split_pair(f32x2 x, unsigned& H, unsigned& M, unsigned& L) {
+  H = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+  const f32x2 r = x - bf2_to_f2(H);
+  M = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+  const f32x2 s = r - bf2_to_f2(M);
+  L = __builtin_bit_cast(unsigned, __builtin_convertvector(s, bf16x2));
+}
 __device__ __forceinline__ void split3(const float4& a, const float4& b, bf16x8& H, bf16x8& M, bf16x8& L) {
-  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+  unsigned hh[4], mm[4], ll[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)x[j];
-    const float r = x[j] - (float)h;
-    const __bf16 m = (__bf16)r;
-    const float s = r - (float)m;
-    H[j] = h;
-    M[j] = m;
-    L[j] = (__bf16)s;
-  }
+  for (int j = 0; j < 4; ++j) split_pair(x[j], hh[j], mm[j], ll[j]);
+  const u32x4 h{hh[0], hh[1], hh[2], hh[3]}, m{mm[0], mm[1], mm[2], mm[3]}, l{ll[0], ll[1], ll[2], ll[3]};
+  H = __builtin_bit_cast(bf16x8, h);
+  M = __builtin_bit_cast(bf16x8, m);
+  L = __builtin_bit_cast(bf16x8, l);
 }
 
 constexpr int kLdsBudget = 81920;  // bytes per workgroup: two workgroups per CU
@@ -210,7 +223,7 @@ __device__ __forceinline__ void wait_stage(int younger) {
 template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2,
           bool BF = false>
 __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
-  static_assert(!BF || (AK && BKM && BK % 16 == 0), "split-bf16 products: K-major operands, 16-k steps");
+  static_assert(!BF || BK % 16 == 0, "split-bf16 products: 16-k steps");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
   using OpB = typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type;
@@ -322,7 +335,7 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
       };
       if constexpr (BF) {
         // 16-k steps: lane (row l32, half h) holds k = 16 t + 8 h + j, j = 0..7
-        // (two float4 of the swizzled K-major image), split into hi / mid / lo;
+        // (two float4 fragments of the K-major or M-/N-major image), split into hi / mid / lo;
         // the products whose magnitude is >= 2^-18 of hi*hi, smallest first
 #pragma unroll
         for (int t = 0; t < BK / 16; ++t) {
@@ -683,20 +696,20 @@ int gemm_pick_config(int M, int N, int K, int splits) {
 
 template <bool AK, bool BKM>
 static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
-  if constexpr (AK && BKM) {
-    if (p.prec == 1) {  // split-bf16 products
-      if (cfg == 0)
-        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 2, 2, 16, 4, 2, true>), g, dim3(256), 0, st, p);
-      else if (cfg == 1)
-        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 1, 2, 32, 4, 2, true>), g, dim3(256), 0, st, p);
-      else if (cfg == 2)
-        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 1, 4, 1, 1, 32, 4, 2, true>), g, dim3(256), 0, st, p);
-      else if (cfg == 3)
-        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 1, 2, 16, 4, 3, true>), g, dim3(256), 0, st, p);
-      else
-        hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 1, 2, 16, 3, 4, true>), g, dim3(256), 0, st, p);
-      return;
-    }
+  if (p.prec == 1) {  // split-bf16 products (same tiles, same LDS images)
+    if (cfg == 0)
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true>), g, dim3(256), 0, st, p);
+    else if (cfg == 1)
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 32, 4, 2, true>), g, dim3(256), 0, st, p);
+    else if (cfg == 2)
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32, 4, 2, true>), g, dim3(256), 0, st, p);
+    else if (cfg == 3)
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true>), g, dim3(256), 0, st, p);
+    else if constexpr (AK && BKM)
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 3, 4, true>), g, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true>), g, dim3(256), 0, st, p);
+    return;
   }
   if (cfg == 0)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16>), g, dim3(256), 0, st, p);
@@ -739,7 +752,6 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
              "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
   if (p.prec < 0) p.prec = gemm_default_prec();
-  if (!(p.a_kmajor && p.b_kmajor)) p.prec = 0;
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
   int cfg = p.cfg >= 0 ? p.cfg : gemm_pick_config(Mest, p.N, Kmax, splits);

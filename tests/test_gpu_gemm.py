@@ -160,31 +160,46 @@ def test_weight_gradient_split_k_every_config(cfg, S, shape):
     assert _rel(C.sum(0), r) < REL_TOL, _rel(C.sum(0), r)
 
 
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
-def test_split_bf16_products_are_fp32_accurate(cfg):
-    """The split-bf16 product path (K-major operands: x = hi + mid + lo bf16,
-    six 32x32x16 bf16 MFMAs per 16-k step, fp32 accumulation) against float64,
-    next to the exact-fp32 MFMA path on the same data: its error is the fp32
-    path's order (measured below it), with ragged M / K tails, gathered rows,
-    wide-range magnitudes and both schedules."""
+def test_split_bf16_products_are_fp32_accurate(ak, bk, cfg):
+    """The split-bf16 product path (x = hi + mid + lo bf16, six 32x32x16 bf16
+    MFMAs per 16-k step, fp32 accumulation) against float64, next to the
+    exact-fp32 MFMA path on the same data, for every operand layout (K-major
+    images read as float4 fragments, M-/N-major images as four k-rows): its
+    error is the fp32 path's order (measured below it), with ragged M / K
+    tails, gathered rows / k-rows, wide-range magnitudes and both schedules."""
+    if cfg == 4 and not (ak and bk):
+        pytest.skip("cfg 4 takes K-major operands only")
     import _native as nat
     lib = nat.lib()
-    g = torch.Generator(device="cuda").manual_seed(99 + cfg)
+    g = torch.Generator(device="cuda").manual_seed(99 + cfg + 7 * ak + 13 * bk)
     old = lib.pinsage_gemm_get_prec()
     try:
         for M, N, K in SHAPES:
+            if not ak and M % 4:
+                M += 4 - M % 4
             A = torch.randn((M, K), device="cuda", generator=g)
             A *= torch.exp2(torch.randint(-20, 20, (M, 1), device="cuda", generator=g).float())
-            B = torch.randn((N, K), device="cuda", generator=g)
-            a_idx = torch.randint(0, M, (M,), device="cuda", generator=g, dtype=torch.int32) if M > 1 else None
+            if not ak:
+                A = A.t().contiguous()
+            B = torch.randn((N, K) if bk else (K, N), device="cuda", generator=g)
+            a_idx = torch.randint(0, M, (M,), device="cuda", generator=g, dtype=torch.int32) \
+                if (ak and M > 1) else None
+            b_idx = None
+            if not bk:
+                B = torch.cat([B, torch.randn(K, N, device="cuda", generator=g)])
+                b_idx = torch.randint(0, 2 * K, (K,), device="cuda", generator=g, dtype=torch.int32)
             bias = torch.randn(N, device="cuda", generator=g)
-            r = _ref(M, N, K, 1, 1, A, a_idx, B, bias, 1)
+            Bv = B if b_idx is None else B[b_idx.long()]
+            r = _ref(M, N, K, ak, bk, A, a_idx, Bv, bias, 1)
             errs = {}
             for prec in (0, 1):
                 assert lib.pinsage_gemm_set_prec(prec) == 0
+                # stream-K takes no gathered k-rows (launch_gemm falls back to tiles)
                 for sk in ((0, 1) if cfg else (0,)):
                     C = torch.full((M, N), float("nan"), device="cuda")
-                    _gemm(M, N, K, 1, 1, A, a_idx, B, C, bias=bias, act=1, cfg=cfg, sk=sk)
+                    _gemm(M, N, K, ak, bk, A, a_idx, B, C, bias=bias, act=1, cfg=cfg, sk=sk, b_idx=b_idx)
                     torch.cuda.synchronize()
                     assert torch.isfinite(C).all()
                     errs[(prec, sk)] = _rel(C, r)
@@ -192,3 +207,26 @@ def test_split_bf16_products_are_fp32_accurate(cfg):
             assert max(errs.values()) < 2e-6, errs
     finally:
         lib.pinsage_gemm_set_prec(old)
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+def test_split_k_weight_gradient_both_arithmetics(prec):
+    """The engine's weight-gradient form (M-major A, gathered N-major B, split-K
+    slabs) under both product arithmetics."""
+    import _native as nat
+    lib = nat.lib()
+    old = lib.pinsage_gemm_get_prec()
+    g = torch.Generator(device="cuda").manual_seed(5 + prec)
+    M, N, K, S = 512, 512, 10552, 32
+    A = torch.randn(K, M, device="cuda", generator=g)
+    B = torch.randn(3 * K, N, device="cuda", generator=g)
+    b_idx = torch.randint(0, 3 * K, (K,), device="cuda", generator=g, dtype=torch.int32)
+    try:
+        assert lib.pinsage_gemm_set_prec(prec) == 0
+        C = torch.full((S, M, N), float("nan"), device="cuda")
+        _gemm(M, N, K, 0, 0, A, None, B, C, epi=3, splits=S, cfg=0, b_idx=b_idx)
+        torch.cuda.synchronize()
+    finally:
+        lib.pinsage_gemm_set_prec(old)
+    r = A.double().t() @ B.double()[b_idx.long()]
+    assert _rel(C.sum(0), r) < 1e-6

@@ -86,7 +86,7 @@ def main():
     ap.add_argument("--sets", type=int, default=1, help="row sets cycled over repetitions")
     ap.add_argument("--bias-act", action="store_true", help="bias + LeakyReLU epilogue (the Q projection)")
     ap.add_argument("--sorted", action="store_true", help="gathered rows in ascending order")
-    ap.add_argument("--prec", default="1", help="product arithmetic(s) of K-major GEMMs: 0 fp32 MFMA, 1 split bf16")
+    ap.add_argument("--prec", default="1", help="product arithmetic(s): 0 fp32 MFMA, 1 split bf16")
     a = ap.parse_args()
     lib = nat.lib()
     stream = torch.cuda.current_stream()
