@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -177,6 +178,19 @@ struct Engine {
   hipStream_t side[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> ev;
   int ev_next = 0;
+  // PINSAGE_DEFER_SIDE bit 0: in the backward, a launch forked onto a side
+  // stream is enqueued after the main chain's next launch (same dependences:
+  // its wait binds to an event recorded at the fork point); bit 1: the loss
+  // monitors likewise, after the head backward.  In a captured graph the
+  // chain's child is then created before the side node, which keeps the chain
+  // on one hardware queue instead of hopping at every fork.
+  // Measured at C2 (bench.py, ms per step): 3 (default) 0.445-0.453, 1 0.456-0.461,
+  // 0 (side launches before the chain's next launch) 0.498; the original order
+  // (side launches after the chain's next launch, un-deferred only within the
+  // backward's own code) 0.463.  Forking the monitors behind the head backward
+  // instead of at the loss measured 0.483-0.491.
+  int defer_side = getenv("PINSAGE_DEFER_SIDE") ? atoi(getenv("PINSAGE_DEFER_SIDE")) : 3;
+  std::vector<std::function<int()>> pend;  // deferred side launches, in order
   ~Engine() {
     for (auto& s : side)
       if (s) (void)hipStreamDestroy(s);
@@ -201,6 +215,30 @@ static int dep(Engine& E, hipStream_t from, hipStream_t to) {
   hipEvent_t e = E.ev[(size_t)(E.ev_next++ % kEvents)];
   PS_CHECK_HIP(hipEventRecord(e, from));
   PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+  return kOk;
+}
+
+// Fork `fn` (launches on `to`) off `from` at this point: the wait on `to`
+// binds to an event recorded on `from` now; with `defer` the launch itself
+// waits in E.pend until run_pend (after the main chain's next launch).
+static int fork_side(Engine& E, hipStream_t from, hipStream_t to, bool defer, std::function<int()> fn) {
+  if (from == to) return fn();
+  hipEvent_t e = E.ev[(size_t)(E.ev_next++ % kEvents)];
+  PS_CHECK_HIP(hipEventRecord(e, from));
+  if (!defer) {
+    PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+    return fn();
+  }
+  E.pend.push_back([to, e, fn]() -> int {
+    PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+    return fn();
+  });
+  return kOk;
+}
+static int run_pend(Engine& E) {
+  std::vector<std::function<int()>> v;
+  v.swap(E.pend);
+  for (auto& f : v) PS_TRY(f());
   return kOk;
 }
 
@@ -730,6 +768,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   // normalisation backward (dp_top) in one kernel, which also zeroes the
   // loss's multiplicity counters (the dY scatter-add targets of the layers
   // below were zeroed by the forward's layer_prep)
+  const bool dfr = (E.defer_side & 1) != 0;
   if (E.fused_head) {
     // the head backward forms dZ = sum_c K[c] G[c] from the loss's
     // accumulators as it loads its rows (and zeroes them), writing dZ for dG2
@@ -737,8 +776,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
                            cnt(top.S), top.S.cap, at<float>(ws, E.H1), E.params + E.pG1w,
                            E.params + E.pG2w, at<float>(ws, top.y), at<float>(ws, top.nrm),
                            at<float>(ws, E.dP1), at<float>(ws, top.dp), st));
-    PS_TRY(dep(E, st, s_wg));
-    PS_TRY(wgrad_g2());
+    PS_TRY(run_pend(E));  // the loss monitors (PINSAGE_DEFER_SIDE bit 1)
+    PS_TRY(fork_side(E, st, s_wg, dfr, wgrad_g2));
   } else {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
@@ -756,6 +795,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     p.mask = at<float>(ws, E.H1);
     p.ldm = o;
     PS_TRY(launch_gemm(p, st));
+    PS_TRY(run_pend(E));
     GemmParams q = p;  // dY_top = dP1 G1
     q.a = at<float>(ws, E.dP1);
     q.b = E.params + E.pG1w;
@@ -767,7 +807,6 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
                                  at<float>(ws, top.dp), nullptr, o, nullptr, at<int>(ws, E.Kc),
                                  3 * top.S.cap, st));
   }
-  PS_TRY(dep(E, st, s_wg));
   {
     WGrad w;  // dG1 and db1
     w.A = at<float>(ws, E.dP1);
@@ -782,8 +821,10 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     w.dst = gr + E.pG1w;
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
-    Timed tw(E, "bwd.wgrad.g1", s_wg);
-    PS_TRY(weight_grad(E, ws, w, s_wg, "bwd.wgrad.g1", nullptr, nullptr, false, s_wg != st));
+    PS_TRY(fork_side(E, st, s_wg, dfr, [&E, ws, w, s_wg, st]() -> int {
+      Timed tw(E, "bwd.wgrad.g1", s_wg);
+      return weight_grad(E, ws, w, s_wg, "bwd.wgrad.g1", nullptr, nullptr, false, s_wg != st);
+    }));
   }
   t_hb.stop();
   for (int l = Lc - 1; l >= 0; --l) {
@@ -799,7 +840,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       PS_TRY(launch_norm_lrelu_bwd(at<float>(ws, lb.y), at<float>(ws, lb.nrm), at<float>(ws, lb.dY),
                                    o, cnt(lb.S), lb.S.cap, dp, nullptr, o, nullptr, nullptr, 0, st));
     hipStream_t s_w = l == 0 ? s_wg0 : s_wg;
-    PS_TRY(dep(E, st, s_w));
+    if (l < Lc - 1) PS_TRY(run_pend(E));  // behind the normalisation backward
     WGrad w_wgrad;
     {
       WGrad w;  // dW = dp^T [h_self || agg], dWb = colsum(dp)
@@ -851,27 +892,30 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       }
       with_sk(E, ws, p);
       apply_choice(E, lname("bwd.dcat", l), p);
+      // the W gradient forks before this launch (it reads dp), enqueued after it
+      PS_TRY(fork_side(E, st, s_w, dfr, [&E, ws, w_wgrad, s_w, st, l]() -> int {
+        Timed tw(E, lname("bwd.w_wgrad", l), s_w);
+        return weight_grad(E, ws, w_wgrad, s_w, lname("bwd.w_wgrad", l), nullptr, nullptr, false, s_w != st);
+      }));
       Timed td(E, lname("bwd.dcat", l), st);
       PS_TRY(launch_gemm(p, st));
     }
-    {
-      Timed tw(E, lname("bwd.w_wgrad", l), s_w);
-      PS_TRY(weight_grad(E, ws, w_wgrad, s_w, lname("bwd.w_wgrad", l), nullptr, nullptr, false,
-                         s_w != st));
-    }
+    PS_TRY(run_pend(E));
     if (adam && l == 0) {  // every gradient but Q0's exists on s_w; W0 was read last
-      PS_TRY(dep(E, st, s_w));
-      Timed ta(E, "adam", s_w);
-      PS_TRY(launch_adam(E.params + l0.pWw, E.grads + l0.pWw, E.adam_m + l0.pWw, E.adam_v + l0.pWw,
-                         E.n_params - l0.pWw, adam->coef, adam->beta1, adam->beta2, adam->eps,
-                         s_w));
+      const int64_t off = l0.pWw, n = E.n_params - l0.pWw;
+      const AdamStep a = *adam;
+      PS_TRY(fork_side(E, st, s_w, dfr, [&E, s_w, off, n, a]() -> int {
+        Timed ta(E, "adam", s_w);
+        return launch_adam(E.params + off, E.grads + off, E.adam_m + off, E.adam_v + off, n, a.coef,
+                           a.beta1, a.beta2, a.eps, s_w);
+      }));
     }
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
                             at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
                             at<int>(ws, lb.off), at<int32_t>(ws, lb.occ), at<float>(ws, lb.wloc), T,
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
                             at<float>(ws, lb.dqpart), st));
-    if (l > 0) PS_TRY(dep(E, st, s_wg));
+    PS_TRY(run_pend(E));
     WGrad q_wgrad;
     {
       // dQ = dpq^T h[q_src], dQb = colsum(dpq)
@@ -892,6 +936,13 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       q_wgrad = w;
     }
     if (l > 0) {
+      // dQ of this layer beside the chain, forked here (dpq complete), enqueued
+      // after the dh launch
+      PS_TRY(fork_side(E, st, s_wg, dfr, [&E, ws, q_wgrad, s_wg, st, l]() -> int {
+        Timed tq(E, lname("bwd.q_wgrad", l), s_wg);
+        return weight_grad(E, ws, q_wgrad, s_wg, lname("bwd.q_wgrad", l), nullptr, nullptr, false,
+                           s_wg != st);
+      }));
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
       p.M_dev = cnt(lb.N);
       p.M_hint = (int)lb.N.hint;
@@ -912,16 +963,16 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
       Timed tdh(E, lname("bwd.dh", l), st);
       PS_TRY(launch_gemm(p, st));
     }
-    {
+    PS_TRY(run_pend(E));
+    if (l == 0) {  // dQ0 ends the chain, on the main stream
       AdamSlice q0;
-      if (adam && l == 0) q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
-      hipStream_t qs = l == 0 ? st : s_wg;
-      Timed tq(E, lname("bwd.q_wgrad", l), qs);
-      PS_TRY(weight_grad(E, ws, q_wgrad, qs, lname("bwd.q_wgrad", l), adam && l == 0 ? &q0 : nullptr,
-                         nullptr, l == 0,
-                         qs != st));
+      if (adam) q0 = adam_slice(E, *adam, lb.pQw, lb.pQb);
+      Timed tq(E, lname("bwd.q_wgrad", l), st);
+      PS_TRY(weight_grad(E, ws, q_wgrad, st, lname("bwd.q_wgrad", l), adam ? &q0 : nullptr, nullptr, true,
+                         false));
     }
   }
+  PS_TRY(run_pend(E));
   // every gradient is written once the side streams drain into st (side[0]
   // also carries the loss monitors, pinsage_engine_loss)
   PS_TRY(dep(E, E.side[0], st));
@@ -1142,20 +1193,24 @@ int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream) {
 
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                            void* stream) {
+  PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
 }
 
 int pinsage_engine_forward_inference(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                                      void* stream) {
+  PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream, false);
 }
 
 int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                             void* stream) {
+  PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_frontier(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
 }
 
 int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream) {
+  PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_layers(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
 }
 
@@ -1173,6 +1228,7 @@ int pinsage_engine_set_fork(pinsage_engine* e, void* ws_next, const int64_t* ids
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
                                  void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(run_pend(*E));
   return launch_gather_out(at<float>(ws, E->Z), (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
                            out, (hipStream_t)stream);
 }
@@ -1197,17 +1253,27 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
                        !E->fused_head, st));
   }
   // the monitors (loss, node-feature loss, variance scalars) beside the
-  // backward, on side stream 0, joined at the backward's end
+  // backward, on side stream 0, joined at the backward's end (with
+  // PINSAGE_DEFER_SIDE bit 1 enqueued behind the head backward's launch, or
+  // by the next engine call that enqueues work)
   PS_TRY(ensure_streams(*E));
-  PS_TRY(dep(*E, st, E->side[0]));
-  Timed tm(*E, "loss.monitor", E->side[0]);
-  return launch_loss_monitor(at<float>(ws, E->part), (int)ceil_div(batch_size, 4), at<float>(ws, E->varpart),
-                             (int)c.out, (int)batch_size, at<float>(ws, E->scal), E->side[0]);
+  PS_TRY(run_pend(*E));
+  float* part = at<float>(ws, E->part);
+  float* varpart = at<float>(ws, E->varpart);
+  float* scal = at<float>(ws, E->scal);
+  const int nb4 = (int)ceil_div(batch_size, 4), out = (int)c.out, B = (int)batch_size;
+  hipStream_t s0 = E->side[0];
+  auto mon = [E, part, varpart, scal, nb4, out, B, s0]() -> int {
+    Timed tm(*E, "loss.monitor", s0);
+    return launch_loss_monitor(part, nb4, varpart, out, B, scal, s0);
+  };
+  return fork_side(*E, st, s0, (E->defer_side & 2) != 0, mon);
 }
 
 int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,
                                    void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(run_pend(*E));
   LayerBuf& top = E->L.back();
   return launch_dz_from_dout(dout, (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
                              at<int>(ws, top.S.count), top.S.cap, at<float>(ws, E->G),
@@ -1232,6 +1298,7 @@ int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef,
 int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,
                         void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(run_pend(*E));
   Timed t(*E, "adam", (hipStream_t)stream);
   if (!E->adam_m || !E->adam_v) {
     set_error("engine_adam: optimizer state not set");
