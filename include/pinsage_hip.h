@@ -300,7 +300,11 @@ int pinsage_engine_set_fork(pinsage_engine* e, void* ws_next, const int64_t* ids
                             int64_t n_ids, void* side_stream);
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
                                  void* stream);
-/* max_margin_loss + monitors on the last forward of a [B][3] batch; writes dZ */
+/* max_margin_loss + monitors on the last forward of a [B][3] batch; writes dZ.
+ * The monitor kernel (loss / node-feature loss / variance scalars, on an engine
+ * side stream, dependent on this loss) is enqueued by the next engine call
+ * that enqueues work (normally the backward, right behind its first kernel;
+ * PINSAGE_DEFER_SIDE=0/1 enqueues it here) and joined at the backward's end. */
 int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float margin,
                         int with_monitors, void* stream);
 /* dZ from an upstream gradient of gather_output (single call, autograd path) */
