@@ -387,6 +387,55 @@ def test_frontier_ahead_matches_serial_step():
             os.chdir(cwd)
 
 
+def test_deferred_side_launches_match_immediate():
+    """PINSAGE_DEFER_SIDE (engine.hip fork_side / run_pend) only changes when the
+    backward's side launches and the loss monitors are enqueued, not what they
+    wait for: the graph-replayed step with them deferred (default) trains like
+    the one enqueuing them at their fork points -- same published losses (the
+    monitors' output) and parameters within rounding (CSR fill order, tuner)."""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(6000, 1500, 40000, seed=41)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(6000, 128, seed=42))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 30000, seed=43))
+    old = os.environ.get("PINSAGE_DEFER_SIDE")
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp,
+                                        nbhds_path=os.path.join(tmp, "nb.pt"))
+            pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
+
+            def run(mode):
+                os.environ["PINSAGE_DEFER_SIDE"] = mode  # read when the engine is built
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
+                tr.batch_size = 256
+                torch.manual_seed(6)
+                losses = []
+                for _ in range(5):
+                    batch, _ = tr.next_batch()
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                return losses, tr._fused.runner.flat.detach().clone()
+
+            l0, p0 = run("0")
+            l3, p3 = run("3")
+            assert all(v > 0 for v in l0)
+            for a, b in zip(l0, l3):
+                assert abs(a - b) <= 1e-4 * abs(a) + 1e-7
+            assert ((p0 - p3).norm() / p0.norm()).item() < 1e-4
+        finally:
+            os.chdir(cwd)
+            if old is None:
+                os.environ.pop("PINSAGE_DEFER_SIDE", None)
+            else:
+                os.environ["PINSAGE_DEFER_SIDE"] = old
+
+
 def test_train_step_three_layers_fanout_50_vs_oracle():
     """The C5 shape (BASELINE.json configs[4]: 3 layers, fanout 50) at a size the
     CPU oracle finishes in seconds: 3000 tracks, d_in 128 (>= out, as put_embeddings needs), batch 32, so the bottom
