@@ -26,14 +26,15 @@ namespace ps {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// x = H + M + L exactly, H, M, L bf16: H = RN(x), r = x - H (exact in fp32,
-// |r| <= 2^-9 |x|, at most 16 significant bits), M = r truncated to bf16 (its
-// upper half), L = r - M (exact, the remaining <= 8 bits).  |M| <= 2^-9 |x| and
-// |L| < 2^-16 |x|; M's sign is random relative to x (RN residual), so the
-// dropped products (aM bL, aL bM, aL bL) carry no bias.  Per pair of elements:
-// one v_cvt_pk_bf16_f32, two v_perm_b32, two packed fp32 subtractions
-// (v_pk_add_f32) and four shifts / masks back to fp32 (the all-RN form with
-// three conversions measured the same to 3 % slower).
+// x = H + M + L with H, M, L bf16: H = RN(x), M = RN(x - H), L = RN(x - H - M);
+// both differences are exact in fp32, so |x - (H + M + L)| <= 2^-9 |x - H - M|
+// <= 2^-26 |x| (the pieces have the exponent range of fp32).  Per pair of
+// elements: three v_cvt_pk_bf16_f32, two packed fp32 subtractions
+// (v_pk_add_f32) and four shifts / masks back to fp32.  (M and L by truncation,
+// one conversion per pair, measured 0-3 % faster but doubles the dropped
+// products' bound to 2^-25; the reference-init gradient check of
+// test_gpu_fly.py, whose head-bias gradient cancels to ~1e-4, then exceeded
+// its 2e-4 bound.)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -43,11 +44,9 @@ __device__ __forceinline__ f32x2 bf2_to_f2(unsigned p) {
 __device__ __forceinline__ void split_pair(f32x2 x, unsigned& H, unsigned& M, unsigned& L) {
   H = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
   const f32x2 r = x - bf2_to_f2(H);
-  // M = r truncated to bf16 (upper halves), L = r - M exactly (r has <= 16
-  // significant bits, M takes 8, the other 8 fit a bf16)
-  M = __builtin_amdgcn_perm(__float_as_uint(r.y), __float_as_uint(r.x), 0x07060302u);
+  M = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
   const f32x2 s = r - bf2_to_f2(M);
-  L = __builtin_amdgcn_perm(__float_as_uint(s.y), __float_as_uint(s.x), 0x07060302u);
+  L = __builtin_bit_cast(unsigned, __builtin_convertvector(s, bf16x2));
 }
 __device__ __forceinline__ void split3(const float4& a, const float4& b, bf16x8& H, bf16x8& M, bf16x8& L) {
   const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
@@ -356,17 +355,18 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
             split3(OpB::frag(Bs, c, 16 * t + 8 * h), OpB::frag(Bs, c, 16 * t + 8 * h + 4), bH[j], bM[j],
                    bL[j]);
           }
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[i], bH[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[i], bL[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM[i], bM[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM[i], bH[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[i], bM[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[i], bH[j], acc[i][j], 0, 0, 0);
-            }
+          // product by product over the blocks: consecutive MFMAs write
+          // different accumulators (1-3 % over block by block)
+#define PS_BF_ALL(X, Y)                                                                       \
+  _Pragma("unroll") for (int i = 0; i < TM; ++i) _Pragma("unroll") for (int j = 0; j < TN; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
+          PS_BF_ALL(aL, bH)
+          PS_BF_ALL(aH, bL)
+          PS_BF_ALL(aM, bM)
+          PS_BF_ALL(aM, bH)
+          PS_BF_ALL(aH, bM)
+          PS_BF_ALL(aH, bH)
+#undef PS_BF_ALL
         }
         return;
       }
