@@ -188,7 +188,9 @@ struct Engine {
   // 0 (side launches before the chain's next launch) 0.498; the original order
   // (side launches after the chain's next launch, un-deferred only within the
   // backward's own code) 0.463.  Forking the monitors behind the head backward
-  // instead of at the loss measured 0.483-0.491.
+  // instead of at the loss measured 0.483-0.491; fewer fork points (the head's
+  // and each layer's W gradients forked together with the layer's Q gradient /
+  // the optimizer pass) 0.454-0.467.
   int defer_side = getenv("PINSAGE_DEFER_SIDE") ? atoi(getenv("PINSAGE_DEFER_SIDE")) : 3;
   std::vector<std::function<int()>> pend;  // deferred side launches, in order
   ~Engine() {
