@@ -153,15 +153,22 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
 // Popular tracks sit in thousands of neighbour lists, so global per-row
 // counters are hot.  When the distinct-neighbour count fits (<= kLdsRows), each
 // block counts its contiguous slice of occurrences in an LDS histogram and
-// flushes one global atomic per row it touched; otherwise lanes of a wave with
-// the same row combine into one global atomic.
+// flushes one global atomic per row it touched.  Up to kMaxRanges x kLdsRows
+// rows, the rows are cut into ranges of kLdsRows and the work into (range,
+// slice of kSlice occurrences) items: a block reads the slice and histograms
+// the occurrences that fall in its range (the slice is read once per range,
+// from L2 after the first).  Beyond that, lanes of a wave with the same row
+// combine into one global atomic.
 constexpr int kLdsRows = 40960;  // 160 KiB: a workgroup may take all of a CU's LDS
+constexpr int kMaxRanges = 64;
+constexpr int kSlice = 65536;
+constexpr int kCsrRangeGrid = 256;  // one 160-KiB workgroup per CU
 __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restrict__ loc,
                                                          const int* __restrict__ nS, int T,
                                                          const int* __restrict__ nN,
                                                          int* __restrict__ cnt,
                                                          float* __restrict__ zero_rows, int zero_n,
-                                                         int* __restrict__ nsplit) {
+                                                         int* __restrict__ nsplit, int max_ranges) {
   extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
   const int U = *nN;
@@ -182,6 +189,26 @@ __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restri
     __syncthreads();
     for (int u = threadIdx.x; u < U; u += blockDim.x)
       if (hist[u]) atomicAdd(cnt + u, hist[u]);
+    return;
+  }
+  const int R = (U + kLdsRows - 1) / kLdsRows;
+  if (R <= max_ranges) {
+    const int64_t items = (int64_t)R * ((n + kSlice - 1) / kSlice);
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+      const int r = (int)(it % R);
+      const int u0 = r * kLdsRows, nu = min(kLdsRows, U - u0);
+      const int64_t e0 = (it / R) * kSlice, e1 = min(n, e0 + kSlice);
+      for (int u = threadIdx.x; u < nu; u += blockDim.x) hist[u] = 0;
+      __syncthreads();
+      for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const int u = loc[e] - u0;
+        if ((unsigned)u < (unsigned)nu) atomicAdd(hist + u, 1);
+      }
+      __syncthreads();
+      for (int u = threadIdx.x; u < nu; u += blockDim.x)
+        if (hist[u]) atomicAdd(cnt + u0 + u, hist[u]);
+      __syncthreads();  // the next item zeroes hist
+    }
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -365,7 +392,7 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
                                                         const int* __restrict__ nN,
                                                         int* __restrict__ cursor,
                                                         int32_t* __restrict__ occ,
-                                                        int32_t* __restrict__ occ_u) {
+                                                        int32_t* __restrict__ occ_u, int max_ranges) {
   extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
   const int U = *nN;
@@ -385,6 +412,35 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
       const int pos = atomicAdd(hist + u, 1);
       occ[pos] = (int32_t)e;
       occ_u[pos] = u;
+    }
+    return;
+  }
+  const int R = (U + kLdsRows - 1) / kLdsRows;
+  if (R <= max_ranges) {  // (range, slice) items as csr_count_kernel's
+    const int64_t items = (int64_t)R * ((n + kSlice - 1) / kSlice);
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+      const int r = (int)(it % R);
+      const int u0 = r * kLdsRows, nu = min(kLdsRows, U - u0);
+      const int64_t e0 = (it / R) * kSlice, e1 = min(n, e0 + kSlice);
+      for (int u = threadIdx.x; u < nu; u += blockDim.x) hist[u] = 0;
+      __syncthreads();
+      for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const int u = loc[e] - u0;
+        if ((unsigned)u < (unsigned)nu) atomicAdd(hist + u, 1);
+      }
+      __syncthreads();
+      for (int u = threadIdx.x; u < nu; u += blockDim.x)
+        if (hist[u]) hist[u] = atomicAdd(cursor + u0 + u, hist[u]);
+      __syncthreads();
+      for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const int u = loc[e] - u0;
+        if ((unsigned)u < (unsigned)nu) {
+          const int pos = atomicAdd(hist + u, 1);
+          occ[pos] = (int32_t)e;
+          occ_u[pos] = u0 + u;
+        }
+      }
+      __syncthreads();  // the next item zeroes hist
     }
     return;
   }
@@ -1141,11 +1197,15 @@ int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, co
                      int32_t* occ_u, int2* chunks, int* nchunks, int2* split, int* nsplit,
                      float* dpq, int hid, hipStream_t st) {
   const int lds = (int)std::min<int64_t>(N_max, kLdsRows) * 4;
-  const int gb = std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
+  // more rows than one histogram: (range, slice) items over a CU-wide grid
+  const int gb = N_max > kLdsRows ? kCsrRangeGrid : std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
   // dq writes every row it owns (no atomics), so dpq needs no zeroing
   (void)dpq;
+  // PINSAGE_CSR_RANGES: the range cap (0: the per-wave global-atomic path
+  // beyond one histogram; A/B and tests)
+  const int max_ranges = getenv("PINSAGE_CSR_RANGES") ? atoi(getenv("PINSAGE_CSR_RANGES")) : kMaxRanges;
   hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt,
-                     (float*)nullptr, hid, nsplit);
+                     (float*)nullptr, hid, nsplit, max_ranges);
   PS_CHECK_LAUNCH();
   if (N_max <= 1024 * 64) {
     hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor, chunks,
@@ -1161,7 +1221,7 @@ int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, co
     PS_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cursor, occ,
-                     occ_u);
+                     occ_u, max_ranges);
   PS_CHECK_LAUNCH();
   return kOk;
 }

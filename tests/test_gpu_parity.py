@@ -562,3 +562,68 @@ def test_conv_layer_autograd_vs_oracle(dims, T, n):
         assert _rel(prm.grad.cpu().numpy(), p[f"conv_layers.0.{k}"].grad.numpy()) < REL_TOL, k
     assert _rel(hg.grad.cpu().numpy(), hr.grad.numpy()) < REL_TOL
     assert float(hg.grad[:, d_in:].abs().max()) == 0.0
+
+
+def test_csr_transpose_ranges_match_atomic_path():
+    """The backward's CSR transpose of the neighbour slots (conv.hip
+    csr_count_kernel / csr_fill_kernel) beyond one LDS histogram (> 40960
+    distinct layer-0 neighbours): the (range, slice) histogram path trains like
+    the per-wave global-atomic path (PINSAGE_CSR_RANGES=0) -- same published
+    losses and parameters within rounding (both fill rows in atomic order)."""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    n = 100000
+    pg = synthetic.make_playlist_graph(n, 25000, 1000000, seed=51)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(n, 128, seed=52))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 400000, seed=53, csr=(indptr, indices)))
+    old = os.environ.get("PINSAGE_CSR_RANGES")
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp,
+                                        nbhds_path=os.path.join(tmp, "nb.pt"))
+            import pinsage_model as pm
+            pm.set_rng_mode("philox")
+            try:
+                pt.PinSage(g, n, feats, pos, log=False, load_save=False)
+            finally:
+                pm.set_rng_mode("mt19937")
+
+            def run(mode):
+                if mode is None:
+                    os.environ.pop("PINSAGE_CSR_RANGES", None)
+                else:
+                    os.environ["PINSAGE_CSR_RANGES"] = mode
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, n, feats, pos, log=False, load_save=False)
+                # fanout 50 (C5's): top-T PPR neighbours concentrate on popular
+                # tracks, so a wide T is what makes the layer-0 set this large
+                tr.model = pm.PinSageModel(g, n, 2, tr.dimensions, tr.n_hops, tr.alpha, 50, tr.nbhds)
+                tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+                tr.batch_size = 4096
+                torch.manual_seed(6)
+                losses = []
+                for _ in range(3):
+                    batch, _ = tr.next_batch()
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                f = tr._fused
+                eng = f.runner.engine
+                u0 = max(int(eng.view(ws, int(eng.off.count_N[0]), torch.int32, 1).item()) for ws in f.wss)
+                return losses, f.runner.flat.detach().clone(), u0
+
+            l0, p0, u0 = run("0")
+            l1, p1, u1 = run(None)
+            assert u0 > 40960 and u1 > 40960, (u0, u1)
+            for a, b in zip(l0, l1):
+                assert abs(a - b) <= 1e-4 * abs(a) + 1e-7
+            assert ((p0 - p1).norm() / p0.norm()).item() < 1e-4
+        finally:
+            os.chdir(cwd)
+            if old is None:
+                os.environ.pop("PINSAGE_CSR_RANGES", None)
+            else:
+                os.environ["PINSAGE_CSR_RANGES"] = old
