@@ -155,13 +155,12 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
 // block counts its contiguous slice of occurrences in an LDS histogram and
 // flushes one global atomic per row it touched.  Up to kMaxRanges x kLdsRows
 // rows, the rows are cut into ranges of kLdsRows and the work into (range,
-// slice of kSlice occurrences) items: a block reads the slice and histograms
+// slice of occurrences) items, about two per workgroup: a block reads the slice and histograms
 // the occurrences that fall in its range (the slice is read once per range,
 // from L2 after the first).  Beyond that, lanes of a wave with the same row
 // combine into one global atomic.
 constexpr int kLdsRows = 40960;  // 160 KiB: a workgroup may take all of a CU's LDS
 constexpr int kMaxRanges = 64;
-constexpr int kSlice = 65536;
 constexpr int kCsrRangeGrid = 256;  // one 160-KiB workgroup per CU
 __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restrict__ loc,
                                                          const int* __restrict__ nS, int T,
@@ -193,11 +192,14 @@ __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restri
   }
   const int R = (U + kLdsRows - 1) / kLdsRows;
   if (R <= max_ranges) {
-    const int64_t items = (int64_t)R * ((n + kSlice - 1) / kSlice);
+    // about two items per workgroup: slices of n / ceil(2 grid / R)
+    const int64_t S = max((int64_t)1, (int64_t)(2 * gridDim.x + R - 1) / R);
+    const int64_t slice = (n + S - 1) / S;
+    const int64_t items = (int64_t)R * S;
     for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
       const int r = (int)(it % R);
       const int u0 = r * kLdsRows, nu = min(kLdsRows, U - u0);
-      const int64_t e0 = (it / R) * kSlice, e1 = min(n, e0 + kSlice);
+      const int64_t e0 = (it / R) * slice, e1 = min(n, e0 + slice);
       for (int u = threadIdx.x; u < nu; u += blockDim.x) hist[u] = 0;
       __syncthreads();
       for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
@@ -417,11 +419,14 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
   }
   const int R = (U + kLdsRows - 1) / kLdsRows;
   if (R <= max_ranges) {  // (range, slice) items as csr_count_kernel's
-    const int64_t items = (int64_t)R * ((n + kSlice - 1) / kSlice);
+    // about two items per workgroup: slices of n / ceil(2 grid / R)
+    const int64_t S = max((int64_t)1, (int64_t)(2 * gridDim.x + R - 1) / R);
+    const int64_t slice = (n + S - 1) / S;
+    const int64_t items = (int64_t)R * S;
     for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
       const int r = (int)(it % R);
       const int u0 = r * kLdsRows, nu = min(kLdsRows, U - u0);
-      const int64_t e0 = (it / R) * kSlice, e1 = min(n, e0 + kSlice);
+      const int64_t e0 = (it / R) * slice, e1 = min(n, e0 + slice);
       for (int u = threadIdx.x; u < nu; u += blockDim.x) hist[u] = 0;
       __syncthreads();
       for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {

@@ -48,14 +48,42 @@ __global__ void bits_mark_i64_kernel(unsigned long long* __restrict__ bits,
 // mark nb_table[members[f]][t] for f < *count, t < T (table row stride ld).
 // lds_words > 0: each block marks its contiguous slice into an LDS copy of the
 // bitmap and ORs the touched words into HBM once (popular ids repeat thousands
-// of times; global atomics on their words would serialise).
+// of times; global atomics on their words would serialise).  range_words > 0
+// (bitmaps larger than LDS): the bitmap is cut into windows of range_words and
+// the work into (window, slice) items, about two per workgroup; a block marks
+// the ids of its slice that fall in its window into LDS (the slice's table rows
+// are re-read once per window, from L2 / the Infinity Cache after the first).
 __global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long long* __restrict__ bits,
                                                                const int32_t* __restrict__ members,
                                                                const int* __restrict__ count,
                                                                const int32_t* __restrict__ nb,
-                                                               int64_t ld, int T, int lds_words) {
+                                                               int64_t ld, int T, int lds_words,
+                                                               int64_t nwords, int range_words) {
   extern __shared__ unsigned long long lbits[];
   const int64_t n = (int64_t)(*count) * T;
+  if (range_words > 0) {
+    const int64_t R = (nwords + range_words - 1) / range_words;
+    const int64_t S = max((int64_t)1, (int64_t)(2 * gridDim.x + R - 1) / R);
+    const int64_t slice = (n + S - 1) / S;
+    for (int64_t it = blockIdx.x; it < R * S; it += gridDim.x) {
+      const int64_t r = it % R, w0 = r * range_words;
+      const int nwr = (int)min((int64_t)range_words, nwords - w0);
+      const int64_t v0 = w0 * 64, vn = (int64_t)nwr * 64;
+      const int64_t e0 = (it / R) * slice, e1 = min(n, e0 + slice);
+      for (int w = threadIdx.x; w < nwr; w += blockDim.x) lbits[w] = 0ull;
+      __syncthreads();
+      for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+        const int64_t f = e / T, t = e - f * T;
+        const int64_t v = (int64_t)nb[(int64_t)members[f] * ld + t] - v0;
+        if (v >= 0 && v < vn) atomicOr(lbits + (v >> 6), 1ull << (v & 63));
+      }
+      __syncthreads();
+      for (int w = threadIdx.x; w < nwr; w += blockDim.x)
+        if (lbits[w]) atomicOr(bits + w0 + w, lbits[w]);
+      __syncthreads();  // the next item zeroes lbits
+    }
+    return;
+  }
   if (lds_words > 0) {
     for (int w = threadIdx.x; w < lds_words; w += blockDim.x) lbits[w] = 0ull;
     __syncthreads();
@@ -294,13 +322,24 @@ int launch_mark_table(unsigned long long* bits, const int32_t* members, const in
                       hipStream_t st) {
   if (max_count <= 0) return kOk;
   const int64_t nw = bitset_words(universe);
+  // windows of a full CU's LDS (the limit is raised once, on the first call,
+  // before any graph capture); PINSAGE_MARK_RANGES caps the window count (0:
+  // global atomics beyond 64 KiB, A/B)
+  constexpr int kWinWords = 20480;  // 160 KiB
+  static const int win_ok = hipFuncSetAttribute((const void*)bits_mark_table_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                kWinWords * 8) == hipSuccess;
+  const int max_win = getenv("PINSAGE_MARK_RANGES") ? atoi(getenv("PINSAGE_MARK_RANGES")) : 64;
   if (nw * 8 <= 64 * 1024) {
     const int gb = std::max(1, std::min(64, ceil_div(max_count * T, 4096)));
     hipLaunchKernelGGL(bits_mark_table_kernel, dim3(gb), dim3(1024), (size_t)nw * 8, st, bits,
-                       members, count, nb, ld, T, (int)nw);
+                       members, count, nb, ld, T, (int)nw, nw, 0);
+  } else if (win_ok && ceil_div(nw, kWinWords) <= max_win) {
+    hipLaunchKernelGGL(bits_mark_table_kernel, dim3(256), dim3(1024), (size_t)kWinWords * 8, st,
+                       bits, members, count, nb, ld, T, 0, nw, kWinWords);
   } else {
     hipLaunchKernelGGL(bits_mark_table_kernel, dim3(grid_for(max_count * T, 1024)), dim3(1024), 0,
-                       st, bits, members, count, nb, ld, T, 0);
+                       st, bits, members, count, nb, ld, T, 0, nw, 0);
   }
   PS_CHECK_LAUNCH();
   return kOk;
