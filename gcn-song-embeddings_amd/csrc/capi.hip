@@ -488,6 +488,41 @@ int pinsage_gemm_set_prec(int prec) {
 
 int pinsage_gemm_get_prec(void) { return gemm_default_prec(); }
 
+int pinsage_split_planes(const float* W, int64_t rows, int64_t cols, int64_t ldw, uint16_t* out,
+                         void* stream) {
+  return launch_split_planes(W, rows, cols, ldw, out, (hipStream_t)stream);
+}
+
+int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
+                           const float* W, const uint16_t* W_planes, int64_t ldws,
+                           const float* bias, int64_t N, int act, float* C, int64_t ldc, int cfg,
+                           void* stream) {
+  if (M < 0 || N <= 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX || cfg < -1 ||
+      cfg > 4) {
+    set_error("linear_split_b: bad argument");
+    return kErrArg;
+  }
+  GemmParams p;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.a = A;
+  p.lda = lda;
+  p.a_idx = a_idx;
+  p.b = W;
+  p.ldb = K;
+  p.b_split = W_planes;
+  p.ldb_split = ldws;
+  p.c = C;
+  p.ldc = ldc;
+  p.bias = bias;
+  p.act = act != 0;
+  p.cfg = cfg;
+  p.stream_k = 0;
+  p.prec = 1;
+  return launch_gemm(p, (hipStream_t)stream);
+}
+
 int64_t pinsage_knn_scratch_bytes(int64_t n, int64_t batch_rows) {
   return knn_scratch_bytes(n, batch_rows < 1 ? 1 : batch_rows);
 }

@@ -96,6 +96,7 @@ struct LayerBuf {
   int64_t d = 0;    // input dim of the layer
   size_t self_src = 0, q_src = 0, loc = 0, wloc = 0;
   size_t q = 0, agg = 0, y = 0, nrm = 0;
+  size_t qsplit = 0;  // the Q weight's hi / mid / lo bf16 planes (split-bf16 Q projection)
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, occ = 0,
          occ_u = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
@@ -133,6 +134,9 @@ struct Engine {
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B)
   bool fused_aggw = !getenv("PINSAGE_FUSED_AGGW") || atoi(getenv("PINSAGE_FUSED_AGGW")) != 0;
+  // Q projections read their weight pre-split into bf16 planes (one small
+  // split launch per layer per forward; the GEMM then converts A only)
+  bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -357,6 +361,7 @@ static void layout(Engine& E) {
     lb.loc = carve(cur, FS * T * 4);
     lb.wloc = carve(cur, FS * T * 4);
     lb.q = carve(cur, FN * c.hid * 4);
+    lb.qsplit = carve(cur, 3 * c.hid * lb.d * 2);
     lb.agg = carve(cur, FS * c.hid * 4);
     lb.y = carve(cur, FS * c.out * 4);
     lb.nrm = carve(cur, FS * 4);
@@ -535,6 +540,13 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     q.ldc = c.hid;
     q.bias = E.params + lb.pQb;
     q.act = true;
+    if (E.presplit_q && gemm_default_prec() == 1 && lb.d % 8 == 0) {
+      uint16_t* planes = at<uint16_t>(ws, lb.qsplit);
+      Timed ts(E, lname("fwd.q_split", l), st);
+      PS_TRY(launch_split_planes(E.params + lb.pQw, c.hid, lb.d, lb.d, planes, st));
+      q.b_split = planes;
+      q.ldb_split = lb.d;
+    }
     {
       Timed tt(E, lname("fwd.q_gemm", l), st);
       with_sk(E, ws, q);

@@ -80,7 +80,19 @@ struct GemmParams {
   // fp32-level error at 2.67x the f32 MFMA rate); K-major A and B only;
   // -1 = the library default (PINSAGE_GEMM_PREC, else 1 where allowed)
   int prec = -1;
+  // split-bf16 only, K-major B: B already split into its hi / mid / lo bf16
+  // planes (launch_split_planes: three [N][ldb_split] planes, bitwise the
+  // kernel's own in-register split), read instead of b.  The kernel then
+  // converts A only.  Used by cfg 0 and 3 (the other tiles' rings do not fit
+  // the 1.5x larger B image); ignored elsewhere.  K and ldb_split % 8 == 0.
+  const uint16_t* b_split = nullptr;
+  int64_t ldb_split = 0;
 };
+
+// hi / mid / lo bf16 planes of a row-major fp32 matrix w[rows][cols] (row
+// stride ldw floats): out[p][r][c], plane stride rows*cols (cols % 8 == 0)
+int launch_split_planes(const float* w, int64_t rows, int64_t cols, int64_t ldw, uint16_t* out,
+                        hipStream_t st);
 
 // default product arithmetic (GemmParams::prec = -1): 0 fp32 MFMA, 1 split bf16
 int gemm_default_prec();

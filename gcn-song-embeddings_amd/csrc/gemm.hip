@@ -131,6 +131,42 @@ struct KOp {
   }
 };
 
+// K-major operand stored pre-split (GemmParams::b_split): three bf16 planes
+// [R][ldb] each, the stage image of each plane a KOp image of BK/2 floats per
+// row (8 bf16 per 16-B chunk, so a lane's 8 k of one 16-k step are one
+// swizzled ds_read_b128 per plane).  k coordinates are in elements; the plane
+// images are addressed in floats (k / 2).
+template <int R, int BK>
+struct KSplitOp {
+  using P = KOp<R, BK / 2>;
+  static constexpr int NI = 3 * P::NI;
+  static constexpr int SZ = 3 * P::SZ;
+  __device__ static __forceinline__ float4 frag(const float* img, int row, int k4) {
+    return P::frag(img, row, k4);  // (only the split-bf16 path reads this operand)
+  }
+  P op;
+  int64_t pstride;  // floats between planes
+  __device__ __forceinline__ void init(int tid, int r0, int rmax, const uint16_t* b, int64_t ldb,
+                                       int64_t rows) {
+    op.init(tid, r0, rmax, reinterpret_cast<const float*>(b), ldb / 2, nullptr, nullptr, 0, nullptr);
+    pstride = rows * ldb / 2;
+  }
+  __device__ __forceinline__ void issue(unsigned img, int wave, int k0, int kend, int) const {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int j = 0; j < P::NI; ++j) {
+        const int k = min(k0 / 2 + op.lc[j], kend / 2 - 4);
+        glds16(op.rp[j] + q * pstride + k,
+               img + (unsigned)(q * P::SZ) * 4u + (unsigned)(j * 256 + wave * 64) * 16u);
+      }
+  }
+  __device__ __forceinline__ void zero_tail(float* img, int tid, int k0, int kend) const {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) op.zero_tail(img + q * P::SZ, tid, k0 / 2, kend / 2);
+  }
+};
+
 // MN-major operand: global [k][col] (k rows optionally gathered; columns >= c1
 // from a second matrix), LDS image linear [BK][R].
 template <int R, int BK>
@@ -224,12 +260,14 @@ __device__ __forceinline__ void wait_stage(int younger) {
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK; at most
 // NSMAX stage buffers in the ring.
 template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2,
-          bool BF = false>
+          bool BF = false, bool PB = false>
 __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   static_assert(!BF || BK % 16 == 0, "split-bf16 products: 16-k steps");
+  static_assert(!PB || (BF && BKM), "pre-split B: split-bf16 products, K-major B");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
-  using OpB = typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type;
+  using OpB = typename std::conditional<
+      PB, KSplitOp<BN, BK>, typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type>::type;
   constexpr int SZA = OpA::SZ, SZB = OpB::SZ, SZS = SZA + SZB;
   constexpr int NG = OpA::NI + OpB::NI;  // DMAs per wave per stage
   constexpr bool GA = !AK, GB = !BKM;    // operands that may need gathered k-rows
@@ -275,7 +313,8 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
     OpB opb;
     if constexpr (AK) opa.init(tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
     else opa.init(tid, m0, M, p.a, p.lda, idxA, -1, nullptr, 0, nullptr);
-    if constexpr (BKM) opb.init(tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
+    if constexpr (PB) opb.init(tid, n0, N, p.b_split, p.ldb_split, N);
+    else if constexpr (BKM) opb.init(tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
     else opb.init(tid, n0, N, p.b, p.ldb, idxB, p.N1, p.b2, p.ldb2, idxB2);
 
     // gathered k-row numbers of the first window (no DMA is in flight here)
@@ -352,8 +391,15 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int c = (wn * TN + j) * 32 + l32;
-            split3(OpB::frag(Bs, c, 16 * t + 8 * h), OpB::frag(Bs, c, 16 * t + 8 * h + 4), bH[j], bM[j],
-                   bL[j]);
+            if constexpr (PB) {  // the planes' 8 k of this lane: one chunk each
+              using P = typename OpB::P;
+              bH[j] = __builtin_bit_cast(bf16x8, P::frag(Bs, c, 8 * t + 4 * h));
+              bM[j] = __builtin_bit_cast(bf16x8, P::frag(Bs + P::SZ, c, 8 * t + 4 * h));
+              bL[j] = __builtin_bit_cast(bf16x8, P::frag(Bs + 2 * P::SZ, c, 8 * t + 4 * h));
+            } else {
+              split3(OpB::frag(Bs, c, 16 * t + 8 * h), OpB::frag(Bs, c, 16 * t + 8 * h + 4), bH[j],
+                     bM[j], bL[j]);
+            }
           }
           // product by product over the blocks: consecutive MFMAs write
           // different accumulators (1-3 % over block by block)
@@ -698,8 +744,51 @@ int gemm_pick_config(int M, int N, int K, int splits) {
   return best;
 }
 
+// 8 elements per thread: the same split_pair as the GEMM's in-register split,
+// so a pre-split operand gives bitwise the same products
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ w, int64_t rows,
+                                                           int64_t cols, int64_t ldw,
+                                                           uint16_t* __restrict__ out) {
+  const int64_t per_row = cols / 8, n = rows * per_row;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = i / per_row, c = (i - r * per_row) * 8;
+  const float4 a = *reinterpret_cast<const float4*>(w + r * ldw + c);
+  const float4 b = *reinterpret_cast<const float4*>(w + r * ldw + c + 4);
+  bf16x8 H, M, L;
+  split3(a, b, H, M, L);
+  const int64_t o = r * cols + c, ps = rows * cols;
+  *reinterpret_cast<bf16x8*>(out + o) = H;
+  *reinterpret_cast<bf16x8*>(out + ps + o) = M;
+  *reinterpret_cast<bf16x8*>(out + 2 * ps + o) = L;
+}
+
+int launch_split_planes(const float* w, int64_t rows, int64_t cols, int64_t ldw, uint16_t* out,
+                        hipStream_t st) {
+  PS_REQUIRE(rows >= 0 && cols % 8 == 0 && ldw % 4 == 0 && ldw >= cols &&
+                 (uintptr_t)w % 16 == 0 && (uintptr_t)out % 16 == 0,
+             kErrArg, "split_planes: cols and ldw must be multiples of 8 and 4, pointers 16-B aligned");
+  const int64_t n = rows * (cols / 8);
+  if (n == 0) return kOk;
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, rows,
+                     cols, ldw, out);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 template <bool AK, bool BKM>
 static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
+  if constexpr (BKM) {
+    if (p.prec == 1 && p.b_split && (cfg == 0 || cfg == 3)) {  // pre-split B planes
+      if (cfg == 0)
+        hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true, true>), g, dim3(256), 0,
+                           st, p);
+      else
+        hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true, true>), g, dim3(256), 0,
+                           st, p);
+      return;
+    }
+  }
   if (p.prec == 1) {  // split-bf16 products (same tiles, same LDS images)
     if (cfg == 0)
       hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true>), g, dim3(256), 0, st, p);
@@ -755,6 +844,9 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
   PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
              "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
+  PS_REQUIRE(!p.b_split || (p.b_kmajor && p.ldb_split % 8 == 0 && p.ldb_split >= Kmax &&
+                            (p.K_dev || p.K % 8 == 0)),
+             kErrArg, "gemm: pre-split B needs K-major B, K and ldb_split multiples of 8");
   if (p.prec < 0) p.prec = gemm_default_prec();
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;

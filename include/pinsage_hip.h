@@ -179,6 +179,20 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
  * Process-wide; other GEMMs always use fp32 MFMA. */
 int pinsage_gemm_set_prec(int prec);
 int pinsage_gemm_get_prec(void);
+/* hi / mid / lo bf16 planes of a row-major fp32 matrix W[rows][cols] (row
+ * stride ldw floats): out[3][rows][cols] as uint16 bf16 bits, the exact split
+ * the split-bf16 GEMM does in registers (cols % 8 == 0, ldw % 4 == 0). */
+int pinsage_split_planes(const float* W, int64_t rows, int64_t cols, int64_t ldw, uint16_t* out,
+                         void* stream);
+/* pinsage_linear's product (K-major A rows gathered by a_idx, W[N][K]) under
+ * split-bf16 arithmetic with W given ALSO as its pre-split planes (from
+ * pinsage_split_planes, row stride ldws elements): the kernel converts A only.
+ * Bitwise equal to the in-register split for cfg 0 and 3 (other cfg values,
+ * -1 included, may run the in-register form; the result is the same). */
+int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
+                           const float* W, const uint16_t* W_planes, int64_t ldws,
+                           const float* bias, int64_t N, int act, float* C, int64_t ldc, int cfg,
+                           void* stream);
 /* agg[f] = sum_t w[f][t] * q[loc[f][t]]  (weights already normalised;
  * pinsage_model.py:202). */
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,

@@ -230,3 +230,67 @@ def test_split_k_weight_gradient_both_arithmetics(prec):
         lib.pinsage_gemm_set_prec(old)
     r = A.double().t() @ B.double()[b_idx.long()]
     assert _rel(C.sum(0), r) < 1e-6
+
+
+def _split_planes_ref(W):
+    """hi / mid / lo bf16 pieces by round-to-nearest-even (torch's fp32 -> bf16
+    cast), each difference exact in fp32 (gemm.hip split_pair)."""
+    H = W.to(torch.bfloat16)
+    r = W - H.float()
+    Mp = r.to(torch.bfloat16)
+    L = (r - Mp.float()).to(torch.bfloat16)
+    return torch.stack([H, Mp, L]).view(torch.int16)
+
+
+@pytest.mark.parametrize("cfg", [0, 3, 1, -1])
+def test_presplit_b_planes_bitwise(cfg):
+    """The Q projection with its weight read as pre-split bf16 planes
+    (pinsage_split_planes + pinsage_linear_split_b) is bitwise the
+    in-register split-bf16 GEMM (same tiles, same products in the same order)
+    for cfg 0 / 3, which run the plane form, and for the configs that fall back
+    to the in-register split (1, and the size-picked one).  The planes
+    themselves are the RN-even split of torch's bf16 cast."""
+    import _native as nat
+    lib = nat.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device="cuda").manual_seed(31 + cfg)
+    old = lib.pinsage_gemm_get_prec()
+    try:
+        assert lib.pinsage_gemm_set_prec(1) == 0
+        for M, N, K in [(1, 128, 8), (37, 128, 136), (200, 256, 520), (3000, 512, 512),
+                        (10541, 512, 512), (24369, 512, 128)]:
+            A = torch.randn(M + 7, K, device="cuda", generator=g)
+            A *= torch.exp2(torch.randint(-20, 20, (M + 7, 1), device="cuda", generator=g).float())
+            W = torch.randn(N, K, device="cuda", generator=g) * 0.05
+            bias = torch.randn(N, device="cuda", generator=g)
+            a_idx = torch.randint(0, M + 7, (M,), device="cuda", generator=g, dtype=torch.int32)
+            planes = torch.empty(3, N, K, dtype=torch.int16, device="cuda")
+            nat.check(lib.pinsage_split_planes(_vp(W), N, K, K, _vp(planes), stream), "split_planes")
+            torch.cuda.synchronize()
+            assert torch.equal(planes, _split_planes_ref(W)), (M, N, K)
+            C0 = torch.full((M, N), float("nan"), device="cuda")
+            C1 = torch.full((M, N), float("nan"), device="cuda")
+            _gemm(M, N, K, 1, 1, A, a_idx, W, C0, bias=bias, act=1, cfg=cfg, sk=0)
+            nat.check(lib.pinsage_linear_split_b(_vp(A), K, _vp(a_idx), M, K, _vp(W), _vp(planes), K,
+                                                 _vp(bias), N, 1, _vp(C1), N, cfg, stream),
+                      "linear_split_b")
+            torch.cuda.synchronize()
+            assert torch.isfinite(C1).all(), (M, N, K)
+            assert torch.equal(C0, C1), (M, N, K, (C0 - C1).abs().max().item())
+            r = _ref(M, N, K, 1, 1, A, a_idx, W, bias, 1)
+            assert _rel(C1, r) < 2e-6, (M, N, K, _rel(C1, r))
+    finally:
+        lib.pinsage_gemm_set_prec(old)
+
+
+def test_presplit_b_argument_checks():
+    import _native as nat
+    lib = nat.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    W = torch.randn(128, 12, device="cuda")
+    planes = torch.empty(3, 128, 12, dtype=torch.int16, device="cuda")
+    assert lib.pinsage_split_planes(_vp(W), 128, 12, 12, _vp(planes), stream) != 0  # cols % 8
+    A = torch.randn(16, 12, device="cuda")
+    C = torch.empty(16, 128, device="cuda")
+    assert lib.pinsage_linear_split_b(_vp(A), 12, None, 16, 12, _vp(W), _vp(planes), 12, None, 128, 0,
+                                      _vp(C), 128, 3, stream) != 0  # K % 8
