@@ -845,8 +845,8 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
              "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
   PS_REQUIRE(!p.b_split || (p.b_kmajor && p.ldb_split % 8 == 0 && p.ldb_split >= Kmax &&
-                            (p.K_dev || p.K % 8 == 0)),
-             kErrArg, "gemm: pre-split B needs K-major B, K and ldb_split multiples of 8");
+                            (p.K_dev || p.K % 8 == 0) && (uintptr_t)p.b_split % 16 == 0),
+             kErrArg, "gemm: pre-split B needs K-major B, K and ldb_split multiples of 8, 16-B aligned planes");
   if (p.prec < 0) p.prec = gemm_default_prec();
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
   const int Mest = p.M_dev ? (p.M_hint > 0 ? std::min(p.M_hint, Mmax) : Mmax) : p.M;
