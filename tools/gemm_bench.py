@@ -32,7 +32,7 @@ def vp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_idx=False):
+def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_idx=False, presplit=False):
     # M,N,K,ak,bk[,gather[,splits]]: gather = rows of A (K-major A) or k-rows
     # of B (N-major B, the weight-gradient form); splits > 1 = split-K slabs
     M, N, K, ak, bk, *g = [int(x) for x in shape.split(",")]
@@ -54,7 +54,16 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_
     b_idx = torch.randperm(K, device=dev).to(torch.int32) if gather and not ak and not bk else None
     args = (M, N, K, ak, bk, vp(A), A.shape[1], vp(a_idx), vp(B), B.shape[1], vp(b_idx), vp(C), N,
             vp(bias), int(bias_act), 3 if splits > 1 else 0, splits, cfg, sk, ctypes.c_void_p(stream.cuda_stream))
-    rc = lib.pinsage_gemm_ex(*args)
+    call = lib.pinsage_gemm_ex
+    if presplit:  # B (K-major, [N][K]) read as pre-split bf16 planes: pinsage_linear_split_b
+        assert ak and bk and splits == 1 and sk == 0, "pre-split B: K-major operands, no split-K/stream-K"
+        planes = torch.empty(3, N, K, dtype=torch.int16, device=dev)
+        nat.check(lib.pinsage_split_planes(vp(B), N, K, K, vp(planes), ctypes.c_void_p(stream.cuda_stream)),
+                  "split_planes")
+        args = (vp(A), A.shape[1], vp(a_idx), M, K, vp(B), vp(planes), K, vp(bias), N, int(bias_act), vp(C),
+                N, cfg, ctypes.c_void_p(stream.cuda_stream))
+        call = lib.pinsage_linear_split_b
+    rc = call(*args)
     if rc != 0:
         raise RuntimeError(lib.pinsage_last_error().decode())
     ref = ((A[a_idx.long()] if a_idx is not None else A) if ak else A.t()).double()
@@ -64,12 +73,13 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_
     err = ((C.sum(0).double() - ref).norm() / ref.norm()).item()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
-        lib.pinsage_gemm_ex(*args)
-    all_args = [tuple(vp(ix) if i == 7 else a for i, a in enumerate(args)) for ix in idx_sets] \
+        call(*args)
+    ai = 2 if presplit else 7  # position of a_idx
+    all_args = [tuple(vp(ix) if i == ai else a for i, a in enumerate(args)) for ix in idx_sets] \
         if idx_sets[0] is not None else [args]
     e0.record(stream)
     for r in range(reps):
-        lib.pinsage_gemm_ex(*all_args[r % len(all_args)])
+        call(*all_args[r % len(all_args)])
     e1.record(stream)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
@@ -86,18 +96,20 @@ def main():
     ap.add_argument("--sets", type=int, default=1, help="row sets cycled over repetitions")
     ap.add_argument("--bias-act", action="store_true", help="bias + LeakyReLU epilogue (the Q projection)")
     ap.add_argument("--sorted", action="store_true", help="gathered rows in ascending order")
-    ap.add_argument("--prec", default="1", help="product arithmetic(s): 0 fp32 MFMA, 1 split bf16")
+    ap.add_argument("--prec", default="1",
+                    help="product arithmetic(s): 0 fp32 MFMA, 1 split bf16, 2 split bf16 with pre-split B planes")
     a = ap.parse_args()
     lib = nat.lib()
     stream = torch.cuda.current_stream()
     for s in a.shapes:
       for prec in [int(x) for x in a.prec.split(",")]:
-        lib.pinsage_gemm_set_prec(prec)
+        lib.pinsage_gemm_set_prec(min(prec, 1))
         for cfg in [int(c) for c in a.cfgs.split(",")]:
             for sk in [int(c) for c in a.sk.split(",")]:
                 if sk == 1 and cfg == 0:
                     continue
-                us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets, a.bias_act, a.sorted)
+                us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets, a.bias_act, a.sorted,
+                                  presplit=prec == 2)
                 print(f"{s:24s} prec={prec} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
                       flush=True)
 
