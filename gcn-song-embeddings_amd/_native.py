@@ -75,6 +75,8 @@ _SIGS = {
                                        vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp]),
     "pinsage_weighted_agg": (ctypes.c_int, [vp, i64, vp, vp, i64, i64, vp, vp]),
+    "pinsage_conv_agg_project": (ctypes.c_int, [vp, i64, i64, vp, vp, i64, i64, vp, vp, i64, i64, vp, vp,
+                                                i64, vp, vp, vp, vp, vp]),
     "pinsage_gemm_set_prec": (ctypes.c_int, [ctypes.c_int]),
     "pinsage_gemm_get_prec": (ctypes.c_int, []),
     "pinsage_split_planes": (ctypes.c_int, [vp, i64, i64, i64, vp, vp]),

@@ -20,7 +20,9 @@
 // one-chunk register double buffer.  Then bias, LeakyReLU and the row L2 norm
 // through a [16][128] LDS image.
 #include <algorithm>
+#include <cstdlib>
 
+#include "bf16split.h"
 #include "common.h"
 
 namespace ps {
@@ -373,6 +375,297 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
     }
     __syncthreads();  // LDS is reused by the next tile
   }
+}
+
+// ---------------------------------------------------------------------------
+// Round-3 form: the aggregation and the projection pipelined inside every wave,
+// the projection on split-bf16 MFMA (v_mfma_f32_32x32x16_bf16, six products per
+// 16-k step) with W pre-split into hi / mid / lo planes stored in MFMA fragment
+// order, K split over the eight waves of a 512-thread workgroup (one per CU).
+//
+// A tile is <= 32 rows.  K is cut into 32-float chunks (one 128-B line of a
+// row); wave w owns chunks w, w + 8, ... of the aggregate part (k in
+// [d, d + hid)) and of the self part (k in [0, d)).  For a chunk, the wave
+// streams the tile's slot rows of q in units of one slot (32 rows x 128 B:
+// four loads per lane, each instruction 8 full rows = 8 whole lines -- the
+// MFMA-fragment-shaped loads of the first form touched 32 lines per
+// instruction and were bound by the load path), RD units in flight, and sums
+// them in slot order t = 0, 1, ... (the fma chain of agg_kernel).  At the
+// chunk's last slot the aggregate goes to agg (the W weight gradient reads it)
+// and through a wave-private LDS image into the MFMA A layout; each of its two
+// 16-k steps runs 4 column blocks x 6 products against B fragments that are
+// one contiguous 1-KB load per (step, column block, plane).  LDS also holds the
+// tile's slot offsets / weights and, at the end, the eight waves' partial
+// [32][128] tiles (aliasing the A images), summed in wave order with bias,
+// LeakyReLU and the row L2 norm (pinsage_model.py:208-211).
+//
+// Rows are dealt in contiguous ranges: block b of G owns [F b / G, F (b+1) / G)
+// in near-equal tiles of <= 32 rows, so G ~ F / 24 blocks fill the CUs (C2
+// layer 0: 238 blocks of 24 rows); padded MFMA rows issue no loads.
+constexpr int kA3Rows = 32;
+constexpr int kA3Waves = 8;
+constexpr int kA3Out = 128;
+constexpr int kA3TMax = 64;
+constexpr int kA3TS = kA3TMax + 1;  // slot-table row stride (words)
+constexpr int kA3RD = 3;            // slot units in flight per wave
+constexpr int kA3AS = 36;           // A image row stride (floats): conflict-free b128 reads
+
+typedef __attribute__((ext_vector_type(16))) float a3_f32x16;
+typedef int a3_v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 a3_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ bf16x8 a3_ldb(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void a3_fma4(float w, const float4& a, float4& x) {
+  x.x = fmaf(w, a.x, x.x);
+  x.y = fmaf(w, a.y, x.y);
+  x.z = fmaf(w, a.z, x.z);
+  x.w = fmaf(w, a.w, x.w);
+}
+constexpr unsigned kA3Off = 0x80000000u;  // past the buffer: the load returns 0, no request
+
+// W [128][K] fp32 -> three bf16 planes in MFMA fragment order:
+// Wf[ks][cb][p][lane][8] = plane p of W[32 cb + lane % 32][16 ks + 8 (lane / 32) + j]
+// (the split is bf16split.h's, so the products are those of the GEMM's split)
+__global__ __launch_bounds__(256) void split_w_frag_kernel(const float* __restrict__ W, int K,
+                                                           uint16_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (ks, cb, lane)
+  const int nks = K >> 4;
+  if (i >= nks * 4 * 64) return;
+  const int lane = i & 63, cb = (i >> 6) & 3, ks = i >> 8;
+  const float* src = W + (int64_t)(32 * cb + (lane & 31)) * K + 16 * ks + 8 * (lane >> 5);
+  bf16x8 H, M, L;
+  split3(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 4), H, M, L);
+  bf16x8* dst = reinterpret_cast<bf16x8*>(out) + ((int64_t)(ks * 4 + cb) * 3) * 64 + lane;
+  dst[0] = H;
+  dst[64] = M;
+  dst[128] = L;
+}
+
+// q: [rows][hid] with rows * hid * 4 < 2^31 (launch_agg_w3 checks)
+__global__ __launch_bounds__(kA3Waves * 64, 2) void agg_w3_kernel(
+    const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
+    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
+    const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
+    const uint16_t* __restrict__ Wf, const float* __restrict__ bias, float* __restrict__ y,
+    float* __restrict__ nrm_out, float* __restrict__ agg, int dbg) {
+  __shared__ __attribute__((aligned(16))) float red[kA3Waves * kA3Rows * kA3Out];  // 128 KiB
+  __shared__ unsigned sOff[kA3Rows * kA3TS];  // byte offsets of the tile's slot rows in q
+  __shared__ float sW[kA3Rows * kA3TS];
+  __shared__ int sSelf[kA3Rows];
+  static_assert(kA3Waves * kA3Rows * kA3AS <= kA3Waves * kA3Rows * kA3Out, "A images alias red");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: SGPR offsets
+  // load layout: lane (rs, kq) holds rows rs + 8 j (j < 4), floats 4 kq .. 4 kq + 3 of a chunk
+  const int rs = lane >> 3, kq = lane & 7;
+  // MFMA layout: lane (row, half) supplies A[row][8 half .. 8 half + 7] of a 16-k step
+  const int row = lane & 31, half = lane >> 5;
+  float* Aimg = red + wave * kA3Rows * kA3AS;  // this wave's [32][36] A image
+  const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc((void*)q, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, 0x7fffffff, 0x00020000);
+  const int64_t F = nS ? (int64_t)*nS : n_static;
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / G, re = F * (b + 1) / G;
+  const int64_t len = re - rb;
+  const int ntile = (int)((len + kA3Rows - 1) / kA3Rows);
+  // this wave's chunks: aggregate part first (T slot units each), then the self part (one unit)
+  const int nca = hid >> 5, ncs = d >> 5;
+  const int na = nca > wave ? (nca - wave + kA3Waves - 1) / kA3Waves : 0;
+  const int ns = ncs > wave ? (ncs - wave + kA3Waves - 1) / kA3Waves : 0;
+  const int nunits = na * T + ns;
+
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int64_t r0 = rb + len * tile / ntile;
+    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
+    for (int i = tid; i < kA3Rows * T; i += kA3Waves * 64) {
+      const int r = i / T, t = i - r * T;
+      const bool ok = r < nrows;
+      sOff[r * kA3TS + t] = ok && !(dbg & 1) ? (unsigned)loc[(r0 + r) * T + t] * (unsigned)hid * 4u : kA3Off;
+      sW[r * kA3TS + t] = ok ? wloc[(r0 + r) * T + t] : 0.f;
+    }
+    if (tid < kA3Rows) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : -1;
+    __syncthreads();
+
+    a3_f32x16 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+
+    // unit s: aggregate chunk s / T, slot s % T; or self chunk s - na T
+    float4 buf[kA3RD][4];
+    auto issue = [&](int s, int u) __attribute__((always_inline)) {
+      if (s < na * T) {
+        const int ci = s / T, t = s - ci * T;
+        const unsigned kb = 128u * (unsigned)(wave + kA3Waves * ci) + 16u * kq;  // bytes into the q row
+#pragma unroll
+        for (int j = 0; j < 4; ++j) buf[u][j] = a3_ld(qr, sOff[(rs + 8 * j) * kA3TS + t] + kb, 0);
+      } else {
+        const int k0 = 32 * (wave + kA3Waves * (s - na * T)) + 4 * kq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int sr = sSelf[rs + 8 * j];
+          buf[u][j] = sr >= 0 ? *reinterpret_cast<const float4*>(h + (int64_t)sr * ldh + k0)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < kA3RD; ++u)
+      if (u < nunits) issue(u, u);
+
+    float4 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int ci = 0, t = 0;  // chunk (in this wave's list) and slot of the unit being consumed
+    for (int s0 = 0; s0 < nunits; s0 += kA3RD) {
+#pragma unroll
+      for (int u = 0; u < kA3RD; ++u) {
+        const int s = s0 + u;
+        if (s >= nunits) break;
+        const bool is_agg = ci < na;
+        if (is_agg) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a3_fma4(sW[(rs + 8 * j) * kA3TS + t], buf[u][j], x[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[j] = buf[u][j];
+        }
+        if (s + kA3RD < nunits) issue(s + kA3RD, u);
+        if (is_agg && ++t < T) continue;
+        // ---- the chunk is complete: agg out, A image, two 16-k steps of MFMAs
+        const int kc = is_agg ? d + 32 * (wave + kA3Waves * ci) : 32 * (wave + kA3Waves * (ci - na));
+        if (is_agg) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (rs + 8 * j < nrows)
+              *reinterpret_cast<float4*>(agg + (r0 + rs + 8 * j) * hid + (kc - d) + 4 * kq) = x[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<float4*>(Aimg + (rs + 8 * j) * kA3AS + 4 * kq) = x[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        ++ci;
+        t = 0;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int ks = (kc >> 4) + st;
+          bf16x8 bw[3][4];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              bw[p][c] = a3_ldb(wr, (dbg & 2) ? kA3Off : (unsigned)lane * 16u, (unsigned)(((ks * 4 + c) * 3 + p) * 1024));
+          if (dbg & 4) continue;
+          const float* ar = Aimg + row * kA3AS + 16 * st + 8 * half;
+          bf16x8 aH, aM, aL;
+          split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), aH, aM, aL);
+#define PS_A3_ALL(X, P)                                                                         \
+  _Pragma("unroll") for (int c = 0; c < 4; ++c) acc[c] =                                      \
+      __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, bw[P][c], acc[c], 0, 0, 0);
+          PS_A3_ALL(aL, 0)
+          PS_A3_ALL(aH, 2)
+          PS_A3_ALL(aM, 1)
+          PS_A3_ALL(aM, 0)
+          PS_A3_ALL(aH, 1)
+          PS_A3_ALL(aH, 0)
+#undef PS_A3_ALL
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with its A image (red aliases them)
+    // partial tiles -> red[wave][row][col]; acc[c][r] is row (r & 3) + 8 (r >> 2) + 4 half, col 32 c + row
+    {
+      float* mine = red + wave * kA3Rows * kA3Out;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mine[((r & 3) + 8 * (r >> 2) + 4 * half) * kA3Out + 32 * c + row] = acc[c][r];
+    }
+    __syncthreads();
+    {
+      const int er = tid >> 4, c8 = (tid & 15) * 8;  // 16 threads per row, 8 columns each
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+      for (int w = 0; w < kA3Waves; ++w) {
+        const float* src = red + (w * kA3Rows + er) * kA3Out + c8;
+        const float4 a = *reinterpret_cast<const float4*>(src);
+        const float4 bq = *reinterpret_cast<const float4*>(src + 4);
+        v[0] += a.x;
+        v[1] += a.y;
+        v[2] += a.z;
+        v[3] += a.w;
+        v[4] += bq.x;
+        v[5] += bq.y;
+        v[6] += bq.z;
+        v[7] += bq.w;
+      }
+      float s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = lrelu(v[e] + bias[c8 + e]);
+        s2 += v[e] * v[e];
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+      const float nrm = sqrtf(s2);
+      if (er < nrows) {
+        float* dst = y + (r0 + er) * kA3Out + c8;
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4] / nrm, v[5] / nrm, v[6] / nrm, v[7] / nrm);
+        if ((tid & 15) == 0 && nrm_out) nrm_out[r0 + er] = nrm;
+      }
+    }
+    __syncthreads();  // red, the A images and the slot tables are reused by the next tile
+  }
+}
+
+int agg_w3_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
+  return out == kA3Out && d % 32 == 0 && hid % 32 == 0 && d > 0 && hid > 0 && T >= 1 && T <= kA3TMax;
+}
+
+// the fragment-ordered planes of W [128][K] (3 * 128 * K uint16 at Wf)
+int launch_split_w_frag(const float* W, int64_t K, uint16_t* Wf, hipStream_t st) {
+  PS_REQUIRE(K % 16 == 0 && K > 0 && (uintptr_t)W % 16 == 0 && (uintptr_t)Wf % 16 == 0, kErrArg,
+             "split_w_frag: K % 16 == 0, 16-B aligned");
+  const int n = (int)(K / 16) * 4 * 64;
+  hipLaunchKernelGGL(split_w_frag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, W, (int)K, Wf);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+static int g_aggw3_rows = -1;  // target rows per workgroup (PINSAGE_AGGW_ROWS)
+
+int launch_agg_w3(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
+                  int64_t q_rows_cap, const int32_t* loc, const float* wloc, int T, const int* nS,
+                  int64_t n_static, int64_t S_est, const uint16_t* Wf, const float* bias, float* y, float* nrm,
+                  float* agg, hipStream_t st) {
+  PS_REQUIRE(agg_w3_supported(d, hid, kA3Out, T), kErrArg, "agg_w3: unsupported shape");
+  PS_REQUIRE(q_rows_cap * hid * 4 < (1LL << 31) && (int64_t)kA3Out * (d + hid) * 2 * 3 < (1LL << 31), kErrArg,
+             "agg_w3: q or W planes too large for 32-bit buffer offsets");
+  PS_REQUIRE(ldh % 4 == 0 && (uintptr_t)h % 16 == 0 && (uintptr_t)q % 16 == 0 && (uintptr_t)agg % 16 == 0 &&
+                 (uintptr_t)y % 16 == 0 && (uintptr_t)Wf % 16 == 0,
+             kErrArg, "agg_w3: 16-B aligned rows required");
+  if (S_est <= 0) return kOk;
+  if (g_aggw3_rows < 0) {
+    const char* e = getenv("PINSAGE_AGGW_ROWS");
+    g_aggw3_rows = e ? std::max(1, atoi(e)) : 24;
+  }
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int64_t g = std::min<int64_t>(cus, std::max<int64_t>(1, (S_est + g_aggw3_rows - 1) / g_aggw3_rows));
+  static const int dbg = getenv("PINSAGE_AGGW_DBG") ? atoi(getenv("PINSAGE_AGGW_DBG")) : 0;  // A/B only
+  hipLaunchKernelGGL(agg_w3_kernel, dim3((unsigned)g), dim3(kA3Waves * 64), 0, st, h, ldh, d, self_src, q,
+                     hid, loc, wloc, T, nS, n_static, Wf, bias, y, nrm, agg, dbg);
+  PS_CHECK_LAUNCH();
+  return kOk;
 }
 
 static int agg_w32_supported(int64_t d, int64_t hid, int64_t T) {

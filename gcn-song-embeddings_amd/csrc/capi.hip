@@ -36,6 +36,11 @@ int launch_mark_table_i64(unsigned long long*, const int64_t*, int64_t, const in
                           int, int64_t, int*, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
+int agg_w3_supported(int64_t, int64_t, int64_t, int64_t);
+int launch_split_w_frag(const float*, int64_t, uint16_t*, hipStream_t);
+int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
+                  const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
+                  float*, float*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int64_t knn_scratch_bytes(int64_t, int64_t);
@@ -537,6 +542,21 @@ int pinsage_knn_cosine(const float* emb, int64_t n, int64_t d, int64_t ld, const
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
                          int64_t n_rows, int64_t T, float* agg, void* stream) {
   return launch_agg(q, (int)hid, loc, w, (int)T, nullptr, n_rows, agg, (hipStream_t)stream);
+}
+
+int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32_t* self_src,
+                             const float* q, int64_t hid, int64_t q_rows, const int32_t* loc,
+                             const float* w, int64_t n_rows, int64_t T, const float* W,
+                             const float* bias, int64_t out, uint16_t* W_planes, float* y,
+                             float* norms, float* agg, void* stream) {
+  if (!agg_w3_supported(d, hid, out, T) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX) {
+    set_error("conv_agg_project: out_dim must be 128, d and hid multiples of 32, 1 <= T <= 64");
+    return kErrArg;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  PS_TRY(launch_split_w_frag(W, d + hid, W_planes, st));
+  return launch_agg_w3(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows,
+                       n_rows, W_planes, bias, y, norms, agg, st);
 }
 
 }  // extern "C"
