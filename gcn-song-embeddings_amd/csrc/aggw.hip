@@ -625,6 +625,256 @@ __global__ __launch_bounds__(kA3Waves * 64, 2) void agg_w3_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Round-3 form, warp-specialised (the default): in a 512-thread workgroup per
+// CU, waves 0-3 only GATHER and waves 4-7 only MULTIPLY, so the slot-row
+// stream never pauses for the projection.
+//
+// Producer wave j streams, for round b, the slot rows of aggregate chunk
+// c = 4 b + j (32 floats of q = one 128-B line per row; one unit = one slot =
+// 32 rows x 128 B = four loads per lane, each instruction 8 whole lines) with
+// RD units in flight (RD | T, so the stream runs on into its next chunk
+// without a bubble), sums them in slot order t = 0, 1, ... (agg_kernel's fma
+// chain), writes agg, splits the sum into bf16 hi / mid / lo and stores the
+// three planes into its ring slot; the self rows of self chunk 4 b + j
+// (k in [0, d)) go to a second slot (loaded a round ahead).  Consumer wave j
+// owns output columns 32 j .. 32 j + 31 for the whole K: per round it runs the
+// round's chunks' 16-k steps (v_mfma_f32_32x32x16_bf16, six products) with B
+// fragments read as contiguous 1-KB lines of the fragment-ordered fp32 W
+// (prefetched a round ahead, split in registers), so no cross-wave reduction
+// is needed.  Rounds are double-buffered halves of an LDS ring (one barrier per
+// round).  The epilogue sums nothing: bias, LeakyReLU and the row L2 norm over
+// the four consumers' [32][32] blocks.
+constexpr int kA4Rows = 32;
+constexpr int kA4RowB = 80;    // ring plane row stride (bytes): conflict-free b64 writes / b128 reads
+constexpr int kA4Plane = kA4Rows * kA4RowB;   // 2560 B
+constexpr int kA4Img = 3 * kA4Plane;          // 7680 B: one chunk image (hi, mid, lo)
+constexpr int kA4Half = 4 * 2 * kA4Img;       // 4 producers x (aggregate, self) images
+constexpr int kA4BMax = 16;                   // 16-k steps per round per consumer (8 chunks x 2)
+
+// fp32 W [128][K] -> MFMA fragment order Wr[ks][cb][qh][lane][4] =
+// W[32 cb + lane % 32][16 ks + 8 (lane / 32) + 4 qh + e]: one 16-k step of one
+// column block is two contiguous 1-KB loads
+__global__ __launch_bounds__(256) void reorder_w_frag_kernel(const float* __restrict__ W, int K,
+                                                             float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (K >> 4) * 512) return;
+  const int lane = i & 63, qh = (i >> 6) & 1, cb = (i >> 7) & 3, ks = i >> 9;
+  const float* src = W + (int64_t)(32 * cb + (lane & 31)) * K + 16 * ks + 8 * (lane >> 5) + 4 * qh;
+  reinterpret_cast<float4*>(out)[i] = *reinterpret_cast<const float4*>(src);
+}
+
+constexpr int kA4TS = kA3TMax + 4;  // slot-table row stride (words): room for T padded to RD
+
+template <int RD>
+__global__ __launch_bounds__(512, 2) void agg_w4_kernel(
+    const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
+    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
+    const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
+    const float* __restrict__ Wr, const float* __restrict__ bias, float* __restrict__ y,
+    float* __restrict__ nrm_out, float* __restrict__ agg) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[2 * kA4Half];  // 120 KiB
+  __shared__ unsigned sOff[kA3Rows * kA4TS];
+  __shared__ float sW[kA3Rows * kA4TS];
+  __shared__ int sSelf[kA3Rows];
+  float* red = reinterpret_cast<float*>(ring);  // [32][128] in the epilogue
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = wave < 4;
+  const int pj = wave & 3;
+  const int rs = lane >> 3, kq = lane & 7;      // producer: rows rs + 8 j, floats 4 kq ..
+  const int row = lane & 31, half = lane >> 5;  // consumer: MFMA lane
+  const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc((void*)q, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)Wr, 0, 0x7fffffff, 0x00020000);
+  const int64_t F = nS ? (int64_t)*nS : n_static;
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / G, re = F * (b + 1) / G;
+  const int64_t len = re - rb;
+  const int ntile = (int)((len + kA4Rows - 1) / kA4Rows);
+  const int nca = hid >> 5, ncs = d >> 5;
+  const int nr = max((nca + 3) >> 2, (ncs + 3) >> 2);  // rounds
+  const int pa = nca > pj ? (nca - pj + 3) >> 2 : 0;   // this producer's aggregate chunks
+  const int Tp = (T + RD - 1) / RD * RD;
+
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int64_t r0 = rb + len * tile / ntile;
+    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
+    // slots T .. Tp - 1 (T padded to a multiple of RD) read nothing with weight 0
+    for (int i = tid; i < kA3Rows * Tp; i += 512) {
+      const int r = i / Tp, t = i - r * Tp;
+      const bool ok = r < nrows && t < T;
+      sOff[r * kA4TS + t] = ok ? (unsigned)loc[(r0 + r) * T + t] * (unsigned)hid * 4u : kA3Off;
+      sW[r * kA4TS + t] = ok ? wloc[(r0 + r) * T + t] : 0.f;
+    }
+    if (tid < kA3Rows) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : -1;
+    __syncthreads();
+
+    if (producer) {
+      float4 buf[RD][4], sb[4], x[4];
+      // unit (ci, t): slot t of this producer's aggregate chunk ci into buf[t % RD]
+      auto issue = [&](int ci, int t, int u) __attribute__((always_inline)) {
+        const unsigned cbase = 128u * (unsigned)(4 * ci + pj);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) buf[u][j] = a3_ld(qr, sOff[(rs + 8 * j) * kA4TS + t] + 16u * kq, cbase);
+      };
+      // self rows of self chunk 4 rr + pj into sb
+      auto issue_self = [&](int rr) __attribute__((always_inline)) {
+        const int c = 4 * rr + pj;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int sr = sSelf[rs + 8 * j];
+          sb[j] = (c < ncs && sr >= 0) ? *reinterpret_cast<const float4*>(h + (int64_t)sr * ldh + 32 * c + 4 * kq)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      };
+      // split 4 rows x 4 floats into the three planes of an image
+      auto put = [&](unsigned char* img) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          unsigned H0, M0, L0, H1, M1, L1;
+          split_pair(f32x2{x[j].x, x[j].y}, H0, M0, L0);
+          split_pair(f32x2{x[j].z, x[j].w}, H1, M1, L1);
+          unsigned char* r = img + (rs + 8 * j) * kA4RowB + 8 * kq;
+          *reinterpret_cast<uint2*>(r) = make_uint2(H0, H1);
+          *reinterpret_cast<uint2*>(r + kA4Plane) = make_uint2(M0, M1);
+          *reinterpret_cast<uint2*>(r + 2 * kA4Plane) = make_uint2(L0, L1);
+        }
+      };
+      if (pa > 0) {
+#pragma unroll
+        for (int u = 0; u < RD; ++u) issue(0, u, u);
+      }
+      issue_self(0);
+      for (int bb = 0; bb <= nr; ++bb) {
+        if (bb < nr) {
+          unsigned char* slot = ring + (bb & 1) * kA4Half + pj * 2 * kA4Img;
+          if (bb < pa) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int t0 = 0; t0 < Tp; t0 += RD) {
+#pragma unroll
+              for (int u = 0; u < RD; ++u) {
+                const int t = t0 + u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a3_fma4(sW[(rs + 8 * j) * kA4TS + t], buf[u][j], x[j]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (t + RD < Tp) issue(bb, t + RD, u);
+                else if (bb + 1 < pa) issue(bb + 1, t + RD - Tp, u);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+            const int c = 4 * bb + pj;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (rs + 8 * j < nrows)
+                *reinterpret_cast<float4*>(agg + (r0 + rs + 8 * j) * hid + 32 * c + 4 * kq) = x[j];
+            put(slot);
+          }
+          if (4 * bb + pj < ncs) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = sb[j];
+            issue_self(bb + 1);
+            put(slot + kA4Img);
+          }
+        }
+        __syncthreads();
+      }
+    } else {
+      // consumer: column block pj for all of K
+      a3_f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      // B fragments of 16-k steps, a ring of kA4BP steps ahead (static indices:
+      // the 16 steps of a round are unrolled, 16 % kA4BP == 0, so the ring runs
+      // on into the next round)
+      constexpr int kA4BP = 4;
+      float4 bq[kA4BP][2];
+      // the 16-k steps of round rr, in order: aggregate chunks 4 rr .. 4 rr + 3 (two steps
+      // each), then self chunks 4 rr .. 4 rr + 3; step i of the round -> global 16-k step
+      auto ks_of = [&](int rr, int i) -> int {
+        const int c = 4 * rr + (i >> 1) % 4;
+        return i < 8 ? ((d >> 4) + 2 * c + (i & 1)) : (2 * c + (i & 1));
+      };
+      auto valid_step = [&](int rr, int i) -> bool {
+        const int c = 4 * rr + (i >> 1) % 4;
+        return rr < nr && (i < 8 ? c < nca : c < ncs);
+      };
+      auto load_b = [&](int rr, int i, int u) __attribute__((always_inline)) {
+        if (valid_step(rr, i)) {
+          const unsigned so = (unsigned)((ks_of(rr, i) * 4 + pj) * 2) * 1024u;
+          bq[u][0] = a3_ld(wr, (unsigned)lane * 16u, so);
+          bq[u][1] = a3_ld(wr, (unsigned)lane * 16u, so + 1024u);
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < kA4BP; ++i) load_b(0, i, i);
+      for (int bb = 0; bb <= nr; ++bb) {
+        if (bb >= 1) {
+          const int rr = bb - 1;
+          const unsigned char* hbase = ring + (rr & 1) * kA4Half;
+#pragma unroll
+          for (int i = 0; i < kA4BMax; ++i) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (valid_step(rr, i)) {
+              const int src = (i >> 1) % 4, kind = i < 8 ? 0 : 1;
+              const unsigned char* ap =
+                  hbase + (src * 2 + kind) * kA4Img + row * kA4RowB + (16 * (i & 1) + 8 * half) * 2;
+              const bf16x8 aH = *reinterpret_cast<const bf16x8*>(ap);
+              const bf16x8 aM = *reinterpret_cast<const bf16x8*>(ap + kA4Plane);
+              const bf16x8 aL = *reinterpret_cast<const bf16x8*>(ap + 2 * kA4Plane);
+              bf16x8 bH, bM, bL;
+              split3(bq[i % kA4BP][0], bq[i % kA4BP][1], bH, bM, bL);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
+            }
+            // the step kA4BP ahead (into the next round for the last ones)
+            if (i + kA4BP < kA4BMax) load_b(rr, i + kA4BP, i % kA4BP);
+            else load_b(rr + 1, i + kA4BP - kA4BMax, i % kA4BP);
+          }
+        }
+        __syncthreads();
+      }
+      // the [32][32] block of columns 32 pj .. -> red (the ring is idle now)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((r & 3) + 8 * (r >> 2) + 4 * half) * kA3Out + 32 * pj + row] = acc[r];
+    }
+    __syncthreads();
+    {
+      const int er = tid >> 4, c8 = (tid & 15) * 8;
+      float v[8];
+      float s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = lrelu(red[er * kA3Out + c8 + e] + bias[c8 + e]);
+        s2 += v[e] * v[e];
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+      const float nrm = sqrtf(s2);
+      if (er < nrows) {
+        float* dst = y + (r0 + er) * kA3Out + c8;
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4] / nrm, v[5] / nrm, v[6] / nrm, v[7] / nrm);
+        if ((tid & 15) == 0 && nrm_out) nrm_out[r0 + er] = nrm;
+      }
+    }
+    __syncthreads();  // red (the ring) and the slot tables are reused by the next tile
+  }
+}
+
+int launch_reorder_w_frag(const float* W, int64_t K, float* Wr, hipStream_t st) {
+  PS_REQUIRE(K % 16 == 0 && K > 0 && (uintptr_t)W % 16 == 0 && (uintptr_t)Wr % 16 == 0, kErrArg,
+             "reorder_w_frag: K % 16 == 0, 16-B aligned");
+  const int n = (int)(K / 16) * 512;
+  hipLaunchKernelGGL(reorder_w_frag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, W, (int)K, Wr);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 int agg_w3_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
   return out == kA3Out && d % 32 == 0 && hid % 32 == 0 && d > 0 && hid > 0 && T >= 1 && T <= kA3TMax;
 }
@@ -635,6 +885,34 @@ int launch_split_w_frag(const float* W, int64_t K, uint16_t* Wf, hipStream_t st)
              "split_w_frag: K % 16 == 0, 16-B aligned");
   const int n = (int)(K / 16) * 4 * 64;
   hipLaunchKernelGGL(split_w_frag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, W, (int)K, Wf);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_agg_w4(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
+                  int64_t q_rows_cap, const int32_t* loc, const float* wloc, int T, const int* nS,
+                  int64_t n_static, int64_t S_est, const float* Wr, const float* bias, float* y, float* nrm,
+                  float* agg, hipStream_t st) {
+  PS_REQUIRE(agg_w3_supported(d, hid, kA3Out, T), kErrArg, "agg_w4: unsupported shape");
+  PS_REQUIRE(q_rows_cap * hid * 4 < (1LL << 31) && (int64_t)kA3Out * (d + hid) * 4 < (1LL << 31), kErrArg,
+             "agg_w4: q or W too large for 32-bit buffer offsets");
+  PS_REQUIRE(ldh % 4 == 0 && (uintptr_t)h % 16 == 0 && (uintptr_t)q % 16 == 0 && (uintptr_t)agg % 16 == 0 &&
+                 (uintptr_t)y % 16 == 0 && (uintptr_t)Wr % 16 == 0,
+             kErrArg, "agg_w4: 16-B aligned rows required");
+  if (S_est <= 0) return kOk;
+  const char* e = getenv("PINSAGE_AGGW_ROWS");
+  const int rows = e ? std::max(1, atoi(e)) : 24;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int64_t g = std::min<int64_t>(cus, std::max<int64_t>(1, (S_est + rows - 1) / rows));
+  const dim3 gr((unsigned)g), bl(512);
+#define PS_A4(R) \
+  hipLaunchKernelGGL(agg_w4_kernel<R>, gr, bl, 0, st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, Wr, \
+                     bias, y, nrm, agg)
+  PS_A4(4);
+#undef PS_A4
   PS_CHECK_LAUNCH();
   return kOk;
 }

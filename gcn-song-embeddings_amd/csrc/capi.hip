@@ -38,6 +38,10 @@ int launch_set_finalize(unsigned long long*, const unsigned long long*, const un
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int agg_w3_supported(int64_t, int64_t, int64_t, int64_t);
 int launch_split_w_frag(const float*, int64_t, uint16_t*, hipStream_t);
+int launch_reorder_w_frag(const float*, int64_t, float*, hipStream_t);
+int launch_agg_w4(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
+                  const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*,
+                  float*, float*, hipStream_t);
 int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
                   const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
                   float*, float*, hipStream_t);
@@ -507,6 +511,10 @@ int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, in
     set_error("linear_split_b: bad argument");
     return kErrArg;
   }
+  if (ldws != K) {  // pinsage_split_planes writes planes of row stride cols = K, plane stride N*K
+    set_error("linear_split_b: W_planes must come from pinsage_split_planes(W, N, K, ...): ldws == K");
+    return kErrArg;
+  }
   GemmParams p;
   p.M = (int)M;
   p.N = (int)N;
@@ -554,9 +562,17 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
     return kErrArg;
   }
   hipStream_t st = (hipStream_t)stream;
-  PS_TRY(launch_split_w_frag(W, d + hid, W_planes, st));
-  return launch_agg_w3(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows,
-                       n_rows, W_planes, bias, y, norms, agg, st);
+  static const int form = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 2;
+  if (form == 3) {  // the in-wave pipelined form (A/B)
+    PS_TRY(launch_split_w_frag(W, d + hid, W_planes, st));
+    return launch_agg_w3(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows,
+                         n_rows, W_planes, bias, y, norms, agg, st);
+  }
+  // the warp-specialised form: W reordered (fp32, 4 * out * (d + hid) bytes of the scratch)
+  float* Wr = reinterpret_cast<float*>(W_planes);
+  PS_TRY(launch_reorder_w_frag(W, d + hid, Wr, st));
+  return launch_agg_w4(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows, n_rows,
+                       Wr, bias, y, norms, agg, st);
 }
 
 }  // extern "C"

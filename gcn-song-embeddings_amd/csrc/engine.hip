@@ -63,6 +63,10 @@ int launch_agg_w(const float*, int64_t, int, const int32_t*, const float*, int, 
                  float*, hipStream_t);
 int agg_w3_supported(int64_t, int64_t, int64_t, int64_t);
 int launch_split_w_frag(const float*, int64_t, uint16_t*, hipStream_t);
+int launch_reorder_w_frag(const float*, int64_t, float*, hipStream_t);
+int launch_agg_w4(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
+                  const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*,
+                  float*, float*, hipStream_t);
 int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
                   const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
                   float*, float*, hipStream_t);
@@ -140,7 +144,8 @@ struct Engine {
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B);
   // 1: the round-2 fused kernel (fp32 MFMA after the gather); 2 (default): the
-  // pipelined split-bf16 kernel (agg_w3_kernel) where its shape is supported
+  // warp-specialised gather / split-bf16 projection kernel (agg_w4_kernel); 3:
+  // the in-wave pipelined form (agg_w3_kernel), where their shapes are supported
   int fused_aggw = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 2;
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
@@ -530,7 +535,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
   auto use_aggw3 = [&](const LayerBuf& lb) {
-    return E.fused_aggw == 2 && agg_w3_supported(lb.d, c.hid, c.out, T) &&
+    return (E.fused_aggw == 2 || E.fused_aggw == 3) && agg_w3_supported(lb.d, c.hid, c.out, T) &&
            lb.N.cap * c.hid * 4 < (1LL << 31);
   };
   // the W weights' bf16 planes for the aggregation + projection kernel (the
@@ -540,7 +545,10 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     LayerBuf& lb = E.L[(size_t)l];
     if (!use_aggw3(lb)) continue;
     Timed ts(E, lname("fwd.w_split", l), st);
-    PS_TRY(launch_split_w_frag(E.params + lb.pWw, lb.d + c.hid, at<uint16_t>(ws, lb.wsplit), st));
+    if (E.fused_aggw == 3)
+      PS_TRY(launch_split_w_frag(E.params + lb.pWw, lb.d + c.hid, at<uint16_t>(ws, lb.wsplit), st));
+    else
+      PS_TRY(launch_reorder_w_frag(E.params + lb.pWw, lb.d + c.hid, at<float>(ws, lb.wsplit), st));
   }
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
@@ -583,11 +591,17 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     if (use_aggw3(lb)) {
       // aggregation pipelined with the split-bf16 projection, bias, lrelu, L2 norm
       Timed taw(E, lname("fwd.aggw", l), st);
-      PS_TRY(launch_agg_w3(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
-                           lb.N.cap, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0,
-                           lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap,
-                           at<uint16_t>(ws, lb.wsplit), E.params + lb.pWb, at<float>(ws, lb.y),
-                           at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
+      const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
+      if (E.fused_aggw == 3)
+        PS_TRY(launch_agg_w3(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
+                             lb.N.cap, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0, S_est,
+                             at<uint16_t>(ws, lb.wsplit), E.params + lb.pWb, at<float>(ws, lb.y),
+                             at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
+      else
+        PS_TRY(launch_agg_w4(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
+                             lb.N.cap, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0, S_est,
+                             at<float>(ws, lb.wsplit), E.params + lb.pWb, at<float>(ws, lb.y),
+                             at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
       continue;
     }
     if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {

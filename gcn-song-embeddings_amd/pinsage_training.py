@@ -280,6 +280,7 @@ class _FusedStep:
         self.parity = 0
         self.ahead_hits = 0
         # in-context GEMM tuner (see _autotune); PINSAGE_AUTOTUNE=0 keeps the size model
+        # (deterministic: the same choices, so the same summation orders, on every run)
         self.autotune = os.environ.get("PINSAGE_AUTOTUNE", "1") != "0"
         self.tuned_choices = None
 
@@ -458,8 +459,15 @@ class _FusedStep:
         order).  The probes run before the step's own forward (the caller runs
         the real step afterwards, so its outputs, gradients and workspace are
         the step's): this step's frontier, layers, loss and backward WITHOUT
-        the optimizer -- parameters and Adam state are untouched, and every
-        choice computes the same products (speed only)."""
+        the optimizer -- parameters and Adam state are untouched.
+
+        Reproducibility: every choice computes the same products, but split-K
+        counts and stream-K change the fp32 summation order of a weight
+        gradient, and which candidate wins depends on timing noise -- two runs
+        can therefore differ at fp32 rounding level.  The choices are recorded
+        (``tuned_choices``; bench.py prints them as "gemm_choices"), and
+        PINSAGE_GEMM_CHOICES=<that json> replays them; PINSAGE_AUTOTUNE=0
+        keeps the deterministic size model instead of tuning."""
         e = self.runner.engine
         L = nat.lib()
         sites = self._gemm_sites()
@@ -585,12 +593,28 @@ class _FusedStep:
         return nxt[rank * B:(rank + 1) * B]
 
     def __call__(self, batch):
+        """One train step; for the caller it is optimizer.step(): the step's
+        Adam update runs inside the graph, and around it the optimizer's (and
+        the global) step pre- / post-hooks fire and torch's bookkeeping advances
+        (``_opt_called``, so an LR scheduler sees optimizer.step() before its own
+        step, as in pinsage_training.py:188-191, 256)."""
+        from itertools import chain
+        import torch.optim.optimizer as _topt
+        opt = self.tr.optimizer
+        pre = list(chain(_topt._global_optimizer_pre_hooks.values(), opt._optimizer_step_pre_hooks.values()))
+        for hook in pre:
+            if hook(opt, (opt,), {}) is not None:
+                raise RuntimeError("the fused train step cannot apply an optimizer pre-hook's new arguments")
         if _HOST_T is not None:
             t0 = time.perf_counter()
             out = self._call(batch)
             _HOST_T["call"] = _HOST_T.get("call", 0.0) + time.perf_counter() - t0
-            return out
-        return self._call(batch)
+        else:
+            out = self._call(batch)
+        opt._opt_called = True
+        for hook in chain(opt._optimizer_step_post_hooks.values(), _topt._global_optimizer_post_hooks.values()):
+            hook(opt, (opt,), {})
+        return out
 
     def _call(self, batch):
         tr = self.tr
@@ -744,6 +768,20 @@ class PinSage:
             return d.get_rank(), d.get_world_size()
         return 0, 1
 
+    def _average_param_grads(self):
+        """Data parallel: every rank's parameter gradients become their mean over
+        the process group (ONE all-reduce of the flattened gradients), so the
+        replicas take the same optimizer step."""
+        rank, world = self._dp()
+        if world <= 1:
+            return
+        params = [p for p in self.model.parameters() if p.grad is not None]
+        flat_g = average_gradients(torch.cat([p.grad.reshape(-1) for p in params]))
+        off = 0
+        for p in params:
+            p.grad.copy_(flat_g[off:off + p.numel()].view(p.shape))
+            off += p.numel()
+
     def next_batch(self):
         """Sample this rank's slice of the global batch (same draws on every rank)."""
         rank, world = self._dp()
@@ -781,6 +819,7 @@ class PinSage:
         loss = max_margin_loss(h_q, h_pos, h_neg, self.margin)
         self.optimizer.zero_grad()
         loss.backward()
+        self._average_param_grads()
         self.optimizer.step()
         norm = torch.nn.functional.normalize
         f = self.features
@@ -844,13 +883,7 @@ class PinSage:
             d = torch.where((first[su] == j // m)[:, None], D[su], torch.zeros((), device=dev))
             y = model(self.features, u)
             torch.autograd.backward([y], [d])
-        rank, world = self._dp()
-        if world > 1:
-            flat_g = average_gradients(torch.cat([p.grad.reshape(-1) for p in params]))
-            off = 0
-            for p in params:
-                p.grad.copy_(flat_g[off:off + p.numel()].view(p.shape))
-                off += p.numel()
+        self._average_param_grads()
         self.optimizer.step()
         norm = torch.nn.functional.normalize
         f = self.features

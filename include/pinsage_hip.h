@@ -186,7 +186,8 @@ int pinsage_split_planes(const float* W, int64_t rows, int64_t cols, int64_t ldw
                          void* stream);
 /* pinsage_linear's product (K-major A rows gathered by a_idx, W[N][K]) under
  * split-bf16 arithmetic with W given ALSO as its pre-split planes (from
- * pinsage_split_planes, row stride ldws elements): the kernel converts A only.
+ * pinsage_split_planes(W, N, K, ...): row stride ldws == K elements, plane
+ * stride N*K; other strides are rejected): the kernel converts A only.
  * Bitwise equal to the in-register split for cfg 0 and 3 (other cfg values,
  * -1 included, may run the in-register form; the result is the same). */
 int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
@@ -330,7 +331,12 @@ int pinsage_engine_set_fork(pinsage_engine* e, void* ws_next, const int64_t* ids
                             int64_t n_ids, void* side_stream);
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
                                  void* stream);
-/* max_margin_loss + monitors on the last forward of a [B][3] batch; writes dZ.
+/* max_margin_loss + monitors on the last forward of a [B][3] batch.  It
+ * accumulates the loss cotangent into the workspace's per-row gradient
+ * accumulators (the head backward forms dZ from them and re-zeroes them), so a
+ * pinsage_engine_backward / _backward_adam MUST follow every loss call on a
+ * workspace before its next loss call (an eval-only loss would leave them
+ * dirty for the next step).
  * The monitor kernel (loss / node-feature loss / variance scalars, on an engine
  * side stream, dependent on this loss) is enqueued by the next engine call
  * that enqueues work (normally the backward, right behind its first kernel;

@@ -189,3 +189,62 @@ def test_precompute_sharded_over_ranks_matches_single_process(mode, n_items):
     for _, w, nb, st in res:
         assert np.array_equal(w, w1.numpy()) and np.array_equal(nb, nb1.numpy())
         assert np.array_equal(st, st1)
+
+
+def _fly_worker(rank, world, port, tmp, out_q):
+    """Two training steps with an on-the-fly model (pinsage_model.py:142-154):
+    each rank samples and trains its own slice, so the replicas stay identical
+    only if the gradients are averaged before the optimizer step."""
+    import sys
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pinsage_model as pm
+        import pinsage_training as pt
+        g, feats, pos = _problem(tmp)
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            torch.manual_seed(5)
+            tr = pt.PinSage(g, N_TRACKS, feats.cuda(), pos, log=False, load_save=False)
+            torch.manual_seed(7)
+            tr.model = pm.PinSageModel(g, N_TRACKS, 2, tr.dimensions, 200, 0.85, 3, None)
+            tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+            tr.batch_size = 8
+            torch.manual_seed(11 + rank)  # the ranks' walks differ: different gradients
+            for _ in range(2):
+                batch, _ = tr.next_batch()
+                tr.train_batch(batch)
+            torch.cuda.synchronize()
+            out_q.put((rank, {k: v.detach().cpu().numpy().copy() for k, v in tr.model.state_dict().items()}))
+        finally:
+            os.chdir(cwd)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_on_the_fly_replicas_stay_identical():
+    tmp = tempfile.mkdtemp()
+    import pinsage_model as pm
+    g, _, _ = _problem(tmp)
+    torch.manual_seed(0)
+    pm.precompute_neighborhoods_topt(g, N_TRACKS, pm.DEF_HOPS, pm.DEF_ALPHA, pm.DEF_T_PRECOMP,
+                                     g.nbhds_path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fly_worker, args=(r, 2, port, tmp, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for k in res[0]:
+        assert np.array_equal(res[0][k], res[1][k]), k

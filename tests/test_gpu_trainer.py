@@ -152,3 +152,31 @@ def test_train_after_large_forward_matches_oracle():
                     tr.model.train()
         finally:
             os.chdir(cwd)
+
+
+def test_fused_step_is_an_optimizer_step_for_hooks_and_scheduler():
+    """The fused step (Adam inside the step graph) behaves like the reference's
+    optimizer.step() (pinsage_training.py:188-191) to callers: step pre- and
+    post-hooks fire once per step, in order, and the epoch's scheduler.step()
+    (:256) does not warn that it ran before optimizer.step()."""
+    import warnings
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            tr.epochs, tr.b_per_e, tr.batch_size = 1, 4, 32
+            events = []
+            tr.optimizer.register_step_pre_hook(lambda opt, a, k: events.append("pre"))
+            tr.optimizer.register_step_post_hook(lambda opt, a, k: events.append("post"))
+            torch.manual_seed(2)
+            with warnings.catch_warnings(record=True) as caught:
+                warnings.simplefilter("always")
+                tr.train()
+            assert not [w for w in caught if "lr_scheduler.step()" in str(w.message)]
+            assert events == ["pre", "post"] * tr.b_per_e
+        finally:
+            os.chdir(cwd)
