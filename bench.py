@@ -269,6 +269,10 @@ def main():
     ap.add_argument("--precompute-rng", default="philox", choices=["philox", "mt19937"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: per-GPU batch fixed; strong: global batch fixed (per-GPU = global / N)")
+    ap.add_argument("--sampling", default="table", choices=["table", "fly"],
+                    help="table: the precomputed top-T neighbourhoods (the reference's default path); "
+                         "fly: every call walks its nodes' neighbourhoods inside the step "
+                         "(relevant_nodes_per_layer, pinsage_model.py:142-154), RNG per --precompute-rng")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.scale != 1.0:
@@ -316,6 +320,14 @@ def main():
             tr.model = pm.PinSageModel(g, tr.n, tr.n_layers, tr.dimensions, tr.n_hops, tr.alpha, tr.T, tr.nbhds)
             tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
             tr.scheduler = torch.optim.lr_scheduler.ExponentialLR(tr.optimizer, tr.decay)
+        if args.sampling == "fly":
+            import pinsage_model as pm
+            pm.set_rng_mode(args.precompute_rng)
+            torch.manual_seed(0)
+            tr.model = pm.PinSageModel(g, tr.n, tr.n_layers, tr.dimensions, tr.n_hops, tr.alpha, tr.T, None)
+            tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+            tr.scheduler = torch.optim.lr_scheduler.ExponentialLR(tr.optimizer, tr.decay)
+            cfg["workload"] += " [sampling on the fly: walks + top-T per layer inside every step]"
         tr.batch_size = cfg["batch"]
         tr.micro_batch = micro
         torch.manual_seed(1234)  # same global batches on every rank
@@ -437,7 +449,7 @@ def main():
                    "memberships": cfg["memberships"], "d_in": cfg["d_in"], "hidden": hid, "out": 128,
                    "n_layers": cfg["n_layers"], "fanout": T, "batch_per_gpu": cfg["batch"],
                    "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
-                   "batch_rng": "mt19937 (reference-exact)"},
+                   "batch_rng": "mt19937 (reference-exact)", "sampling": args.sampling},
         "roofline": {"bound": "mfma", "kernel": "fwd.q_gemm.l0 (gather + Q projection on MFMA)",
                      "arithmetic": gemm_arith,
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",

@@ -77,6 +77,10 @@ _SIGS = {
     "pinsage_weighted_agg": (ctypes.c_int, [vp, i64, vp, vp, i64, i64, vp, vp]),
     "pinsage_conv_agg_project": (ctypes.c_int, [vp, i64, i64, vp, vp, i64, i64, vp, vp, i64, i64, vp, vp,
                                                 i64, vp, vp, vp, vp, vp]),
+    "pinsage_gather_rows": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, vp, i64, vp]),
+    "pinsage_concat_linear_l2norm": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, i64, i64, vp, vp, i64, vp, vp,
+                                                    vp]),
+    "pinsage_norm_lrelu_backward": (ctypes.c_int, [vp, vp, vp, i64, i64, vp, vp]),
     "pinsage_gemm_set_prec": (ctypes.c_int, [ctypes.c_int]),
     "pinsage_gemm_get_prec": (ctypes.c_int, []),
     "pinsage_split_planes": (ctypes.c_int, [vp, i64, i64, i64, vp, vp]),

@@ -24,6 +24,7 @@
 
 #include "bf16split.h"
 #include "common.h"
+#include "lds_dma.h"
 
 namespace ps {
 
@@ -864,6 +865,242 @@ __global__ __launch_bounds__(512, 2) void agg_w4_kernel(
     }
     __syncthreads();  // red (the ring) and the slot tables are reused by the next tile
   }
+}
+
+// ---------------------------------------------------------------------------
+// Form 5: warp-specialised, the gather on LDS-DMA.  One 512-thread workgroup
+// per CU owns a contiguous row range, in tiles of <= 32 rows.  Waves 0-3
+// (producers) stream slot rows of q HBM -> LDS with global_load_lds_dwordx4
+// (a unit = one 128-B chunk of 32 rows = four wave-instructions of 8 rows x
+// 128 B, k5RD units in flight per producer ~ 64 KiB per CU) and retire them with
+// counted s_waitcnt vmcnt: the compiler's waitcnt pass never sees these loads,
+// so it cannot drain the queue at control-flow joins (the register-load forms
+// 3 and 4 compiled to vmcnt(0) / vmcnt(1) waits between nearly every unit).
+// Producer j sums chunk c = 4 r + j of the aggregate over the slots in order
+// t = 0, 1, ... (agg_kernel's fma chain), writes it to agg (the W gradient
+// reads it) and into the round's fp32 A image; the self rows' chunk 4 r + j
+// (k in [0, d)) goes through the same ring.  Waves 4-7 (consumers) own 32
+// output columns each over all of K: per round, 16 k-steps of
+// v_mfma_f32_32x32x16_bf16 x 6 (A and W split into bf16 hi / mid / lo in
+// registers; W fragments from L2 prefetched 8 steps ahead).  A images are
+// double-buffered per round, one s_barrier per round.  Epilogue: bias,
+// LeakyReLU and the row L2 norm (pinsage_model.py:208-211).
+int agg_w3_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
+
+constexpr int k5Rows = 32;
+constexpr int k5RD = 4;                 // units in flight per producer
+constexpr int k5Unit = k5Rows * 128;    // bytes per unit
+constexpr int k5AS = 36;                // A image row stride (floats): conflict-free b128 reads
+constexpr int k5ImgF = k5Rows * k5AS;   // floats per A image
+constexpr int k5TS = kA3TMax + 4;       // slot-table row stride (words)
+constexpr int k5WP = 8;                 // W fragment prefetch distance (16-k steps)
+
+__device__ __forceinline__ void k5_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+__global__ __launch_bounds__(512, 1) void agg_w5_kernel(
+    const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
+    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
+    const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
+    const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y,
+    float* __restrict__ nrm_out, float* __restrict__ agg) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[4 * k5RD * k5Unit];  // 64 KiB
+  __shared__ __attribute__((aligned(16))) float aimg[2 * 8 * k5ImgF];            // 72 KiB
+  __shared__ int sLoc[k5Rows * k5TS];
+  __shared__ float sW[k5Rows * k5TS];
+  __shared__ int sSelf[k5Rows];
+  float* red = reinterpret_cast<float*>(ring);  // [32][128] in the epilogue
+  const unsigned ring_lds = (unsigned)(size_t)((__attribute__((address_space(3))) unsigned char*)ring);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = wave < 4;
+  const int pj = wave & 3;
+  const int rs = lane >> 3, kq = lane & 7;      // producer lane: rows rs + 8 j, floats 4 kq ..
+  const int row = lane & 31, half = lane >> 5;  // consumer lane: MFMA row / k half
+  const int K = d + hid;
+  const int64_t F = nS ? (int64_t)*nS : n_static;
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / G, re = F * (b + 1) / G;
+  const int64_t len = re - rb;
+  const int ntile = (int)((len + k5Rows - 1) / k5Rows);
+  const int nca = hid >> 5, ncs = d >> 5;
+  const int nr = max((nca + 3) >> 2, (ncs + 3) >> 2);  // rounds
+
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int64_t r0 = rb + len * tile / ntile;
+    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
+    // padded rows read the tile's first row (a cache hit) with weight 0
+    for (int i = tid; i < k5Rows * T; i += 512) {
+      const int r = i / T, t = i - r * T;
+      const int rr = r < nrows ? r : 0;
+      sLoc[r * k5TS + t] = loc[(r0 + rr) * T + t];
+      sW[r * k5TS + t] = r < nrows ? wloc[(r0 + rr) * T + t] : 0.f;
+    }
+    if (tid < k5Rows) sSelf[tid] = self_src[r0 + (tid < nrows ? tid : 0)];
+    __syncthreads();
+
+    if (producer) {
+      // this producer's units, round by round: T aggregate slots of chunk
+      // 4 r + pj (if < nca), then the self chunk 4 r + pj (if < ncs)
+      auto n_in = [&](int r) { return (4 * r + pj < nca ? T : 0) + (4 * r + pj < ncs ? 1 : 0); };
+      int total = 0;
+      for (int r = 0; r < nr; ++r) total += n_in(r);
+      int ir = 0, ik = 0;  // issue cursor (round, position in round)
+      auto issue_next = [&](int slot) __attribute__((always_inline)) {
+        while (ik >= n_in(ir)) {
+          ++ir;
+          ik = 0;
+        }
+        const int c = 4 * ir + pj;
+        const bool is_agg = 4 * ir + pj < nca && ik < T;
+        const unsigned dst = ring_lds + (unsigned)(pj * k5RD + slot) * k5Unit;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rw = rs + 8 * j;
+          const float* src = is_agg ? q + (int64_t)sLoc[rw * k5TS + ik] * hid + 32 * c + 4 * kq
+                                    : h + (int64_t)sSelf[rw] * ldh + 32 * c + 4 * kq;
+          glds16(src, dst + j * 1024);
+        }
+        ++ik;
+      };
+      for (int u = 0; u < k5RD && u < total; ++u) issue_next(u);
+      float4 x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      int s = 0;
+      for (int r = 0; r < nr; ++r) {
+        float* img = aimg + ((r & 1) * 8) * k5ImgF;
+        const int na = 4 * r + pj < nca ? T : 0, nin = n_in(r);
+        for (int k = 0; k < nin; ++k, ++s) {
+          wait_stage<4, k5RD - 1>(min(k5RD - 1, total - 1 - s));
+          const unsigned char* src = ring + (pj * k5RD + s % k5RD) * k5Unit + lane * 16;
+          float4 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const float4*>(src + j * 1024);
+          if (k < na) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a3_fma4(sW[(rs + 8 * j) * k5TS + k], v[j], x[j]);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+          if (s + k5RD < total) issue_next(s % k5RD);
+          if (k == na - 1) {  // aggregate chunk complete: agg out, A image
+            const int c = 4 * r + pj;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (rs + 8 * j < nrows)
+                *reinterpret_cast<float4*>(agg + (r0 + rs + 8 * j) * hid + 32 * c + 4 * kq) = x[j];
+              *reinterpret_cast<float4*>(img + pj * k5ImgF + (rs + 8 * j) * k5AS + 4 * kq) = x[j];
+              x[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          } else if (k >= na) {  // self chunk
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              *reinterpret_cast<float4*>(img + (4 + pj) * k5ImgF + (rs + 8 * j) * k5AS + 4 * kq) = v[j];
+          }
+        }
+        k5_barrier();  // round r's images are complete
+      }
+    } else {
+      // consumer pj: output columns 32 pj .. 32 pj + 31 over all of K.  Step i of
+      // round r: aggregate chunk 4 r + (i >> 1) % 4 (i < 8) or self chunk (i >= 8),
+      // 16-k half i & 1
+      a3_f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      auto kk_of = [&](int r, int i) -> int {  // global 16-k step, clamped into range
+        const int c = 4 * r + ((i >> 1) & 3);
+        const int kk = i < 8 ? (d >> 4) + 2 * c + (i & 1) : 2 * c + (i & 1);
+        return min(kk, (K >> 4) - 1);
+      };
+      const float* wrow = W + (int64_t)(32 * pj + row) * K + 8 * half;
+      float4 bq[k5WP][2];
+#pragma unroll
+      for (int i = 0; i < k5WP; ++i) {
+        const float* p = wrow + 16 * kk_of(0, i);
+        bq[i][0] = *reinterpret_cast<const float4*>(p);
+        bq[i][1] = *reinterpret_cast<const float4*>(p + 4);
+      }
+      for (int r = 0; r < nr; ++r) {
+        k5_barrier();  // round r's images are complete
+        const float* img = aimg + ((r & 1) * 8) * k5ImgF;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = 4 * r + ((i >> 1) & 3);
+          const bool valid = i < 8 ? c < nca : c < ncs;
+          const float4 b0 = bq[i % k5WP][0], b1 = bq[i % k5WP][1];
+          {  // refill the slot with the step k5WP ahead (into the next round for the last ones)
+            const int rn = i + k5WP < 16 ? r : r + 1, in = (i + k5WP) & 15;
+            const float* p = wrow + 16 * kk_of(rn < nr ? rn : r, in);
+            bq[i % k5WP][0] = *reinterpret_cast<const float4*>(p);
+            bq[i % k5WP][1] = *reinterpret_cast<const float4*>(p + 4);
+          }
+          if (valid) {
+            const float* ar = img + (i < 8 ? ((i >> 1) & 3) : 4 + ((i >> 1) & 3)) * k5ImgF + row * k5AS +
+                              16 * (i & 1) + 8 * half;
+            bf16x8 aH, aM, aL, bH, bM, bL;
+            split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), aH, aM, aL);
+            split3(b0, b1, bH, bM, bL);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
+          }
+        }
+      }
+      // every producer passed its last round's barrier: the ring is idle
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[((e & 3) + 8 * (e >> 2) + 4 * half) * kA3Out + 32 * pj + row] = acc[e];
+    }
+    __syncthreads();
+    {
+      const int er = tid >> 4, c8 = (tid & 15) * 8;
+      float v[8];
+      float s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = lrelu(red[er * kA3Out + c8 + e] + bias[c8 + e]);
+        s2 += v[e] * v[e];
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+      const float nrm = sqrtf(s2);
+      if (er < nrows) {
+        float* dst = y + (r0 + er) * kA3Out + c8;
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4] / nrm, v[5] / nrm, v[6] / nrm, v[7] / nrm);
+        if ((tid & 15) == 0 && nrm_out) nrm_out[r0 + er] = nrm;
+      }
+    }
+    __syncthreads();  // red (the ring) and the slot tables are reused by the next tile
+  }
+}
+
+int launch_agg_w5(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
+                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_est,
+                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st) {
+  PS_REQUIRE(agg_w3_supported(d, hid, kA3Out, T), kErrArg, "agg_w5: unsupported shape");
+  PS_REQUIRE(ldh % 4 == 0 && (uintptr_t)h % 16 == 0 && (uintptr_t)q % 16 == 0 && (uintptr_t)agg % 16 == 0 &&
+                 (uintptr_t)y % 16 == 0 && (uintptr_t)W % 16 == 0,
+             kErrArg, "agg_w5: 16-B aligned rows required");
+  if (S_est <= 0) return kOk;
+  static int rows_per_block = -1;
+  if (rows_per_block < 0) {
+    const char* e = getenv("PINSAGE_AGGW_ROWS");
+    rows_per_block = e ? std::max(1, atoi(e)) : 16;
+  }
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int64_t g = std::min<int64_t>(cus, std::max<int64_t>(1, (S_est + rows_per_block - 1) / rows_per_block));
+  hipLaunchKernelGGL(agg_w5_kernel, dim3((unsigned)g), dim3(512), 0, st, h, ldh, d, self_src, q, hid, loc, wloc,
+                     T, nS, n_static, W, bias, y, nrm, agg);
+  PS_CHECK_LAUNCH();
+  return kOk;
 }
 
 int launch_reorder_w_frag(const float* W, int64_t K, float* Wr, hipStream_t st) {

@@ -42,11 +42,17 @@ int launch_reorder_w_frag(const float*, int64_t, float*, hipStream_t);
 int launch_agg_w4(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
                   const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*,
                   float*, float*, hipStream_t);
+int launch_agg_w5(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*, const float*, int,
+                  const int*, int64_t, int64_t, const float*, const float*, float*, float*, float*, hipStream_t);
 int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
                   const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
                   float*, float*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
+int launch_gather_rows(const float*, int64_t, int64_t, int, const int64_t*, int64_t, float*, int64_t,
+                       hipStream_t);
+int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t, float*, float*,
+                          int, const int*, int*, int64_t, hipStream_t);
 int64_t knn_scratch_bytes(int64_t, int64_t);
 int launch_knn_cosine(const float*, int64_t, int64_t, int64_t, const int64_t*, int64_t, int64_t,
                       float, void*, int64_t, float*, int64_t*, int*, hipStream_t);
@@ -562,8 +568,13 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
     return kErrArg;
   }
   hipStream_t st = (hipStream_t)stream;
-  static const int form = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 2;
-  if (form == 3) {  // the in-wave pipelined form (A/B)
+  // the in-wave pipelined form (C2 layer-0 shape: 44.0 us incl. the split vs 49.5
+  // for the warp-specialised form, tools/aggw_bench.py); PINSAGE_FUSED_AGGW=2 for that one
+  const int form = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 3;
+  if (form == 5)
+    return launch_agg_w5(h, ldh, (int)d, self_src, q, (int)hid, loc, w, (int)T, nullptr, n_rows, n_rows, W, bias,
+                         y, norms, agg, st);
+  if (form != 2) {
     PS_TRY(launch_split_w_frag(W, d + hid, W_planes, st));
     return launch_agg_w3(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows,
                          n_rows, W_planes, bias, y, norms, agg, st);
@@ -573,6 +584,56 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
   PS_TRY(launch_reorder_w_frag(W, d + hid, Wr, st));
   return launch_agg_w4(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows, n_rows,
                        Wr, bias, y, norms, agg, st);
+}
+
+int pinsage_gather_rows(const float* h, int64_t ldh, int64_t n_h, int64_t d, const int64_t* idx, int64_t n,
+                        float* out, int64_t ldo, void* stream) {
+  if (d < 0 || d > INT32_MAX || n < 0 || n_h < 0 || ldh < d || ldo < d) {
+    set_error("gather_rows: bad sizes");
+    return kErrArg;
+  }
+  return launch_gather_rows(h, ldh, n_h, (int)d, idx, n, out, ldo, (hipStream_t)stream);
+}
+
+int pinsage_concat_linear_l2norm(const float* h, int64_t ldh, const int32_t* self_idx, int64_t n, int64_t d,
+                                 const float* agg, int64_t ld_agg, int64_t hid, const float* W,
+                                 const float* bias, int64_t out, float* y, float* norms, void* stream) {
+  if (n < 0 || n > INT32_MAX || d <= 0 || hid <= 0 || d + hid > INT32_MAX || out <= 0 || out > 128 ||
+      ldh < d || ld_agg < hid) {
+    set_error("concat_linear_l2norm: bad sizes (0 < out <= 128)");
+    return kErrArg;
+  }
+  if (n == 0) return kOk;
+  GemmParams p;
+  p.M = (int)n;
+  p.N = (int)out;
+  p.K = (int)(d + hid);
+  p.a = h;
+  p.lda = ldh;
+  p.a_idx = self_idx;
+  p.K1 = (int)d;
+  p.a2 = agg;
+  p.lda2 = ld_agg;
+  p.b = W;
+  p.ldb = d + hid;
+  p.c = y;
+  p.ldc = out;
+  p.bias = bias;
+  p.epi = kEpiL2Norm;
+  p.norms = norms;
+  p.stream_k = 0;
+  return launch_gemm(p, (hipStream_t)stream);
+}
+
+int pinsage_norm_lrelu_backward(const float* y, const float* norms, const float* dy, int64_t n, int64_t out,
+                                float* dp, void* stream) {
+  if (n < 0 || out <= 0 || out > INT32_MAX) {
+    set_error("norm_lrelu_backward: bad sizes");
+    return kErrArg;
+  }
+  if (n == 0) return kOk;
+  return launch_norm_lrelu_bwd(y, norms, dy, (int)out, nullptr, n, dp, nullptr, 0, nullptr, nullptr, 0,
+                               (hipStream_t)stream);
 }
 
 }  // extern "C"

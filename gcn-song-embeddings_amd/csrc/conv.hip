@@ -641,6 +641,7 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
                                                              const float* __restrict__ nrm,
                                                              const float* __restrict__ dy, int n,
                                                              const int* __restrict__ nrows,
+                                                             int64_t n_static,
                                                              float* __restrict__ dp,
                                                              float* __restrict__ z, int z_n,
                                                              const int* __restrict__ z_rows,
@@ -653,7 +654,7 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
   }
   if (zi)
     for (int64_t i = gt; i < zi_n; i += gs) zi[i] = 0;
-  const int64_t R = *nrows;
+  const int64_t R = nrows ? (int64_t)*nrows : n_static;
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -992,6 +993,30 @@ __global__ void gather_out_kernel(const float* __restrict__ Z, int d, const int3
   }
 }
 
+// get_embeddings' row gather h[idx, :d] (pinsage_model.py:21-23) as an op:
+// one wave per output row, float4 columns when rows are 16-B aligned.  Ids
+// outside [0, n_h) give a zero row (the caller validates; the reference raises).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ h, int64_t ldh,
+                                                          int64_t n_h, int d, const int64_t* __restrict__ idx,
+                                                          int64_t n, float* __restrict__ out, int64_t ldo,
+                                                          bool vec) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += nw) {
+    const int64_t s = idx[r];
+    const bool ok = s >= 0 && s < n_h;
+    const float* src = h + (ok ? s : 0) * ldh;
+    float* dst = out + r * ldo;
+    if (vec) {
+      for (int c = lane; c < (d >> 2); c += 64)
+        reinterpret_cast<float4*>(dst)[c] =
+            ok ? reinterpret_cast<const float4*>(src)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      for (int c = lane; c < d; c += 64) dst[c] = ok ? src[c] : 0.f;
+    }
+  }
+}
+
 // one call: G[r] = sum of dout rows at positions of node r, K[r] = multiplicity
 __global__ void dout_accum_kernel(const float* __restrict__ dout, int d,
                                   const int32_t* __restrict__ pr, int64_t n, float* __restrict__ G,
@@ -1101,6 +1126,17 @@ int launch_gather_out(const float* Z, int d, const int32_t* pr, int64_t n, float
   if (n <= 0) return kOk;
   hipLaunchKernelGGL(gather_out_kernel, dim3(grid_for(n * d, 256)), dim3(256), 0, st, Z, d, pr, n,
                      out);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+int launch_gather_rows(const float* h, int64_t ldh, int64_t n_h, int d, const int64_t* idx, int64_t n,
+                       float* out, int64_t ldo, hipStream_t st) {
+  PS_REQUIRE(d >= 0 && n >= 0 && ldh >= d && ldo >= d, kErrArg, "gather_rows: bad sizes");
+  if (n == 0 || d == 0) return kOk;
+  const bool vec = d % 4 == 0 && ldh % 4 == 0 && ldo % 4 == 0 && (uintptr_t)h % 16 == 0 && (uintptr_t)out % 16 == 0;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n * 64, 256, 8192)), dim3(256), 0, st, h, ldh, n_h, d, idx,
+                     n, out, ldo, vec);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -1261,7 +1297,7 @@ int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int
                           const int* nrows, int64_t max_rows, float* dp, float* z, int z_n,
                           const int* z_rows, int* zi, int64_t zi_n, hipStream_t st) {
   hipLaunchKernelGGL(norm_lrelu_bwd_kernel, dim3(grid_for(max_rows * 64, 256, 4096)), dim3(256), 0,
-                     st, y, nrm, dy, n, nrows, dp, z, z_n, z_rows, zi, zi_n);
+                     st, y, nrm, dy, n, nrows, max_rows, dp, z, z_n, z_rows, zi, zi_n);
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -67,6 +67,8 @@ int launch_reorder_w_frag(const float*, int64_t, float*, hipStream_t);
 int launch_agg_w4(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
                   const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*,
                   float*, float*, hipStream_t);
+int launch_agg_w5(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*, const float*, int,
+                  const int*, int64_t, int64_t, const float*, const float*, float*, float*, float*, hipStream_t);
 int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
                   const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
                   float*, float*, hipStream_t);
@@ -143,10 +145,12 @@ struct Engine {
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B);
-  // 1: the round-2 fused kernel (fp32 MFMA after the gather); 2 (default): the
+  // 1 (default): the round-2 fused kernel (fp32 MFMA after the gather); 2: the
   // warp-specialised gather / split-bf16 projection kernel (agg_w4_kernel); 3:
-  // the in-wave pipelined form (agg_w3_kernel), where their shapes are supported
-  int fused_aggw = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 2;
+  // the in-wave pipelined form (agg_w3_kernel), where their shapes are supported.
+  // Measured in the C2 step (bench.py, one box): 1: layer 0 41.5 us, layer 1
+  // 22.9 us, 0.458 ms/step; 2: 48.2 / 31.3 us, 0.476 ms; 3: 39.7 / 30.3 us, 0.470 ms.
+  int fused_aggw = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 1;
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
   bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
@@ -538,6 +542,9 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     return (E.fused_aggw == 2 || E.fused_aggw == 3) && agg_w3_supported(lb.d, c.hid, c.out, T) &&
            lb.N.cap * c.hid * 4 < (1LL << 31);
   };
+  auto use_aggw5 = [&](const LayerBuf& lb) {
+    return E.fused_aggw == 5 && agg_w3_supported(lb.d, c.hid, c.out, T);
+  };
   // the W weights' bf16 planes for the aggregation + projection kernel (the
   // parameters change every step: split once per forward, off the chain's
   // inputs -- nothing here depends on the frontier)
@@ -579,7 +586,9 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     }
     {
       Timed tt(E, lname("fwd.q_gemm", l), st);
-      with_sk(E, ws, q);
+      // the plane-reading tile is pinned bitwise to the in-register split for
+      // whole-tile schedules only (tests/test_gpu_gemm.py): no stream-K with it
+      if (!q.b_split) with_sk(E, ws, q);
       apply_choice(E, lname("fwd.q_gemm", l), q);
       PS_TRY(launch_gemm(q, st));
     }
@@ -587,6 +596,16 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(ensure_streams(E));
       PS_TRY(dep(E, st, E.fork.stream));
       PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
+    }
+    if (use_aggw5(lb)) {
+      // LDS-DMA gather warp-specialised against the split-bf16 projection, bias, lrelu, L2 norm
+      Timed taw(E, lname("fwd.aggw", l), st);
+      const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
+      PS_TRY(launch_agg_w5(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
+                           at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0, S_est,
+                           E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y), at<float>(ws, lb.nrm),
+                           at<float>(ws, lb.agg), st));
+      continue;
     }
     if (use_aggw3(lb)) {
       // aggregation pipelined with the split-bf16 projection, bias, lrelu, L2 norm

@@ -1,9 +1,13 @@
 """torch.ops.pinsage: the hot path's kernels as PyTorch-ROCm operators.
 
 ``libpinsage_torch.so`` (csrc/torch_ops.cpp, built in-tree by csrc/Makefile)
-registers the schemas of SURVEY.md §8(b2) -- ppr_topk, frontier, linear,
-gemm, weighted_agg (+ weighted_agg_backward), segment_wmean -- on the HIP
-device, each calling libpinsage_hip.so's C-ABI on the current stream.  This
+registers the schemas of SURVEY.md §8(b2) -- walk, ppr_topk, frontier,
+gather_rows / scatter_add_rows, linear, concat_linear_lrelu_l2norm (+
+norm_lrelu_backward), gemm, weighted_agg (+ weighted_agg_backward),
+segment_wmean -- on the HIP device, each calling libpinsage_hip.so's C-ABI on
+the current stream.  walk / ppr_topk take rng_mode "mt19937" (the reference's
+own draws from torch's global generator, advanced as the reference advances
+it) or "philox" (seed, offset, src_base: counter-based, generator untouched).  This
 module loads it and registers the autograd formulas of the differentiable ops
 (torch.library.register_autograd), so ``conv_layer`` below -- the standalone
 ConvLayer forward (pinsage_model.py:189-212) -- trains through torch autograd
@@ -84,9 +88,76 @@ def _agg_backward(ctx, dagg):
     return torch.ops.pinsage.weighted_agg_backward(dagg.contiguous(), loc, w, ctx.n_q), None, None
 
 
+def _gather_setup(ctx, inputs, output):
+    h, idx, width = inputs
+    ctx.save_for_backward(idx)
+    ctx.shape = tuple(h.shape)
+
+
+def _gather_backward(ctx, dout):
+    """get_embeddings' gradient: index_add of the rows' cotangents (repeated ids summed)."""
+    idx, = ctx.saved_tensors
+    n, w = ctx.shape
+    return torch.ops.pinsage.scatter_add_rows(dout.contiguous(), idx, n, w), None, None
+
+
+def _scatter_setup(ctx, inputs, output):
+    grad, idx, n_rows, width = inputs
+    ctx.save_for_backward(idx)
+    ctx.d = grad.shape[1]
+
+
+def _scatter_backward(ctx, dout):
+    idx, = ctx.saved_tensors
+    return torch.ops.pinsage.gather_rows(dout.contiguous(), idx, ctx.d), None, None, None
+
+
+def _cat_setup(ctx, inputs, output):
+    h, rows, agg, W, b = inputs
+    y, norms = output
+    ctx.save_for_backward(h, rows, agg, W, y, norms)
+    ctx.mark_non_differentiable(norms)
+
+
+def _cat_backward(ctx, dy, _dnorms):
+    """y = normalize(lrelu([h[rows, :d] || agg] W^T + b)) (pinsage_model.py:208-210):
+    dp = norm_lrelu_backward(dy); dW = dp^T [h[rows] || agg], db = sum dp,
+    dh[rows, :d] += dp W[:, :d], dagg = dp W[:, d:] (products on pinsage::gemm)."""
+    h, rows, agg, W, y, norms = ctx.saved_tensors
+    ops = torch.ops.pinsage
+    out, K = W.shape
+    hid = agg.shape[1]
+    d = K - hid
+    n = y.shape[0]
+    dp = ops.norm_lrelu_backward(dy.contiguous(), y, norms)
+    dh = dagg = dW = db = None
+    if ctx.needs_input_grad[3]:
+        dp4 = _pad4(dp)
+        idx = rows.to(torch.int32) if rows is not None else torch.arange(n, dtype=torch.int32, device=dp.device)
+        idx4 = _pad4(idx)
+        dW = torch.cat([ops.gemm(dp4, False, None, h, False, idx4, out, d, dp4.shape[0]),
+                        ops.gemm(dp4, False, None, _pad4(agg.contiguous()), False, None, out, hid, dp4.shape[0])], 1)
+    if ctx.needs_input_grad[4]:
+        db = dp.sum(0)
+    if ctx.needs_input_grad[0]:
+        d_rows = ops.gemm(dp, True, None, W[:, :d], False, None, n, d, out)
+        if rows is None:
+            dh = torch.zeros_like(h)
+            dh[:n, :d] += d_rows
+        else:
+            dh = ops.scatter_add_rows(d_rows, rows, h.shape[0], h.shape[1])
+    if ctx.needs_input_grad[2]:
+        dagg = ops.gemm(dp, True, None, W[:, d:], False, None, n, hid, out)
+    return dh, None, dagg, dW, db
+
+
 def _register_autograd():
     torch.library.register_autograd("pinsage::linear", _linear_backward, setup_context=_linear_setup)
     torch.library.register_autograd("pinsage::weighted_agg", _agg_backward, setup_context=_agg_setup)
+    torch.library.register_autograd("pinsage::gather_rows", _gather_backward, setup_context=_gather_setup)
+    torch.library.register_autograd("pinsage::scatter_add_rows", _scatter_backward, setup_context=_scatter_setup)
+    torch.library.register_autograd("pinsage::concat_linear_lrelu_l2norm", _cat_backward,
+                                    setup_context=_cat_setup)
 
 
 def conv_layer(h, nodeset, nb_nodes, nb_weights, Qw, Qb, Ww, Wb):
@@ -120,7 +191,6 @@ def conv_layer(h, nodeset, nb_nodes, nb_weights, Qw, Qb, Ww, Wb):
     loc = inv.view(n, T).to(torch.int32).contiguous()
     q = ops.linear(hd, uniq.to(torch.int32).contiguous(), Qw, Qb, True)
     agg = ops.weighted_agg(q, loc, wn)
-    cat = torch.cat([hd[ns, :d], agg], 1).contiguous()
-    z = ops.linear(cat, None, Ww, Wb, True)
-    y = z / z.norm(dim=1, keepdim=True)
+    # [h[nodeset, :d] || agg] W^T + b, lrelu, row L2 norm: the concat read in place
+    y, _ = ops.concat_linear_lrelu_l2norm(hd, ns, agg, Ww, Wb)
     return y.to(h.device)

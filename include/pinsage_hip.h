@@ -215,6 +215,26 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
                              const float* bias, int64_t out, uint16_t* W_planes, float* y,
                              float* norms, float* agg, void* stream);
 
+/* get_embeddings' row gather (pinsage_model.py:21-23): out[i][0..d) =
+ * h[idx[i]][0..d), idx int64 (device).  Ids outside [0, n_h) give zero rows
+ * (the reference raises IndexError: callers validate).  Its transpose
+ * (the gradient, an index_add over repeated ids) is a pinsage_segment_wmean
+ * over the CSR of idx, deterministic in summation order. */
+int pinsage_gather_rows(const float* h, int64_t ldh, int64_t n_h, int64_t d, const int64_t* idx, int64_t n,
+                        float* out, int64_t ldo, void* stream);
+/* ConvLayer's W projection alone (pinsage_model.py:208-210):
+ *   y[f] = normalize(lrelu([h[self_idx[f]][0..d) || agg[f]] W^T + bias)),
+ *   norms[f] = ||lrelu(.)||_2
+ * with the concat read in place (no concat buffer).  self_idx int32 nullable
+ * (rows 0..n-1), W f32 [out][d+hid], 0 < out <= 128, d and hid multiples of 4. */
+int pinsage_concat_linear_l2norm(const float* h, int64_t ldh, const int32_t* self_idx, int64_t n, int64_t d,
+                                 const float* agg, int64_t ld_agg, int64_t hid, const float* W,
+                                 const float* bias, int64_t out, float* y, float* norms, void* stream);
+/* Backward of y = lrelu(p) / ||lrelu(p)|| (the autograd of pinsage_model.py:209-210):
+ *   dp = lrelu'(y) * (dy - y (y . dy)) / norms     (y, dy, dp f32 [n][out]) */
+int pinsage_norm_lrelu_backward(const float* y, const float* norms, const float* dy, int64_t n, int64_t out,
+                                float* dp, void* stream);
+
 /* ------------------------------------------------------------------ step hand-off
  * (PinSage.train_batch, pinsage_training.py:181-214, as ONE graph launch per step)
  * pinsage_step_stage: copy nbytes at src_off of slot (*ctr % R) of a pinned host

@@ -66,8 +66,16 @@ CASES = [  # n_rows, d, ldh, hid, T, U (q rows), n_h (h rows)
 ]
 
 
+@pytest.fixture(params=["3", "5"])
+def form(request, monkeypatch):
+    """the kernel form behind pinsage_conv_agg_project: 3 in-wave pipelined,
+    5 warp-specialised with the gather on LDS-DMA (read per call)"""
+    monkeypatch.setenv("PINSAGE_FUSED_AGGW", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("n_rows,d,ldh,hid,T,U,n_h", CASES)
-def test_agg_project_matches_f64(n_rows, d, ldh, hid, T, U, n_h):
+def test_agg_project_matches_f64(n_rows, d, ldh, hid, T, U, n_h, form):
     g = torch.Generator().manual_seed(n_rows * 7 + T)
     h = torch.randn(n_h, ldh, generator=g).cuda()
     q = torch.nn.functional.leaky_relu(torch.randn(U, hid, generator=g), 0.01).cuda()
@@ -89,7 +97,7 @@ def test_agg_project_matches_f64(n_rows, d, ldh, hid, T, U, n_h):
     assert ((nrm.double() - rn).abs() / rn).max().item() <= 1e-4
 
 
-def test_agg_project_agg_is_the_slot_order_fma_chain():
+def test_agg_project_agg_is_the_slot_order_fma_chain(form):
     """agg equals the unfused aggregation kernel (pinsage_weighted_agg, the same
     fma chain in slot order) bitwise."""
     import _native as nat

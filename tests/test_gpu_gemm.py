@@ -258,7 +258,7 @@ def test_presplit_b_planes_bitwise(cfg):
     try:
         assert lib.pinsage_gemm_set_prec(1) == 0
         for M, N, K in [(1, 128, 8), (37, 128, 136), (200, 256, 520), (3000, 512, 512),
-                        (10541, 512, 512), (24369, 512, 128)]:
+                        (10541, 512, 512), (24369, 512, 128), (500, 200, 264), (77, 72, 40)]:
             A = torch.randn(M + 7, K, device="cuda", generator=g)
             A *= torch.exp2(torch.randint(-20, 20, (M + 7, 1), device="cuda", generator=g).float())
             W = torch.randn(N, K, device="cuda", generator=g) * 0.05

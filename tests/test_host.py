@@ -373,8 +373,9 @@ def test_torch_operator_library_registers_every_op():
     import torch
     import pinsage_ops
     pinsage_ops.load()
-    for name in ("ppr_topk", "frontier", "linear", "gemm", "weighted_agg", "weighted_agg_backward",
-                 "segment_wmean"):
+    for name in ("walk", "ppr_topk", "frontier", "gather_rows", "scatter_add_rows", "linear",
+                 "concat_linear_lrelu_l2norm", "norm_lrelu_backward", "gemm", "weighted_agg",
+                 "weighted_agg_backward", "segment_wmean"):
         assert hasattr(torch.ops.pinsage, name), name
     x = torch.zeros(4, 8)
     W = torch.zeros(4, 8)
