@@ -386,7 +386,8 @@ def main():
             torch.cuda.synchronize()
             off = eng.off
             # micro-batched: the frontier of the last slice's outputs-only forward
-            ws = tr._fused.ws if tr._fused is not None else tr.model.runner()._ws
+            rn = tr.model.runner()
+            ws = tr._fused.ws if tr._fused is not None else (rn._ws if rn._ws is not None else rn.last_ws)
             cN0 = int(eng.view(ws, int(off.count_N[0]), torch.int32, 1).item())
             cS0 = int(eng.view(ws, int(off.count_S[0]), torch.int32, 1).item())
             sizes.append((cN0, cS0))

@@ -149,6 +149,60 @@ __global__ __launch_bounds__(256) void agg_kernel(const float* __restrict__ q, i
   }
 }
 
+// XCD-sliced aggregation.  Workgroups are dealt round-robin over the 8 XCDs,
+// so block b runs on XCD b % 8; that XCD owns column slice b % 8 (hid / 8
+// floats) of q and agg.  Each XCD then gathers only its eighth of the q table
+// (U x hid / 8 x 4 B: 2.7 MB at C2 layer 0), which its 4-MiB L2 holds, instead
+// of every XCD pulling random whole rows of the full table through the
+// Infinity Cache.  A wave covers 64 / SW4 rows (SW4 float4s of the slice per
+// row), the T slots summed in order t = 0, 1, ... (bitwise agg_kernel).
+constexpr int kXcds = 8;
+template <int SW4>
+__global__ __launch_bounds__(256) void agg_sliced_kernel(const float* __restrict__ q, int hid,
+                                                         const int32_t* __restrict__ loc,
+                                                         const float* __restrict__ wloc, int T,
+                                                         const int* __restrict__ nS, int64_t nS_host,
+                                                         float* __restrict__ agg) {
+  constexpr int RPW = 64 / SW4;  // rows per wave pass
+  constexpr int UF = 8;          // slots in flight per lane
+  const int64_t F = nS ? (int64_t)(*nS) : nS_host;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slice = blockIdx.x % kXcds;
+  const int64_t G = gridDim.x / kXcds, g = blockIdx.x / kXcds;
+  const int r_in = lane / SW4, c4 = lane % SW4;
+  const int hid4 = hid >> 2;
+  const float4* q4 = reinterpret_cast<const float4*>(q) + slice * SW4 + c4;
+  for (int64_t rg = g * 4 + wave; rg * RPW < F; rg += G * 4) {
+    const int64_t f = rg * RPW + r_in;
+    const int64_t fr = f < F ? f : F - 1;
+    const int32_t* lr = loc + fr * T;
+    const float* wr = wloc + fr * T;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t0 = 0; t0 < T; t0 += UF) {
+      int32_t ix[UF];
+      float w[UF];
+#pragma unroll
+      for (int u = 0; u < UF; ++u) {
+        const int t = min(t0 + u, T - 1);
+        ix[u] = lr[t];
+        w[u] = t0 + u < T ? wr[t] : 0.f;
+      }
+      float4 x[UF];
+#pragma unroll
+      for (int u = 0; u < UF; ++u) x[u] = q4[(int64_t)ix[u] * hid4];
+#pragma unroll
+      for (int u = 0; u < UF; ++u) {
+        const bool ok = t0 + u < T;  // padded slots keep the sum (no fma with w = 0)
+        a.x = ok ? fmaf(w[u], x[u].x, a.x) : a.x;
+        a.y = ok ? fmaf(w[u], x[u].y, a.y) : a.y;
+        a.z = ok ? fmaf(w[u], x[u].z, a.z) : a.z;
+        a.w = ok ? fmaf(w[u], x[u].w, a.w) : a.w;
+      }
+    }
+    if (f < F) reinterpret_cast<float4*>(agg + f * hid)[slice * SW4 + c4] = a;
+  }
+}
+
 // ---------------------------------------------------------------- transpose (CSR by q row)
 // Popular tracks sit in thousands of neighbour lists, so global per-row
 // counters are hot.  When the distinct-neighbour count fits (<= kLdsRows), each
@@ -236,6 +290,7 @@ __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restri
 // zero for the next step).  Multi-block form: one block per 1024 rows, each
 // block sums its predecessors' totals itself.
 constexpr int kDqChunk = 16;
+constexpr int kDqSplit = 0x100;  // chunk flag: the row's sum is split over several chunks
 constexpr int kScanB = 256, kScanPer = 4, kScanChunk = kScanB * kScanPer;
 __device__ __forceinline__ int n_chunks(int c) { return (c + kDqChunk - 1) / kDqChunk; }
 __device__ __forceinline__ void wave_scan2(int& a, int& b, int lane) {
@@ -251,7 +306,8 @@ __device__ __forceinline__ void wave_scan2(int& a, int& b, int lane) {
 // thread whose range holds index n also writes off[n] and the chunk count
 __device__ __forceinline__ void scan_emit(int* __restrict__ cnt, int64_t i0, int per, int64_t n,
                                           int& p, int& pc, int* __restrict__ off,
-                                          int* __restrict__ cursor, int2* __restrict__ chunks,
+                                          int* __restrict__ cursor, int* __restrict__ cbase,
+                                          int2* __restrict__ chunks,
                                           int* __restrict__ nchunks, int2* __restrict__ split,
                                           int* __restrict__ nsplit) {
   for (int q = 0; q < per; ++q) {
@@ -260,9 +316,12 @@ __device__ __forceinline__ void scan_emit(int* __restrict__ cnt, int64_t i0, int
       const int v = cnt[i];
       off[i] = p;
       cursor[i] = p;
+      cbase[i] = pc;
       cnt[i] = 0;
       const int nc = n_chunks(v);
-      for (int j = 0; j < nc; ++j) chunks[pc + j] = make_int2((int)i, p + j * kDqChunk);
+      // chunk = {row, occurrences (<= kDqChunk) | kDqSplit if the row spans several chunks}
+      for (int j = 0; j < nc; ++j)
+        chunks[pc + j] = make_int2((int)i, min(kDqChunk, v - j * kDqChunk) | (nc > 1 ? kDqSplit : 0));
       if (nc > 1) split[atomicAdd(nsplit, 1)] = make_int2((int)i, pc);  // order is irrelevant
       p += v;
       pc += nc;
@@ -302,6 +361,7 @@ __global__ __launch_bounds__(kScanB) void scan_apply_kernel(int* __restrict__ cn
                                                             const int2* __restrict__ bsum,
                                                             int* __restrict__ off,
                                                             int* __restrict__ cursor,
+                                                            int* __restrict__ cbase,
                                                             int2* __restrict__ chunks,
                                                             int* __restrict__ nchunks,
                                                             int2* __restrict__ split,
@@ -346,13 +406,14 @@ __global__ __launch_bounds__(kScanB) void scan_apply_kernel(int* __restrict__ cn
     p += ws[0][i];
     pc += ws[1][i];
   }
-  scan_emit(cnt, i0, kScanPer, n, p, pc, off, cursor, chunks, nchunks, split, nsplit);
+  scan_emit(cnt, i0, kScanPer, n, p, pc, off, cursor, cbase, chunks, nchunks, split, nsplit);
 }
 // single-block form, U <= 1024 * 64
 __global__ __launch_bounds__(1024) void scan_small_kernel(int* __restrict__ cnt,
                                                           const int* __restrict__ n_dev,
                                                           int* __restrict__ off,
                                                           int* __restrict__ cursor,
+                                                          int* __restrict__ cbase,
                                                           int2* __restrict__ chunks,
                                                           int* __restrict__ nchunks,
                                                           int2* __restrict__ split,
@@ -381,7 +442,7 @@ __global__ __launch_bounds__(1024) void scan_small_kernel(int* __restrict__ cnt,
     p += wsum[0][i];
     pc += wsum[1][i];
   }
-  scan_emit(cnt, i0, per, U, p, pc, off, cursor, chunks, nchunks, split, nsplit);
+  scan_emit(cnt, i0, per, U, p, pc, off, cursor, cbase, chunks, nchunks, split, nsplit);
   // no range holds index U when U == 1024 * per: thread 1023 ends on the totals
   if (threadIdx.x == 1023 && U == 1024 * per) {
     off[U] = p;
@@ -389,12 +450,26 @@ __global__ __launch_bounds__(1024) void scan_small_kernel(int* __restrict__ cnt,
   }
 }
 
+// occurrence (slot e = f T + t) at position pos of row u's range: its
+// {source row f, weight} goes to entry (pos - off[u]) % kDqChunk of chunk
+// cbase[u] + (pos - off[u]) / kDqChunk, so a dq wave reads its chunk's rows
+// and weights with one load
+__device__ __forceinline__ void put_occ(int2* __restrict__ occ2, const int* __restrict__ off,
+                                        const int* __restrict__ cbase, const float* __restrict__ wloc,
+                                        int T, int u, int pos, int64_t e) {
+  const int local = pos - off[u];
+  occ2[(int64_t)(cbase[u] + local / kDqChunk) * kDqChunk + local % kDqChunk] =
+      make_int2((int)(e / T), __float_as_int(wloc[e]));
+}
+
 __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restrict__ loc,
+                                                        const float* __restrict__ wloc,
                                                         const int* __restrict__ nS, int T,
                                                         const int* __restrict__ nN,
                                                         int* __restrict__ cursor,
-                                                        int32_t* __restrict__ occ,
-                                                        int32_t* __restrict__ occ_u, int max_ranges) {
+                                                        const int* __restrict__ off,
+                                                        const int* __restrict__ cbase,
+                                                        int2* __restrict__ occ2, int max_ranges) {
   extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
   const int U = *nN;
@@ -412,8 +487,7 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
     for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
       const int32_t u = loc[e];
       const int pos = atomicAdd(hist + u, 1);
-      occ[pos] = (int32_t)e;
-      occ_u[pos] = u;
+      put_occ(occ2, off, cbase, wloc, T, u, pos, e);
     }
     return;
   }
@@ -441,8 +515,7 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
         const int u = loc[e] - u0;
         if ((unsigned)u < (unsigned)nu) {
           const int pos = atomicAdd(hist + u, 1);
-          occ[pos] = (int32_t)e;
-          occ_u[pos] = u0 + u;
+          put_occ(occ2, off, cbase, wloc, T, u0 + u, pos, e);
         }
       }
       __syncthreads();  // the next item zeroes hist
@@ -466,10 +539,7 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
       if (u == v) pos = b + __popcll(m & ((1ull << lane) - 1));
       rem &= ~m;
     }
-    if (e < n) {
-      occ[pos] = (int32_t)e;
-      occ_u[pos] = u;
-    }
+    if (e < n) put_occ(occ2, off, cbase, wloc, T, u, pos, e);
   }
 }
 
@@ -477,16 +547,17 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
 // table of w[f][t] * dagg[f]   (the transpose of agg, pinsage_model.py:202).
 // One wave per chunk of <= kDqChunk occurrences of ONE row u (chunk list from
 // the CSR scan; popular tracks, in thousands of neighbour lists, span many
-// chunks): the wave issues its q row and all of its dagg rows at once, so a
-// chunk costs one memory round trip.  A row with one chunk is finished here;
-// a row split over several chunks leaves one raw partial per chunk in `part`
-// and dq_combine_kernel sums them in chunk order (deterministic, and no
+// chunks).  A chunk is {u, n | split} plus its n {row f, weight} pairs, one
+// load each; the wave prefetches its next chunk's pair while it issues this
+// chunk's q row and all of its dagg rows at once, so a chunk costs about one
+// memory round trip.  A row with one chunk is finished here; a row split over
+// several chunks leaves one raw partial per chunk in `part` and
+// dq_combine_kernel sums them in chunk order (deterministic, and no
 // device-scope float atomics: with per-XCD L2s those run at the memory side
 // and serialise on popular rows).
 template <int VEC>
 __global__ __launch_bounds__(256) void dq_chunk_kernel(
-    const int2* __restrict__ chunks, const int* __restrict__ nchunks, const int* __restrict__ off,
-    const int32_t* __restrict__ occ, const float* __restrict__ wloc, int T,
+    const int2* __restrict__ chunks, const int* __restrict__ nchunks, const int2* __restrict__ occ2,
     const float* __restrict__ dagg, int64_t ld_dagg, const float* __restrict__ q, int hid,
     float* __restrict__ dpq, float* __restrict__ part) {
   const int lane = threadIdx.x & 63;
@@ -494,19 +565,21 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int h4 = hid >> 2;
   const int nch = *nchunks;
+  int2 dsc = make_int2(0, 0), oc = make_int2(0, 0);
+  if (wid < nch) {
+    dsc = chunks[wid];
+    if (lane < kDqChunk) oc = occ2[wid * kDqChunk + lane];
+  }
   for (int64_t ci = wid; ci < nch; ci += nw) {
-    const int2 ch = chunks[ci];
-    const int u = ch.x, p0 = ch.y;
-    const int s0 = off[u], s1 = off[u + 1];
-    const int n = min(kDqChunk, s1 - p0);
-    const bool split = s1 - s0 > kDqChunk;
-    int32_t my_row = 0;
-    float my_w = 0.f;
-    if (lane < n) {
-      const int32_t e = occ[p0 + lane];
-      my_row = e / T;
-      my_w = wloc[e];
+    int2 dsc_n = make_int2(0, 0), oc_n = make_int2(0, 0);
+    if (ci + nw < nch) {  // the next chunk's descriptor and pairs, under this one
+      dsc_n = chunks[ci + nw];
+      if (lane < kDqChunk) oc_n = occ2[(ci + nw) * kDqChunk + lane];
     }
+    const int u = dsc.x, n = dsc.y & 0xff;
+    const bool split = (dsc.y & kDqSplit) != 0;
+    const int32_t my_row = oc.x;
+    const float my_w = __int_as_float(oc.y);
     for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
       float4 qv[VEC], x[kDqChunk][VEC];
 #pragma unroll
@@ -561,6 +634,8 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
                                      acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
       }
     }
+    dsc = dsc_n;
+    oc = oc_n;
   }
 }
 
@@ -1200,6 +1275,19 @@ int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, i
                const int* nS, int64_t S_max, float* agg, hipStream_t st) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "agg: hidden dim must be a multiple of 4");
   if (S_max <= 0) return kOk;
+  const bool sliced = !getenv("PINSAGE_AGG_SLICED") || atoi(getenv("PINSAGE_AGG_SLICED")) != 0;
+  if (sliced && (hid == 512 || hid == 256 || hid == 128)) {
+    // 4 waves per block, blocks in groups of 8 (one per XCD slice), ~2 passes per wave
+    const int rpw = 64 / (hid / 32);
+    const int64_t per_block = 4 * rpw * 2;
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>((S_max + per_block - 1) / per_block, 1024));
+    const dim3 gr((unsigned)(G * kXcds)), bl(256);
+    if (hid == 512) hipLaunchKernelGGL((agg_sliced_kernel<16>), gr, bl, 0, st, q, hid, loc, wloc, T, nS, S_max, agg);
+    else if (hid == 256) hipLaunchKernelGGL((agg_sliced_kernel<8>), gr, bl, 0, st, q, hid, loc, wloc, T, nS, S_max, agg);
+    else hipLaunchKernelGGL((agg_sliced_kernel<4>), gr, bl, 0, st, q, hid, loc, wloc, T, nS, S_max, agg);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
   // hid >= 512: one wave per row (2 float4 per lane per slot, 8 slots in flight);
   // measured faster than two waves per row with all 16 slots in flight
   if (hid >= 512)
@@ -1233,10 +1321,9 @@ int csr_prepare() {
   return rc;
 }
 
-int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, const int* nN,
-                     int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int32_t* occ,
-                     int32_t* occ_u, int2* chunks, int* nchunks, int2* split, int* nsplit,
-                     float* dpq, int hid, hipStream_t st) {
+int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64_t S_max, int T, const int* nN,
+                     int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int* cbase, int2* occ2,
+                     int2* chunks, int* nchunks, int2* split, int* nsplit, float* dpq, int hid, hipStream_t st) {
   const int lds = (int)std::min<int64_t>(N_max, kLdsRows) * 4;
   // more rows than one histogram: (range, slice) items over a CU-wide grid
   const int gb = N_max > kLdsRows ? kCsrRangeGrid : std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
@@ -1249,7 +1336,7 @@ int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, co
                      (float*)nullptr, hid, nsplit, max_ranges);
   PS_CHECK_LAUNCH();
   if (N_max <= 1024 * 64) {
-    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor, chunks,
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor, cbase, chunks,
                        nchunks, split, nsplit);
     PS_CHECK_LAUNCH();
   } else {
@@ -1258,11 +1345,11 @@ int launch_csr_build(const int32_t* loc, const int* nS, int64_t S_max, int T, co
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bs);
     PS_CHECK_LAUNCH();
     hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanB), 0, st, cnt, nN, bs, off, cursor,
-                       chunks, nchunks, split, nsplit);
+                       cbase, chunks, nchunks, split, nsplit);
     PS_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cursor, occ,
-                     occ_u, max_ranges);
+  hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, wloc, nS, T, nN, cursor, off, cbase,
+                     occ2, max_ranges);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -1275,17 +1362,19 @@ int64_t dq_chunk_capacity(int64_t S_max, int T, int64_t N_max) {
 int64_t dq_split_capacity(int64_t S_max, int T) { return S_max * T / (kDqChunk + 1) + 1; }
 
 int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks, const int2* split,
-                     const int* nsplit, int64_t max_split, const int* off, const int32_t* occ,
-                     const float* wloc, int T, const float* dagg, int64_t ld_dagg, const float* q,
+                     const int* nsplit, int64_t max_split, const int* off, const int2* occ2,
+                     const float* dagg, int64_t ld_dagg, const float* q,
                      int hid, float* dpq, float* part, hipStream_t st) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
-  const int grid = grid_for(max_chunks * 64, 256, 8192);
+  // persistent waves (each prefetches its next chunk): PINSAGE_DQ_GRID overrides (A/B)
+  static const int cap = getenv("PINSAGE_DQ_GRID") ? atoi(getenv("PINSAGE_DQ_GRID")) : 2048;
+  const int grid = grid_for(max_chunks * 64, 256, std::max(1, cap));
   if (hid >= 512)
-    hipLaunchKernelGGL((dq_chunk_kernel<2>), dim3(grid), dim3(256), 0, st, chunks, nchunks, off, occ,
-                       wloc, T, dagg, ld_dagg, q, hid, dpq, part);
+    hipLaunchKernelGGL((dq_chunk_kernel<2>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg, ld_dagg,
+                       q, hid, dpq, part);
   else
-    hipLaunchKernelGGL((dq_chunk_kernel<1>), dim3(grid), dim3(256), 0, st, chunks, nchunks, off, occ,
-                       wloc, T, dagg, ld_dagg, q, hid, dpq, part);
+    hipLaunchKernelGGL((dq_chunk_kernel<1>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg, ld_dagg,
+                       q, hid, dpq, part);
   PS_CHECK_LAUNCH();
   hipLaunchKernelGGL(dq_combine_kernel, dim3((int)std::max<int64_t>(1, std::min<int64_t>(max_split, 512))),
                      dim3(1024), 0, st, split, nsplit, off, part, q, hid, dpq);

@@ -43,14 +43,12 @@ int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const
                       const int64_t*, int64_t, int32_t*, float*, int, const int*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
-int launch_csr_build(const int32_t*, const int*, int64_t, int, const int*, int64_t, int*, int*,
-                     int*, int*, int32_t*, int32_t*, int2*, int*, int2*, int*, float*, int,
-                     hipStream_t);
+int launch_csr_build(const int32_t*, const float*, const int*, int64_t, int, const int*, int64_t, int*, int*,
+                     int*, int*, int*, int2*, int2*, int*, int2*, int*, float*, int, hipStream_t);
 int64_t dq_chunk_capacity(int64_t, int, int64_t);
 int64_t dq_split_capacity(int64_t, int);
 int launch_dq_chunks(const int2*, const int*, int64_t, const int2*, const int*, int64_t, const int*,
-                     const int32_t*, const float*, int, const float*, int64_t, const float*, int,
-                     float*, float*, hipStream_t);
+                     const int2*, const float*, int64_t, const float*, int, float*, float*, hipStream_t);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
@@ -110,8 +108,8 @@ struct LayerBuf {
   size_t qsplit = 0;  // the Q weight's hi / mid / lo bf16 planes (split-bf16 Q projection)
   size_t wsplit = 0;  // the W weight's planes (the aggregation + projection kernel's B operand)
   // backward
-  size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, occ = 0,
-         occ_u = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
+  size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
+         occ2 = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
   int64_t max_chunks = 0, max_split = 0;
   // parameter offsets (floats) into the flat param / grad buffers
   int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
@@ -391,9 +389,9 @@ static void layout(Engine& E) {
     lb.bsum = carve(cur, (int64_t)ceil_div(FN + 1, 1024) * 8 + 16);
     lb.off = carve(cur, (FN + 1) * 4);
     lb.cursor = carve(cur, (FN + 1) * 4);
-    lb.occ = carve(cur, FS * T * 4);
-    lb.occ_u = carve(cur, FS * T * 4);
     lb.max_chunks = dq_chunk_capacity(FS, (int)T, FN);
+    lb.cbase = carve(cur, (FN + 1) * 4);
+    lb.occ2 = carve(cur, lb.max_chunks * 16 * 8);  // {row, weight} pairs, 16 per chunk
     lb.chunks = carve(cur, lb.max_chunks * 8);
     lb.nchunks = carve(cur, 16);
     lb.dqpart = carve(cur, lb.max_chunks * c.hid * 4);  // partials of split dq rows
@@ -523,9 +521,9 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
     Timed tc(E, lname("fwd.csr", l), st);
-    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), cnt(lb.S), lb.S.cap, T, cnt(lb.N), lb.N.cap,
-                            at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
-                            at<int>(ws, lb.cursor), at<int32_t>(ws, lb.occ), at<int32_t>(ws, lb.occ_u),
+    PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), cnt(lb.S), lb.S.cap, T, cnt(lb.N),
+                            lb.N.cap, at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
+                            at<int>(ws, lb.cursor), at<int>(ws, lb.cbase), at<int2>(ws, lb.occ2),
                             at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), at<int2>(ws, lb.split),
                             at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, st));
   }
@@ -807,7 +805,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   const LayerBuf& l0 = E.L[0];
   PS_REQUIRE(!adam || (l0.pQw == 0 && l0.pQb == l0.pQw + c.hid * l0.d && l0.pWw == l0.pQb + c.hid),
              kErrArg, "engine: Q0 must lead the flat parameter layout");
-  const int Lc = (int)c.n_layers, T = (int)c.T;
+  const int Lc = (int)c.n_layers;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
   const int o = (int)c.out, hd = (int)c.hid;
@@ -991,7 +989,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     }
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
                             at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
-                            at<int>(ws, lb.off), at<int32_t>(ws, lb.occ), at<float>(ws, lb.wloc), T,
+                            at<int>(ws, lb.off), at<int2>(ws, lb.occ2),
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
                             at<float>(ws, lb.dqpart), st));
     PS_TRY(run_pend(E));

@@ -653,6 +653,7 @@ class _EngineRunner:
         self._table_key = None
         self._table = None
         self._ws = None
+        self.last_ws = None  # workspace of the last autograd forward
 
     # -- parameters
     def names(self):
@@ -838,6 +839,7 @@ class _EngineFn(torch.autograd.Function):
         nat.check(nat.lib().pinsage_engine_gather_output(e.h, nat.ptr(ws), n, nat.ptr(out),
                                                          nat.stream_ptr()), "gather")
         ctx.runner, ctx.ws, ctx.feats, ctx.table, ctx.n = runner, ws, feats, table, n
+        runner.last_ws = ws  # (bench.py reads the last call's frontier sizes)
         ctx.tabs = tabs  # the frontier's tables stay alive with the workspace
         ctx.engine = e
         return out

@@ -127,3 +127,28 @@ def test_agg_project_rejects_unsupported_shapes():
                                                 _vp(dummy), 1, T, _vp(dummy), _vp(dummy), out, _vp(dummy),
                                                 _vp(dummy), _vp(dummy), _vp(dummy), None)
         assert rc == -2
+
+
+@pytest.mark.parametrize("hid,T,n_rows,U", [(512, 10, 5704, 10550), (256, 50, 333, 2000), (128, 3, 1, 5),
+                                            (512, 64, 77, 300)])
+def test_xcd_sliced_aggregation_is_bitwise_the_row_kernel(hid, T, n_rows, U, monkeypatch):
+    """pinsage_weighted_agg on the XCD-sliced kernel (column slice b % 8 per
+    block) equals the one-wave-per-row kernel bitwise: same fma chain per
+    element, slot order t = 0, 1, ..."""
+    import _native as nat
+    g = torch.Generator().manual_seed(hid + T)
+    q = torch.randn(U, hid, generator=g).cuda()
+    loc = torch.randint(0, U, (n_rows, T), generator=g, dtype=torch.int32).cuda()
+    w = torch.rand(n_rows, T, generator=g).cuda()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out = []
+    for sliced in ("1", "0"):
+        monkeypatch.setenv("PINSAGE_AGG_SLICED", sliced)
+        a = torch.full((n_rows, hid), float("nan"), device="cuda")
+        nat.check(nat.lib().pinsage_weighted_agg(_vp(q), hid, _vp(loc), _vp(w), n_rows, T, _vp(a), st), "agg")
+        torch.cuda.synchronize()
+        out.append(a)
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1])
+    ref = (w.double()[:, :, None] * q.double()[loc.long()]).sum(1)
+    assert ((out[0].double() - ref).norm() / ref.norm()).item() < 1e-6

@@ -31,6 +31,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="c2l0,c2l1,c4l0,c4sl0")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--agg-only", action="store_true",
+                    help="time the aggregation alone (pinsage_weighted_agg; PINSAGE_AGG_SLICED=0/1)")
     args = ap.parse_args()
     import _native as nat
     lib = nat.lib()
@@ -51,7 +53,12 @@ def main():
         agg = torch.empty(F, hid, device="cuda")
         planes = torch.empty(3 * 128 * (d + hid), dtype=torch.int16, device="cuda")
 
+        def run_agg():
+            nat.check(lib.pinsage_weighted_agg(vp(q), hid, vp(loc), vp(w), F, T, vp(agg), st), "weighted_agg")
+
         def run():
+            if args.agg_only:
+                return run_agg()
             nat.check(lib.pinsage_conv_agg_project(vp(h), d, d, vp(self_src), vp(q), hid, U, vp(loc), vp(w), F, T,
                                                    vp(W), vp(bias), 128, vp(planes), vp(y), vp(nrm), vp(agg), st),
                       "conv_agg_project")
@@ -70,6 +77,13 @@ def main():
         distinct = min(U, F * T)
         alg = distinct * hid * 4 + F * T * 8 + F * d * 4 + 3 * 128 * (d + hid) * 2 + F * (hid + 129) * 4
         logical = F * T * hid * 4 + F * T * 8 + F * d * 4 + F * (hid + 129) * 4
+        if args.agg_only:
+            alg = distinct * hid * 4 + F * T * 8 + F * hid * 4
+            logical = F * T * hid * 4 + F * T * 8 + F * hid * 4
+            print(json.dumps({"shape": name, "agg_only": True, "sliced": os.environ.get("PINSAGE_AGG_SLICED", "1"),
+                              "us": round(us, 2), "alg_frac_hbm": round(alg / us / 1e3 / 8000, 3),
+                              "logical_TBs": round(logical / us / 1e6, 2)}), flush=True)
+            continue
         print(json.dumps({"shape": name, "form": os.environ.get("PINSAGE_FUSED_AGGW", "3"), "F": F, "d": d, "T": T, "U": U, "us": round(us, 2),
                           "note": "includes the W split launch",
                           "alg_GBs": round(alg / us / 1e3, 1), "alg_frac_hbm": round(alg / us / 1e3 / 8000, 3),
