@@ -109,6 +109,7 @@ _SIGS = {
     "pinsage_engine_loss": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_int, vp]),
     "pinsage_engine_set_output_grad": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_backward": (ctypes.c_int, [vp, vp, vp]),
+    "pinsage_engine_backward_stage": (ctypes.c_int, [vp, vp, ctypes.c_int, vp]),
     "pinsage_engine_adam": (ctypes.c_int, [vp, vp, f32, f32, f32, vp]),
     "pinsage_engine_backward_adam": (ctypes.c_int, [vp, vp, vp, f32, f32, f32, vp]),
     "pinsage_engine_read_counts": (ctypes.c_int, [vp, vp, vp, vp, vp]),

@@ -5,20 +5,18 @@
 //             pre-normalised by their f64 row sum = sum(w*q)/sum(w))
 //   y[f]    = normalize(lrelu([h[self f] || agg[f]] W^T + b))   (:208-211)
 //
-// One workgroup (8 waves) per 16 rows, two workgroups per CU, so one
-// workgroup's gather overlaps the other's projection (a 32-row tile at one
-// workgroup per CU ran gather, then MFMA, then epilogue back to back: 38 us at
-// C2, 55 us at C4).  The workgroup stages the 16 rows' A operand
-// [h_self || agg] in LDS -- the self rows gathered from h, the aggregate formed
-// right there from the T gathered q rows (fma in slot order t = 0, 1, ..., the
-// same arithmetic as agg_kernel) and also written out for the backward's
-// weight gradient -- so agg is never read back from memory.  The projection
-// runs on fp32 MFMA v_mfma_f32_16x16x4_f32: wave w owns output columns
-// 16 w .. 16 w + 15 over all of K, two accumulators alternating (its 40-cycle
-// dependent latency over a 32-cycle issue); A fragments are ds_read_b128 of
-// the tile, B fragments (W rows, K-major) stream from global / L2 with a
-// one-chunk register double buffer.  Then bias, LeakyReLU and the row L2 norm
-// through a [16][128] LDS image.
+// A workgroup owns a contiguous range of rows (~F / #blocks), in tiles.  Per
+// tile it stages [h_self || agg] in LDS -- the self rows gathered from h, the
+// aggregate formed right there from the T gathered q rows (fma in slot order
+// t = 0, 1, ..., the same arithmetic as agg_kernel) and also written out for
+// the backward's weight gradient -- so agg is never read back from memory.
+// The projection runs on split-bf16 MFMA (each fp32 operand split exactly into
+// bf16 hi / mid / lo in registers, six products, fp32 accumulation:
+// bf16split.h), then bias, LeakyReLU and the row L2 norm through an LDS image.
+// Two shapes: 16 rows per 512-thread workgroup, two workgroups per CU
+// (v_mfma_f32_16x16x32_bf16, each wave 16 output columns over all of K), and
+// 32 rows per 1024-thread workgroup, one per CU (v_mfma_f32_32x32x16_bf16, K
+// split four ways over the waves; W read once per 32 rows).
 #include <algorithm>
 #include <cstdlib>
 
@@ -53,11 +51,15 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
   float* sW = reinterpret_cast<float*>(sLoc + kAwRows * kAwTMax);  // [16][T]
   int* sSelf = reinterpret_cast<int*>(sW + kAwRows * kAwTMax);     // [16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // rows dealt in contiguous ranges: block b of G owns [F b / G, F (b+1) / G)
+  // in near-equal tiles of <= 16 rows (two blocks per CU: G ~ F / 12 fills them)
   const int64_t F = *nS;
-  const int64_t tiles = (F + kAwRows - 1) / kAwRows;
-  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const int64_t r0 = tile * kAwRows;
-    const int nrows = (int)min((int64_t)kAwRows, F - r0);
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / G, len = F * (b + 1) / G - rb;
+  const int ntile = (int)((len + kAwRows - 1) / kAwRows);
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int64_t r0 = rb + len * tile / ntile;
+    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
     // ---- slot lists and self-row indices of the tile
     for (int i = tid; i < kAwRows * T; i += kAwThreads) {
       const int row = i / T, t = i - row * T;
@@ -136,43 +138,39 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
       }
     }
     __syncthreads();
-    // ---- projection: wave w, columns 16 w .. 16 w + 15, all of K.
-    // v_mfma_f32_16x16x4_f32: lane l supplies A[row l & 15][k] and B[k][col l & 15]
-    // for k = (l >> 4) (+4 per instruction); a float4 of k-quad g = l >> 4 feeds
-    // four instructions, the r-th taking k = 16 s + 4 g + r (a bijection onto the
-    // 16 k of chunk s)
+    // ---- projection: wave w, columns 16 w .. 16 w + 15, all of K, on split-bf16
+    // products (v_mfma_f32_16x16x32_bf16, six per 32-k step; A and W split into
+    // bf16 hi / mid / lo in registers, bf16split.h).  Lane l supplies
+    // A[row l & 15][k0 + 8 (l >> 4) ..] and W[col l & 15][same k]; W fragments
+    // of step s+1 load from L2 while step s runs.
     const int l16 = lane & 15, g = lane >> 4;
-    const float* wrow = W + (int64_t)(wave * 16 + l16) * K;
-    const float* arow = sA + l16 * lda;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    // chunks of 4 k-sixteens (64 k); B fragments of chunk c+1 load while c runs
-    const int nch = K / 64;
-    float4 bcur[4], bnxt[4];
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) bcur[s2] = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 4 * g);
-    for (int ch = 0; ch < nch; ++ch) {
-      const int k0 = 64 * ch;
-      if (ch + 1 < nch) {
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2)
-          bnxt[s2] = *reinterpret_cast<const float4*>(wrow + k0 + 64 + 16 * s2 + 4 * g);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        const float4 av = *reinterpret_cast<const float4*>(arow + k0 + 16 * s2 + 4 * g);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bcur[s2].x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bcur[s2].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bcur[s2].z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bcur[s2].w, acc1, 0, 0, 0);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) bcur[s2] = bnxt[s2];
+    const float* wrow = W + (int64_t)(wave * 16 + l16) * K + 8 * g;
+    const float* arow = sA + l16 * lda + 8 * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int nst = K / 32;
+    float4 b0 = *reinterpret_cast<const float4*>(wrow), b1 = *reinterpret_cast<const float4*>(wrow + 4);
+    for (int s = 0; s < nst; ++s) {
+      const int kn = s + 1 < nst ? 32 * (s + 1) : 32 * s;  // (the last step reloads itself)
+      const float4 n0 = *reinterpret_cast<const float4*>(wrow + kn);
+      const float4 n1 = *reinterpret_cast<const float4*>(wrow + kn + 4);
+      const float* ap = arow + 32 * s;
+      bf16x8 aH, aM, aL, bH, bM, bL;
+      split3(*reinterpret_cast<const float4*>(ap), *reinterpret_cast<const float4*>(ap + 4), aH, aM, aL);
+      split3(b0, b1, bH, bM, bL);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aL, bH, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aH, bL, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aM, bM, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aM, bH, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aH, bM, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aH, bH, acc, 0, 0, 0);
+      b0 = n0;
+      b1 = n1;
     }
     __syncthreads();  // every wave is done reading the A tile
     // ---- the [16][128] output tile -> LDS, then bias, lrelu, row L2 norm
     float* red = sA;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(4 * g + r) * kAwOut + wave * 16 + l16] = acc0[r] + acc1[r];
+    for (int r = 0; r < 4; ++r) red[(4 * g + r) * kAwOut + wave * 16 + l16] = acc[r];
     __syncthreads();
     {
       const int row = tid >> 5, c4 = tid & 31;  // 4 columns 4 c4 .. 4 c4 + 3
@@ -226,11 +224,15 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
   float* sW = reinterpret_cast<float*>(sLoc + kAw32Rows * kAw32TMax);  // [32][T]
   int* sSelf = reinterpret_cast<int*>(sW + kAw32Rows * kAw32TMax);     // [32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // rows dealt in contiguous ranges: block b of G owns [F b / G, F (b+1) / G)
+  // in near-equal tiles of <= 32 rows, so G ~ F / 24 blocks fill the CUs
   const int64_t F = *nS;
-  const int64_t tiles = (F + kAw32Rows - 1) / kAw32Rows;
-  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const int64_t r0 = tile * kAw32Rows;
-    const int nrows = (int)min((int64_t)kAw32Rows, F - r0);
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / G, len = F * (b + 1) / G - rb;
+  const int ntile = (int)((len + kAw32Rows - 1) / kAw32Rows);
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int64_t r0 = rb + len * tile / ntile;
+    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
     // ---- slot lists and self-row indices of the tile
     for (int i = tid; i < kAw32Rows * T; i += kAw32Threads) {
       const int row = i / T, t = i - row * T;
@@ -309,37 +311,49 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
       }
     }
     __syncthreads();
-    // ---- projection: wave (kq, cg), k quarter kq, columns 32 cg ..
+    // ---- projection: wave (kq, cg), k quarter kq, columns 32 cg ..; split-bf16
+    // products (v_mfma_f32_32x32x16_bf16, six per 16-k step: A and W split into
+    // bf16 hi / mid / lo in registers, bf16split.h), 2.67x the fp32 MFMA rate:
+    // at fp32 MFMA the projection of a 32-row tile (8.4 MFLOP) held a CU ~14 us
     const int cg = wave & 3, kq = wave >> 2;
     const int l32 = lane & 31, hh = lane >> 5;
     const int kspan = K >> 2, kb = kq * kspan;
-    const float* wrow = W + (int64_t)(cg * 32 + l32) * K;
-    const float* arow = sA + l32 * lda;
+    const float* wrow = W + (int64_t)(cg * 32 + l32) * K + kb + 8 * hh;
+    const float* arow = sA + l32 * lda + kb + 8 * hh;
     aw_f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    // chunks of 4 k-octets (32 k); B fragments of chunk c+1 load while c runs
+    // chunks of two 16-k steps (32 k); W fragments of chunk c+1 load while c runs
     const int nch = kspan / 32;
     float4 bcur[4], bnxt[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) bcur[s] = *reinterpret_cast<const float4*>(wrow + kb + 8 * s + 4 * hh);
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bcur[2 * s2] = *reinterpret_cast<const float4*>(wrow + 16 * s2);
+      bcur[2 * s2 + 1] = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 4);
+    }
     for (int ch = 0; ch < nch; ++ch) {
-      const int k0 = kb + 32 * ch;
-      if (ch + 1 < nch) {
+      const int k0 = 32 * ch;
+      const int kn = ch + 1 < nch ? k0 + 32 : k0;  // (the last chunk reloads itself: no branch)
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          bnxt[s] = *reinterpret_cast<const float4*>(wrow + k0 + 32 + 8 * s + 4 * hh);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bnxt[2 * s2] = *reinterpret_cast<const float4*>(wrow + kn + 16 * s2);
+        bnxt[2 * s2 + 1] = *reinterpret_cast<const float4*>(wrow + kn + 16 * s2 + 4);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const float4 av = *reinterpret_cast<const float4*>(arow + k0 + 8 * s + 4 * hh);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bcur[s].x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bcur[s].y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bcur[s].z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bcur[s].w, acc, 0, 0, 0);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const float* ap = arow + k0 + 16 * s2;
+        bf16x8 aH, aM, aL, bH, bM, bL;
+        split3(*reinterpret_cast<const float4*>(ap), *reinterpret_cast<const float4*>(ap + 4), aH, aM, aL);
+        split3(bcur[2 * s2], bcur[2 * s2 + 1], bH, bM, bL);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) bcur[s] = bnxt[s];
+      for (int s2 = 0; s2 < 4; ++s2) bcur[s2] = bnxt[s2];
     }
     __syncthreads();  // every wave is done reading the A tile
     // ---- partial tiles -> LDS red[kq][row][col], fixed-order sum, epilogue
@@ -1198,6 +1212,8 @@ int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
          T >= 1 && T <= kAwTMax && 2 * lds <= 160 * 1024;
 }
 
+// S_max: the expected row count (the frontier size hint; the kernels read the
+// actual count from nS and deal it over their blocks)
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st) {
@@ -1215,9 +1231,17 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
-  const int64_t tiles = (S_max + kAwRows - 1) / kAwRows;
-  const int grid = (int)std::min<int64_t>(tiles, 2 * (int64_t)cus);
-  if (K >= 1024 && agg_w32_supported(d, hid, T)) {
+  // ~12 rows per block (a 16-row tile with headroom), two blocks per CU
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(2 * (int64_t)cus, (S_max + 11) / 12));
+  // The 32-row form (one block per CU, W read once per 32 rows) when the rows
+  // fill ~16 per CU; below that the 16-row form (two blocks per CU, one's gather
+  // beside the other's products) hides more latency.  Measured (bench.py):
+  // C2 layer 0 (5.7k rows, K 1024) 36.5 vs 55.3 us, C4 layer 0 (8.6k, K 640)
+  // 50.2 vs 73.4 us; the layers 1 (1.5-2k rows, K 640) 21.5-21.8 vs 24.7-25.3 us.
+  // PINSAGE_AGGW32_MIN_ROWS overrides the switch point (A/B).
+  const int64_t min_rows32 =
+      getenv("PINSAGE_AGGW32_MIN_ROWS") ? atoll(getenv("PINSAGE_AGGW32_MIN_ROWS")) : 16 * (int64_t)cus;
+  if (S_max >= min_rows32 && agg_w32_supported(d, hid, T)) {
     const int lds32 = kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
     static bool prepared32 = false;
     if (!prepared32) {
@@ -1225,8 +1249,9 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       prepared32 = true;
     }
-    const int64_t tiles32 = (S_max + kAw32Rows - 1) / kAw32Rows;
-    hipLaunchKernelGGL(agg_w32_kernel, dim3((int)std::min<int64_t>(tiles32, cus)), dim3(kAw32Threads), lds32,
+    // ~24 rows per block (a 32-row tile with headroom) over every CU
+    const int64_t g32 = std::max<int64_t>(1, std::min<int64_t>(cus, (S_max + 23) / 24));
+    hipLaunchKernelGGL(agg_w32_kernel, dim3((int)g32), dim3(kAw32Threads), lds32,
                        st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, W, bias, y, nrm, agg);
   } else {
     hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,

@@ -1275,7 +1275,10 @@ int launch_agg(const float* q, int hid, const int32_t* loc, const float* wloc, i
                const int* nS, int64_t S_max, float* agg, hipStream_t st) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "agg: hidden dim must be a multiple of 4");
   if (S_max <= 0) return kOk;
-  const bool sliced = !getenv("PINSAGE_AGG_SLICED") || atoi(getenv("PINSAGE_AGG_SLICED")) != 0;
+  // opt-in (PINSAGE_AGG_SLICED=1): in the step, where popular q rows repeat and
+  // hit L2 anyway, the sliced form measured slower (C2 layer 0 15.9 vs 13.6 us,
+  // C4 22.3 vs 19.1 us); on uniformly random slots it is faster (15.6 vs 20.3 us)
+  const bool sliced = getenv("PINSAGE_AGG_SLICED") && atoi(getenv("PINSAGE_AGG_SLICED")) != 0;
   if (sliced && (hid == 512 || hid == 256 || hid == 128)) {
     // 4 waves per block, blocks in groups of 8 (one per XCD slice), ~2 passes per wave
     const int rpw = 64 / (hid / 32);

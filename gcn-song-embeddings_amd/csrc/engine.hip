@@ -624,9 +624,10 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {
       // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
       Timed taw(E, lname("fwd.aggw", l), st);
+      const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
       PS_TRY(launch_agg_w(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q),
                           (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S),
-                          lb.S.cap, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
+                          S_est, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
                           at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
       continue;
     }
@@ -798,7 +799,11 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
 // Q0's Adam itself, and the weight-gradient stream updates every other
 // parameter (contiguous behind Q0 in the flat layout) once the main stream has
 // read W0 for the last time -- the optimizer pass is off the critical path.
-int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
+// stage -1: the whole backward; 0: the head and layers L-1 .. 1 (every
+// gradient but layer 0's is complete when the call's stream reaches its end);
+// 1: layer 0 (after a stage-0 call on the same workspace).  A data-parallel
+// step all-reduces stage 0's gradients while stage 1 runs.
+int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, int stage = -1) {
   const EngineConfig& c = E.cfg;
   PS_REQUIRE(E.grads, kErrArg, "engine: grad buffer not set");
   PS_REQUIRE(!adam || (E.adam_m && E.adam_v), kErrArg, "engine: optimizer state not set");
@@ -820,6 +825,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   hipStream_t s_wg0 = E.stream_mode == 4 ? E.side[1] : s_wg;
   // the CSR transposes were built with the frontier (engine_frontier)
   // weight gradients run on s_wg, each forked once its inputs exist on st
+  const bool dfr = (E.defer_side & 1) != 0;
+  PS_REQUIRE(stage < 0 || !adam, kErrArg, "engine: a staged backward runs without the fused optimizer");
+  if (stage <= 0) {
   Timed t_hb(E, "bwd.head", st);
   auto wgrad_g2 = [&]() -> int {  // dG2 = dZ^T H1 beside the chain
     Timed tw(E, "bwd.wgrad.g2", s_wg);
@@ -845,7 +853,6 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
   // normalisation backward (dp_top) in one kernel, which also zeroes the
   // loss's multiplicity counters (the dY scatter-add targets of the layers
   // below were zeroed by the forward's layer_prep)
-  const bool dfr = (E.defer_side & 1) != 0;
   if (E.fused_head) {
     // the head backward forms dZ = sum_c K[c] G[c] from the loss's
     // accumulators as it loads its rows (and zeroes them), writing dZ for dG2
@@ -904,7 +911,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam) {
     }));
   }
   t_hb.stop();
+  }
   for (int l = Lc - 1; l >= 0; --l) {
+    if ((stage == 0 && l == 0) || (stage == 1 && l != 0)) continue;
     Timed tb(E, lname("bwd.layer", l), st);
     LayerBuf& lb = E.L[(size_t)l];
     const int d = (int)lb.d;
@@ -1360,6 +1369,14 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
 
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream) {
   return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream, nullptr);
+}
+
+int pinsage_engine_backward_stage(pinsage_engine* e, void* ws, int stage, void* stream) {
+  if (stage != 0 && stage != 1) {
+    set_error("engine_backward_stage: stage 0 (head and layers L-1 .. 1) or 1 (layer 0)");
+    return kErrArg;
+  }
+  return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream, nullptr, stage);
 }
 
 int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, float beta1,

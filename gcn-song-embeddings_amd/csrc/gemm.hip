@@ -527,25 +527,55 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
         const int col = n0 + (wn * TN + j) * 32 + l32;
         bj[j] = (p.bias && col < N) ? p.bias[col] : 0.f;
       }
+      // Per 8 rows of a 32-row block: every load (scatter rows, lrelu' masks, the
+      // values an accumulate adds to) is issued before those rows' first store --
+      // loads interleaved with stores that may alias them were waited on one
+      // element at a time (vmcnt counts the stores too): the C2 layer-1
+      // scatter-adds of dh / dcat took ~30 us per launch
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (row >= M) continue;
-          const int64_t dst = p.c_idx ? p.c_idx[row] : row;
+        for (int r0 = 0; r0 < 16; r0 += 8) {
+          int dsts[8];
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int col = n0 + (wn * TN + j) * 32 + l32;
-            if (col >= N) continue;
-            float v = acc[i][j][r] + bj[j];
-            if (p.act) v = lrelu(v);
-            if (p.mask) v *= lrelu_grad(p.mask[(int64_t)row * p.ldm + col]);
-            if (p.c2 && col >= p.N1) {
-              p.c2[(int64_t)row * p.ldc2 + (col - p.N1)] = v;
-            } else {
-              float* o = p.c + dst * p.ldc + col;
-              *o = accum ? *o + v : v;
+          for (int r = 0; r < 8; ++r) {
+            const int row = m0 + (wm * TM + i) * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * h;
+            dsts[r] = row < M ? (p.c_idx ? p.c_idx[row] : row) : -1;
+          }
+          // pre: lrelu'(mask) with a mask, else the values an accumulate adds to
+          // (mask and accumulate together -- no caller -- reload the old value)
+          float pre[8][TN];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int row = m0 + (wm * TM + i) * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * h;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int col = n0 + (wn * TN + j) * 32 + l32;
+              const bool ok = dsts[r] >= 0 && col < N;
+              float x = 0.f;
+              if (p.mask) x = ok ? lrelu_grad(p.mask[(int64_t)row * p.ldm + col]) : 0.f;
+              else if (accum && !(p.c2 && col >= p.N1)) x = ok ? p.c[(int64_t)dsts[r] * p.ldc + col] : 0.f;
+              pre[r][j] = x;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int row = m0 + (wm * TM + i) * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * h;
+            if (row >= M) continue;
+            const int64_t dst = dsts[r];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int col = n0 + (wn * TN + j) * 32 + l32;
+              if (col >= N) continue;
+              float v = acc[i][j][r0 + r] + bj[j];
+              if (p.act) v = lrelu(v);
+              if (p.mask) v *= pre[r][j];
+              if (p.c2 && col >= p.N1) {
+                p.c2[(int64_t)row * p.ldc2 + (col - p.N1)] = v;
+              } else {
+                float* o = p.c + dst * p.ldc + col;
+                *o = accum ? (p.mask ? *o : pre[r][j]) + v : v;
+              }
             }
           }
         }

@@ -200,6 +200,25 @@ def batch_variance(h):
 
 
 # ----------------------------------------------------------------------------- data parallel
+def _allreduce_start(flat):
+    """Begin the mean of a flat gradient bucket over the process group, ordered
+    after the current stream's work; returns a handle for _allreduce_finish
+    (RCCL: asynchronous on its own stream, averaged in the collective; gloo:
+    synchronous, then scaled)."""
+    d = torch.distributed
+    if d.get_backend() == "nccl":
+        return d.all_reduce(flat, op=d.ReduceOp.AVG, async_op=True)
+    d.all_reduce(flat)
+    flat.mul_(1.0 / d.get_world_size())
+    return None
+
+
+def _allreduce_finish(work):
+    """The current stream waits for a bucket started by _allreduce_start."""
+    if work is not None:
+        work.wait()
+
+
 def average_gradients(flat):
     """Mean of a flat gradient buffer over the process group: ONE all-reduce
     (RCCL over xGMI on MI355X nodes; gloo on CPU)."""
@@ -267,7 +286,13 @@ class _FusedStep:
         self.m = self.v = None
         self.grads = None
         self._tuned = False
-        self.dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+        self.dist = (torch.distributed.is_available() and torch.distributed.is_initialized()
+                     and torch.distributed.get_world_size() > 1)
+        # data parallel: the backward runs in two stages (head and layers L-1..1,
+        # then layer 0) and the first stage's gradients are all-reduced while the
+        # second runs (PINSAGE_DP_BUCKETS=0: one all-reduce after the backward)
+        self.dp_buckets = os.environ.get("PINSAGE_DP_BUCKETS", "1") != "0"
+        self.comm = None
         # the device step is captured into hipGraphs and replayed
         self.use_graph = os.environ.get("PINSAGE_HIPGRAPH", "1") != "0"
         # Adam fused into the gradient reductions (0: separate optimizer pass)
@@ -392,9 +417,10 @@ class _FusedStep:
         nat.check(nat.lib().pinsage_engine_frontier(e.h, nat.ptr(self.wss[q]), nat.ptr(self.ids_view[q]),
                                                     3 * B, nat.stream_ptr()), "frontier")
 
-    def _main(self, B, p, with_adam, before_backward=None):
+    def _main(self, B, p, with_adam, before_backward=None, stage=None):
         """Layers, head, loss, backward (and Adam) of workspace p's frontier;
-        before_backward() is called (to fork work) between loss and backward."""
+        before_backward() is called (to fork work) between loss and backward.
+        stage=0: the backward's first stage only (_dp_tail runs the rest)."""
         tr = self.tr
         e = self.runner.engine
         st = nat.stream_ptr()
@@ -406,7 +432,44 @@ class _FusedStep:
             self._tuned = True
         if before_backward is not None:
             before_backward()
+        if stage == 0:
+            nat.check(L.pinsage_engine_backward_stage(e.h, nat.ptr(self.wss[p]), 0, st), "backward_stage")
+            return
         self._backward(p, with_adam)
+
+    def _dp_split(self):
+        """Flat offset of layer 1's first parameter: [0, split) are layer 0's
+        gradients (the backward's last stage), [split, n) the rest."""
+        return sum(p.numel() for p in self.runner.params()[:4])
+
+    def _dp_tail(self, p, g2):
+        """Data-parallel end of a step whose first backward stage is enqueued:
+        all-reduce that stage's gradients (head and layers L-1..1) on a comm
+        stream while layer 0's backward runs (graph g2, or eagerly), then layer
+        0's bucket, then Adam on the averaged gradients (pinsage_training.py:
+        188-191 with the gradients averaged over the ranks)."""
+        cur = torch.cuda.current_stream()
+        if self.comm is None:
+            self.comm = torch.cuda.Stream()
+        split = self._dp_split()
+        bucket_a, bucket_b = self.grads[split:], self.grads[:split]
+        self.comm.wait_stream(cur)
+        with torch.cuda.stream(self.comm):
+            wa = _allreduce_start(bucket_a)
+        if g2 is not None:
+            g2.replay()
+        else:
+            e = self.runner.engine
+            nat.check(nat.lib().pinsage_engine_backward_stage(e.h, nat.ptr(self.wss[p]), 1, nat.stream_ptr()),
+                      "backward_stage")
+            self._publish(p)
+        self.comm.wait_stream(cur)
+        with torch.cuda.stream(self.comm):
+            wb = _allreduce_start(bucket_b)
+            _allreduce_finish(wa)
+            _allreduce_finish(wb)
+        cur.wait_stream(self.comm)
+        self._adam(p)
 
     def _backward(self, p, with_adam):
         """Backward; with_adam: Adam fused into the gradient reductions
@@ -538,17 +601,28 @@ class _FusedStep:
         step graph whose branch stages the predicted next ids into workspace
         1-p and computes their frontier there."""
         adam = not self.dist
+        staged = self.dist and self.dp_buckets  # DP: backward stage 1 in its own graph (g2)
+        stage = 0 if staged else None
         side = torch.cuda.Stream()
         graphs = []
         for p in (0, 1):
-            gf, gm, ga = (torch.cuda.CUDAGraph() for _ in range(3))
+            gf, gm, ga, g2 = (torch.cuda.CUDAGraph() for _ in range(4))
             with torch.cuda.graph(gf):
                 self._stage(B, self.slot_ids, p, None)
                 self._frontier(B, p)
             with torch.cuda.graph(gm):
                 self._stage(B, 0, None, p)
-                self._main(B, p, with_adam=adam)
-                self._publish(p)
+                self._main(B, p, with_adam=adam, stage=stage)
+                if not staged:
+                    self._publish(p)
+            if staged:
+                with torch.cuda.graph(g2):
+                    e = self.runner.engine
+                    nat.check(nat.lib().pinsage_engine_backward_stage(e.h, nat.ptr(self.wss[p]), 1,
+                                                                      nat.stream_ptr()), "backward_stage")
+                    self._publish(p)
+            else:
+                g2 = None
             with torch.cuda.graph(ga):
                 cur = torch.cuda.current_stream()
 
@@ -560,9 +634,9 @@ class _FusedStep:
                 # the next step's ids go to workspace 1-p, whose last user
                 # (the previous step) is done: graph launches are stream-ordered
                 self._stage(B, self.slot_next, 1 - p, p)
-                if self.ahead_mode == "start":
+                if self.ahead_mode == "start" or staged:
                     fork_next_frontier()
-                    self._main(B, p, with_adam=adam)
+                    self._main(B, p, with_adam=adam, stage=stage)
                 elif self.ahead_mode == "fwd":  # forked inside, after the layer-0 Q projection
                     side.wait_stream(cur)
                     e = self.runner.engine
@@ -576,8 +650,9 @@ class _FusedStep:
                 else:  # beside the backward: a latency-bound chain with CUs to spare
                     self._main(B, p, with_adam=adam, before_backward=fork_next_frontier)
                 cur.wait_stream(side)
-                self._publish(p)
-            graphs.append((gf, gm, ga))
+                if not staged:
+                    self._publish(p)
+            graphs.append((gf, gm, ga, g2))
         self.graphs = graphs
         self.graph_B = B
         self.graph_sig = sig
@@ -638,8 +713,10 @@ class _FusedStep:
             self.ring_ev[k].synchronize()
         self._slot_write_coef(k)
         _tick("slot_wait")
+        staged = self.dist and self.dp_buckets
+        staged_done = False  # the eager path below runs its own staged tail
         if self.graphs is not None:
-            gf, gm, ga = self.graphs[p]
+            gf, gm, ga, g2 = self.graphs[p]
             pend = self.pending[p]
             if pend is not None and np.array_equal(pend, batch.reshape(B, 3).cpu().numpy()):
                 self.ahead_hits += 1
@@ -673,12 +750,19 @@ class _FusedStep:
                 # the probes' backward scatter-added into this frontier's dY
                 # targets, which only the frontier (layer_prep) zeroes: redo it
                 self._frontier(B, p)
-            self._main(B, p, with_adam=not self.dist)
-            self._publish(p)
+            self._main(B, p, with_adam=not self.dist, stage=0 if staged else None)
+            if staged:
+                self._dp_tail(p, None)
+            else:
+                self._publish(p)
             self.pending = [None, None]
             if self.use_graph and self._tuned:
                 self._capture(B, sig)
-        if self.dist:
+            g2 = None
+            staged_done = staged
+        if self.dist and staged and not staged_done:
+            self._dp_tail(p, g2)
+        elif self.dist and not staged:
             average_gradients(self.grads)
             self._adam(p)
         ev = torch.cuda.Event()
@@ -844,25 +928,55 @@ class PinSage:
            distinct id's cotangent enters exactly once); parameter gradients add
            up over slices as they would inside one backward.
         Then torch's Adam.  Costs one extra forward per step."""
-        m = int(self.micro_batch)
         model = self.model
-        runner = model.runner()
-        dev = runner.dev
+        dev = model.runner().dev
         out = model.out_dim
         batch = torch.as_tensor(batch).to(torch.int64)
         B = int(batch.shape[0])
-        n = int(self.n)
         ids = batch.t().contiguous().to(dev)  # [3, B]: the q, pos and neg calls
-        Z = torch.empty((3, B, out), dtype=torch.float32, device=dev)
-        with torch.no_grad():
-            for j in range(0, B, m):
-                part = ids[:, j:j + m]
-                Z[:, j:j + m] = model(self.features, part.reshape(-1)).view(3, -1, out)
+        Z = self._micro_forward(ids)
         self.last_outputs = Z  # [3, B, out] rows the loss read (tests pin them)
         Zr = Z.detach().requires_grad_()
         with torch.enable_grad():
             loss = max_margin_loss(Zr[0], Zr[1], Zr[2], self.margin)
             (g,) = torch.autograd.grad(loss, [Zr])
+        self._micro_backward(ids, g)
+        self._average_param_grads()
+        self.optimizer.step()
+        norm = torch.nn.functional.normalize
+        f = self.features
+        bq = batch.to(f.device)
+        node_feat_loss = COSINE_TRIPLET_LOSS(norm(f[bq[:, 0]], dim=1), norm(f[bq[:, 1]], dim=1),
+                                             norm(f[bq[:, 2]], dim=1))
+        variance = batch_variance(Z[0])
+        return loss.detach(), node_feat_loss, variance
+
+    def _micro_forward(self, ids):
+        """Outputs [3, B, out] of the three calls over ids [3, B], slice by slice
+        (nothing kept)."""
+        m = int(self.micro_batch)
+        model = self.model
+        B = int(ids.shape[1])
+        Z = torch.empty((3, B, model.out_dim), dtype=torch.float32, device=ids.device)
+        with torch.no_grad():
+            for j in range(0, B, m):
+                part = ids[:, j:j + m]
+                Z[:, j:j + m] = model(self.features, part.reshape(-1)).view(3, -1, model.out_dim)
+        return Z
+
+    def _micro_backward(self, ids, g):
+        """Parameter gradients of the three calls over ids [3, B] under the
+        cotangent g [3, B, out] of their outputs, slice by slice with recompute:
+        a call's repeated id gets K x (its rows' summed cotangent) (index_put,
+        pinsage_model.py:257-265), summed over the calls into one cotangent per
+        distinct id, which enters with the first slice holding that id."""
+        m = int(self.micro_batch)
+        model = self.model
+        runner = model.runner()
+        dev = runner.dev
+        out = model.out_dim
+        B = int(ids.shape[1])
+        n = int(self.n)
         g = g.reshape(3 * B, out)
         flat = ids.reshape(-1)
         call = torch.arange(3, device=dev).repeat_interleave(B)
@@ -883,15 +997,6 @@ class PinSage:
             d = torch.where((first[su] == j // m)[:, None], D[su], torch.zeros((), device=dev))
             y = model(self.features, u)
             torch.autograd.backward([y], [d])
-        self._average_param_grads()
-        self.optimizer.step()
-        norm = torch.nn.functional.normalize
-        f = self.features
-        bq = batch.to(f.device)
-        node_feat_loss = COSINE_TRIPLET_LOSS(norm(f[bq[:, 0]], dim=1), norm(f[bq[:, 1]], dim=1),
-                                             norm(f[bq[:, 2]], dim=1))
-        variance = batch_variance(Z[0])
-        return loss.detach(), node_feat_loss, variance
 
     def train(self):
         from tqdm import tqdm

@@ -368,6 +368,11 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
                                    void* stream);
 /* all parameter gradients from dZ into the grad buffer (overwritten) */
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
+/* the same backward in two calls, for data-parallel steps that all-reduce the
+ * first call's gradients while the second runs (pinsage_training.py:188-191
+ * under DP): stage 0 = the head and layers L-1 .. 1 (every gradient but layer
+ * 0's is complete in stream order at the call's end), stage 1 = layer 0. */
+int pinsage_engine_backward_stage(pinsage_engine* e, void* ws, int stage, void* stream);
 /* torch.optim.Adam step over the flat buffers (pinsage_training.py:147,191).
  * coef: device f32[2] = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} for this step
  * t, computed by the caller in double as torch does (kept in device memory so

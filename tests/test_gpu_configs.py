@@ -125,6 +125,35 @@ def test_fixed_cotangent_reference_init(L, T):
     fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), L, T, seed=L * 10 + T)
 
 
+def test_fixed_cotangent_c1_shape():
+    """The C1 flow's exact model shape (dataset_micro through dashboard.py:
+    d_in 512, 1 layer, fanout 3, batch 32 -- 32 ids per call, repeats included)
+    under a fixed random cotangent at the reference init: forward rows and every
+    gradient within 1e-4 of the oracle (test_gpu_dashboard.py holds the flow's
+    hinge-conditioned gradient to 1e-3; this pins its kernels at 1e-4)."""
+    import graph
+    import pinsage_model as pm
+    import synthetic
+    n = 4324  # dataset_micro's track count
+    pg = synthetic.make_playlist_graph(n, 1100, 60000, seed=17)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices)
+    feats = torch.from_numpy(synthetic.make_features(n, 512, seed=18))
+    pm.set_rng_mode("philox")
+    try:
+        torch.manual_seed(0)
+        w, nb = pm.precompute_neighborhoods_topt(g, n, 500, 0.85, 100, None)
+    finally:
+        pm.set_rng_mode("mt19937")
+    rng = np.random.default_rng(3)
+    for trial in range(3):
+        ids = rng.integers(0, n, 32)
+        ids[5] = ids[0]
+        torch.manual_seed(4 + trial)
+        m = pm.PinSageModel(g, n, 1, (512, 512, 128), 500, 0.85, 3, (w, nb))
+        fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), 1, 3, seed=40 + trial)
+
+
 # ----------------------------------------------------------------------------- full size
 def _full(cfg):
     """bench.py's config (the graph the benchmark trains on), batch = its global batch."""

@@ -82,6 +82,38 @@ def test_micro_batched_step_c5_shape_vs_oracle(tmpdir_cwd):
     assert res["grad_rel_A_max"] <= 1e-3, res
 
 
+def test_micro_batched_backward_fixed_cotangent_c5_shape(tmpdir_cwd):
+    """The micro-batched step's backward (PinSage._micro_backward: slices of 16
+    triples with recompute, repeated ids inside and across slices) at the C5
+    shape (3 layers, fanout 50, d_in 256) and the reference init, under a fixed
+    random cotangent on the three calls' outputs: every parameter gradient
+    within 1e-4 of the oracle's autograd (pinsage_model.py:246-265 per call,
+    index_put's repeated-id semantics).  The random cotangent removes the
+    hinge's conditioning (test_micro_batched_step_c5_shape_vs_oracle), so this
+    pins the sliced kernels themselves at the north star's tolerance."""
+    from oracle import oracle as orc
+    n = 4000
+    g, feats, pos, w, nb = _problem(tmpdir_cwd, n, 1000, 50000, 256, seed=21)
+    tr = make_trainer(g, n, feats.cuda(), pos, 3, 50, 64, margin=1e-5, seed=7)
+    tr.micro_batch = 16
+    b = _batch_with_repeats(tr, 8)
+    B = b.shape[0]
+    init = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()}
+    c = torch.from_numpy(np.random.default_rng(5).standard_normal((3, B, tr.out_dim)).astype(np.float32))
+    ids = b.t().contiguous().cuda()
+    tr._micro_backward(ids, c.cuda())
+    torch.cuda.synchronize()
+    p = {k: v.float().requires_grad_() for k, v in init.items()}
+    tot = 0.0
+    for j in range(3):
+        y = orc.model_forward(p, feats, b[:, j].numpy(), 3, 50, w.numpy(), nb.numpy(), tr.out_dim)
+        tot = tot + (y * c[j]).sum()
+    tot.backward()
+    errs = {k: parity_util.rel(prm.grad.cpu().numpy(), p[k].grad.numpy())
+            for k, prm in tr.model.named_parameters()}
+    assert max(errs.values()) <= 1e-4, errs
+
+
 @pytest.mark.parametrize("L,T,m", [(2, 10, 7), (3, 50, 16)])
 def test_micro_batched_step_equals_fused_step(tmpdir_cwd, L, T, m):
     """The sliced step against the one-launch fused step on the same batch and
