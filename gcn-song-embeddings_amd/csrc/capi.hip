@@ -36,17 +36,9 @@ int launch_mark_table_i64(unsigned long long*, const int64_t*, int64_t, const in
                           int, int64_t, int*, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
-int agg_w3_supported(int64_t, int64_t, int64_t, int64_t);
-int launch_split_w_frag(const float*, int64_t, uint16_t*, hipStream_t);
-int launch_reorder_w_frag(const float*, int64_t, float*, hipStream_t);
-int launch_agg_w4(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
-                  const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*,
-                  float*, float*, hipStream_t);
-int launch_agg_w5(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*, const float*, int,
-                  const int*, int64_t, int64_t, const float*, const float*, float*, float*, float*, hipStream_t);
-int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
-                  const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
-                  float*, float*, hipStream_t);
+int agg_w_supported(int64_t, int64_t, int64_t, int64_t);
+int launch_agg_w(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*, const float*, int,
+                 const int*, int64_t, int64_t, const float*, const float*, float*, float*, float*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_gather_rows(const float*, int64_t, int64_t, int, const int64_t*, int64_t, float*, int64_t,
@@ -563,27 +555,17 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
                              const float* w, int64_t n_rows, int64_t T, const float* W,
                              const float* bias, int64_t out, uint16_t* W_planes, float* y,
                              float* norms, float* agg, void* stream) {
-  if (!agg_w3_supported(d, hid, out, T) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX) {
-    set_error("conv_agg_project: out_dim must be 128, d and hid multiples of 32, 1 <= T <= 64");
+  (void)W_planes;  // (scratch of an earlier kernel form; unused)
+  if (!agg_w_supported(d, hid, out, T) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX || ldh < d ||
+      ldh % 4 != 0) {
+    set_error("conv_agg_project: out_dim must be 128, d + hid a multiple of 64, d and hid multiples of 4, "
+              "1 <= T <= 64");
     return kErrArg;
   }
-  hipStream_t st = (hipStream_t)stream;
-  // the in-wave pipelined form (C2 layer-0 shape: 44.0 us incl. the split vs 49.5
-  // for the warp-specialised form, tools/aggw_bench.py); PINSAGE_FUSED_AGGW=2 for that one
-  const int form = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 3;
-  if (form == 5)
-    return launch_agg_w5(h, ldh, (int)d, self_src, q, (int)hid, loc, w, (int)T, nullptr, n_rows, n_rows, W, bias,
-                         y, norms, agg, st);
-  if (form != 2) {
-    PS_TRY(launch_split_w_frag(W, d + hid, W_planes, st));
-    return launch_agg_w3(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows,
-                         n_rows, W_planes, bias, y, norms, agg, st);
-  }
-  // the warp-specialised form: W reordered (fp32, 4 * out * (d + hid) bytes of the scratch)
-  float* Wr = reinterpret_cast<float*>(W_planes);
-  PS_TRY(launch_reorder_w_frag(W, d + hid, Wr, st));
-  return launch_agg_w4(h, ldh, (int)d, self_src, q, (int)hid, q_rows, loc, w, (int)T, nullptr, n_rows, n_rows,
-                       Wr, bias, y, norms, agg, st);
+  if (n_rows == 0) return kOk;
+  // the engine's kernel (aggw.hip): the form by row count, rows from n_rows
+  return launch_agg_w(h, ldh, (int)d, self_src, q, (int)hid, loc, w, (int)T, nullptr, n_rows, n_rows, W, bias, y,
+                      norms, agg, (hipStream_t)stream);
 }
 
 int pinsage_gather_rows(const float* h, int64_t ldh, int64_t n_h, int64_t d, const int64_t* idx, int64_t n,

@@ -57,19 +57,8 @@ int launch_loss(const float*, int, const int32_t*, int, float, const float*, int
 int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
 int agg_w_supported(int64_t, int64_t, int64_t, int64_t);
 int launch_agg_w(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*,
-                 const float*, int, const int*, int64_t, const float*, const float*, float*, float*,
+                 const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*, float*,
                  float*, hipStream_t);
-int agg_w3_supported(int64_t, int64_t, int64_t, int64_t);
-int launch_split_w_frag(const float*, int64_t, uint16_t*, hipStream_t);
-int launch_reorder_w_frag(const float*, int64_t, float*, hipStream_t);
-int launch_agg_w4(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
-                  const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*,
-                  float*, float*, hipStream_t);
-int launch_agg_w5(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*, const float*, int,
-                  const int*, int64_t, int64_t, const float*, const float*, float*, float*, float*, hipStream_t);
-int launch_agg_w3(const float*, int64_t, int, const int32_t*, const float*, int, int64_t, const int32_t*,
-                  const float*, int, const int*, int64_t, int64_t, const uint16_t*, const float*, float*,
-                  float*, float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
                 hipStream_t);
 int csr_prepare();
@@ -106,7 +95,6 @@ struct LayerBuf {
   size_t self_src = 0, q_src = 0, loc = 0, wloc = 0;
   size_t q = 0, agg = 0, y = 0, nrm = 0;
   size_t qsplit = 0;  // the Q weight's hi / mid / lo bf16 planes (split-bf16 Q projection)
-  size_t wsplit = 0;  // the W weight's planes (the aggregation + projection kernel's B operand)
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
          occ2 = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
@@ -143,11 +131,9 @@ struct Engine {
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B);
-  // 1 (default): the round-2 fused kernel (fp32 MFMA after the gather); 2: the
-  // warp-specialised gather / split-bf16 projection kernel (agg_w4_kernel); 3:
-  // the in-wave pipelined form (agg_w3_kernel), where their shapes are supported.
-  // Measured in the C2 step (bench.py, one box): 1: layer 0 41.5 us, layer 1
-  // 22.9 us, 0.458 ms/step; 2: 48.2 / 31.3 us, 0.476 ms; 3: 39.7 / 30.3 us, 0.470 ms.
+  // 1 (default): one launch (aggw.hip).  Experimental forms measured slower and
+  // removed: register-pipelined split-bf16 (C2 layer 0 39.7 us),
+  // warp-specialised on LDS-DMA (45.8) or on registers (41.4), against 36.5.
   int fused_aggw = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 1;
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
@@ -377,7 +363,6 @@ static void layout(Engine& E) {
     lb.wloc = carve(cur, FS * T * 4);
     lb.q = carve(cur, FN * c.hid * 4);
     lb.qsplit = carve(cur, 3 * c.hid * lb.d * 2);
-    lb.wsplit = carve(cur, 3 * c.out * (lb.d + c.hid) * 2);
     lb.agg = carve(cur, FS * c.hid * 4);
     lb.y = carve(cur, FS * c.out * 4);
     lb.nrm = carve(cur, FS * 4);
@@ -536,25 +521,6 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   const int Lc = (int)c.n_layers, T = (int)c.T;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
-  auto use_aggw3 = [&](const LayerBuf& lb) {
-    return (E.fused_aggw == 2 || E.fused_aggw == 3) && agg_w3_supported(lb.d, c.hid, c.out, T) &&
-           lb.N.cap * c.hid * 4 < (1LL << 31);
-  };
-  auto use_aggw5 = [&](const LayerBuf& lb) {
-    return E.fused_aggw == 5 && agg_w3_supported(lb.d, c.hid, c.out, T);
-  };
-  // the W weights' bf16 planes for the aggregation + projection kernel (the
-  // parameters change every step: split once per forward, off the chain's
-  // inputs -- nothing here depends on the frontier)
-  for (int l = 0; l < Lc; ++l) {
-    LayerBuf& lb = E.L[(size_t)l];
-    if (!use_aggw3(lb)) continue;
-    Timed ts(E, lname("fwd.w_split", l), st);
-    if (E.fused_aggw == 3)
-      PS_TRY(launch_split_w_frag(E.params + lb.pWw, lb.d + c.hid, at<uint16_t>(ws, lb.wsplit), st));
-    else
-      PS_TRY(launch_reorder_w_frag(E.params + lb.pWw, lb.d + c.hid, at<float>(ws, lb.wsplit), st));
-  }
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
@@ -595,38 +561,12 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(dep(E, st, E.fork.stream));
       PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
     }
-    if (use_aggw5(lb)) {
-      // LDS-DMA gather warp-specialised against the split-bf16 projection, bias, lrelu, L2 norm
-      Timed taw(E, lname("fwd.aggw", l), st);
-      const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
-      PS_TRY(launch_agg_w5(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
-                           at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0, S_est,
-                           E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y), at<float>(ws, lb.nrm),
-                           at<float>(ws, lb.agg), st));
-      continue;
-    }
-    if (use_aggw3(lb)) {
-      // aggregation pipelined with the split-bf16 projection, bias, lrelu, L2 norm
-      Timed taw(E, lname("fwd.aggw", l), st);
-      const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
-      if (E.fused_aggw == 3)
-        PS_TRY(launch_agg_w3(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
-                             lb.N.cap, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0, S_est,
-                             at<uint16_t>(ws, lb.wsplit), E.params + lb.pWb, at<float>(ws, lb.y),
-                             at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
-      else
-        PS_TRY(launch_agg_w4(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q), (int)c.hid,
-                             lb.N.cap, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0, S_est,
-                             at<float>(ws, lb.wsplit), E.params + lb.pWb, at<float>(ws, lb.y),
-                             at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
-      continue;
-    }
     if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {
       // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
       Timed taw(E, lname("fwd.aggw", l), st);
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
       PS_TRY(launch_agg_w(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q),
-                          (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S),
+                          (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0,
                           S_est, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
                           at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
       continue;

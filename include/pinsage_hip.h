@@ -204,11 +204,11 @@ int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const 
  *   agg[f]  = sum_t w[f][t] * q[loc[f][t]]                     (:202, w normalised)
  *   y[f]    = normalize(lrelu([h[self_src[f]] || agg[f]] W^T + bias))   (:208-210)
  *   norms[f] = ||lrelu(.)||_2 (nullable)
- * in one launch: the aggregation pipelined with the projection on split-bf16
- * MFMA (W is split into W_planes, device scratch of 3*out*(d+hid) uint16, first).
- * h f32 [.][ldh], q f32 [q_rows][hid], loc int32 / w f32 [n_rows][T], W f32
- * [out][d+hid], y f32 [n_rows][out], agg f32 [n_rows][hid].  out == 128, d and
- * hid multiples of 32, 1 <= T <= 64, q_rows*hid*4 < 2^31. */
+ * in one launch (the engine's kernel): the aggregate staged in LDS and written
+ * out once, the projection on split-bf16 MFMA.  h f32 [.][ldh], q f32
+ * [q_rows][hid], loc int32 / w f32 [n_rows][T], W f32 [out][d+hid], y f32
+ * [n_rows][out], agg f32 [n_rows][hid].  out == 128, d + hid a multiple of 64,
+ * d and hid multiples of 4, 1 <= T <= 64.  W_planes is unused (may be null). */
 int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32_t* self_src,
                              const float* q, int64_t hid, int64_t q_rows, const int32_t* loc,
                              const float* w, int64_t n_rows, int64_t T, const float* W,

@@ -66,11 +66,11 @@ CASES = [  # n_rows, d, ldh, hid, T, U (q rows), n_h (h rows)
 ]
 
 
-@pytest.fixture(params=["3", "5"])
+@pytest.fixture(params=["0", "1000000000"])
 def form(request, monkeypatch):
-    """the kernel form behind pinsage_conv_agg_project: 3 in-wave pipelined,
-    5 warp-specialised with the gather on LDS-DMA (read per call)"""
-    monkeypatch.setenv("PINSAGE_FUSED_AGGW", request.param)
+    """the kernel form behind pinsage_conv_agg_project: the 32-row form (one
+    block per CU) from PINSAGE_AGGW32_MIN_ROWS rows on, else the 16-row form"""
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", request.param)
     return request.param
 
 

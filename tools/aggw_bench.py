@@ -84,7 +84,7 @@ def main():
                               "us": round(us, 2), "alg_frac_hbm": round(alg / us / 1e3 / 8000, 3),
                               "logical_TBs": round(logical / us / 1e6, 2)}), flush=True)
             continue
-        print(json.dumps({"shape": name, "form": os.environ.get("PINSAGE_FUSED_AGGW", "3"), "F": F, "d": d, "T": T, "U": U, "us": round(us, 2),
+        print(json.dumps({"shape": name, "F": F, "d": d, "T": T, "U": U, "us": round(us, 2),
                           "note": "includes the W split launch",
                           "alg_GBs": round(alg / us / 1e3, 1), "alg_frac_hbm": round(alg / us / 1e3 / 8000, 3),
                           "logical_TBs": round(logical / us / 1e6, 2),
