@@ -75,7 +75,7 @@ def main():
         times.sort()
         us = times[len(times) // 2]
         distinct = min(U, F * T)
-        alg = distinct * hid * 4 + F * T * 8 + F * d * 4 + 3 * 128 * (d + hid) * 2 + F * (hid + 129) * 4
+        alg = distinct * hid * 4 + F * T * 8 + F * d * 4 + 128 * (d + hid) * 4 + F * (hid + 129) * 4
         logical = F * T * hid * 4 + F * T * 8 + F * d * 4 + F * (hid + 129) * 4
         if args.agg_only:
             alg = distinct * hid * 4 + F * T * 8 + F * hid * 4
@@ -85,7 +85,6 @@ def main():
                               "logical_TBs": round(logical / us / 1e6, 2)}), flush=True)
             continue
         print(json.dumps({"shape": name, "F": F, "d": d, "T": T, "U": U, "us": round(us, 2),
-                          "note": "includes the W split launch",
                           "alg_GBs": round(alg / us / 1e3, 1), "alg_frac_hbm": round(alg / us / 1e3 / 8000, 3),
                           "logical_TBs": round(logical / us / 1e6, 2),
                           "tflops": round(2 * F * (d + hid) * 128 / us / 1e6, 1)}), flush=True)
