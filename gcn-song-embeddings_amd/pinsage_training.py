@@ -302,6 +302,8 @@ class _FusedStep:
         self.ahead_mode = mode
         self.graphs = None
         self.graph_B = None
+        self.side = None
+        self.gfr = None
         self.parity = 0
         self.ahead_hits = 0
         # in-context GEMM tuner (see _autotune); PINSAGE_AUTOTUNE=0 keeps the size model
@@ -499,7 +501,7 @@ class _FusedStep:
     # per-site candidates: (cfg, stream_k, splits); a GEMM site takes a block-tile
     # config with or without stream-K, a weight-gradient site a config and a split-K count
     _GEMM_OPTS = [(c, k, 0) for c in (0, 1, 2, 3) for k in (0, 1) if not (c == 0 and k == 1)]
-    _WGRAD_OPTS = [(c, -1, sp) for c in (0, 1, 2) for sp in (1, 2, 4, 8, 16, 32)]
+    _WGRAD_OPTS = [(c, -1, sp) for c in (0, 1, 2) for sp in (2, 4, 8, 16, 32, 64)]
 
     def _gemm_sites(self):
         sites = []
@@ -604,12 +606,22 @@ class _FusedStep:
         staged = self.dist and self.dp_buckets  # DP: backward stage 1 in its own graph (g2)
         stage = 0 if staged else None
         side = torch.cuda.Stream()
+        split = self.ahead_mode == "split"
+        if split:
+            if self.side is None:
+                self.side = torch.cuda.Stream()
+            self.gfr = []
         graphs = []
         for p in (0, 1):
             gf, gm, ga, g2 = (torch.cuda.CUDAGraph() for _ in range(4))
             with torch.cuda.graph(gf):
                 self._stage(B, self.slot_ids, p, None)
                 self._frontier(B, p)
+            if split:  # the frontier alone: a linear graph, replayed on self.side
+                gfr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gfr):
+                    self._frontier(B, p)
+                self.gfr.append(gfr)
             with torch.cuda.graph(gm):
                 self._stage(B, 0, None, p)
                 self._main(B, p, with_adam=adam, stage=stage)
@@ -634,7 +646,19 @@ class _FusedStep:
                 # the next step's ids go to workspace 1-p, whose last user
                 # (the previous step) is done: graph launches are stream-ordered
                 self._stage(B, self.slot_next, 1 - p, p)
-                if self.ahead_mode == "start" or staged:
+                if split:  # the step alone; _call stages and forks the frontier
+                    self._main(B, p, with_adam=adam, stage=stage)
+                elif self.ahead_mode == "late":
+                    # forked at the start like "start", but captured after
+                    # the main chain (the runtime dispatches a multi-stream
+                    # graph's nodes in capture order)
+                    fork_ev = torch.cuda.Event()
+                    fork_ev.record(cur)
+                    self._main(B, p, with_adam=adam, stage=stage)
+                    side.wait_event(fork_ev)
+                    with torch.cuda.stream(side):
+                        self._frontier(B, 1 - p)
+                elif self.ahead_mode == "start" or staged:
                     fork_next_frontier()
                     self._main(B, p, with_adam=adam, stage=stage)
                 elif self.ahead_mode == "fwd":  # forked inside, after the layer-0 Q projection
@@ -649,7 +673,8 @@ class _FusedStep:
                         nat.lib().pinsage_engine_set_fork(e.h, None, None, 0, None)
                 else:  # beside the backward: a latency-bound chain with CUs to spare
                     self._main(B, p, with_adam=adam, before_backward=fork_next_frontier)
-                cur.wait_stream(side)
+                if not split:
+                    cur.wait_stream(side)
                 if not staged:
                     self._publish(p)
             graphs.append((gf, gm, ga, g2))
@@ -715,6 +740,7 @@ class _FusedStep:
         _tick("slot_wait")
         staged = self.dist and self.dp_buckets
         staged_done = False  # the eager path below runs its own staged tail
+        join = None  # split look-ahead: the side stream's frontier
         if self.graphs is not None:
             gf, gm, ga, g2 = self.graphs[p]
             pend = self.pending[p]
@@ -728,7 +754,22 @@ class _FusedStep:
             _tick("peek")
             if nxt is not None:
                 self._slot_write_ids(k, self.slot_next, nxt, B)
-                ga.replay()
+                if self.ahead_mode == "split":
+                    # stage (next ids -> workspace 1-p, coefficients -> p),
+                    # then the step's graph here and the next frontier's on
+                    # the side stream; the next step waits for the latter
+                    cur = torch.cuda.current_stream()
+                    self._stage(B, self.slot_next, 1 - p, p)
+                    fork = torch.cuda.Event()
+                    fork.record(cur)
+                    ga.replay()
+                    self.side.wait_event(fork)
+                    with torch.cuda.stream(self.side):
+                        self.gfr[1 - p].replay()
+                    join = torch.cuda.Event()
+                    join.record(self.side)
+                else:
+                    ga.replay()
             else:
                 gm.replay()
             self.pending[1 - p] = nxt
@@ -765,6 +806,8 @@ class _FusedStep:
         elif self.dist and not staged:
             average_gradients(self.grads)
             self._adam(p)
+        if join is not None:  # the next step reads the look-ahead frontier
+            torch.cuda.current_stream().wait_event(join)
         ev = torch.cuda.Event()
         ev.record()
         self.ring_ev[k] = ev

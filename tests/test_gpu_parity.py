@@ -339,9 +339,11 @@ def test_fused_adam_matches_backward_plus_adam():
             os.chdir(cwd)
 
 
-def test_frontier_ahead_matches_serial_step():
+@pytest.mark.parametrize("mode", ["start", "split", "late"])
+def test_frontier_ahead_matches_serial_step(mode):
     """The step graph that also computes the next batch's frontier (from the
-    sampler's speculative draw) trains exactly like the serial step: same
+    sampler's speculative draw; each PINSAGE_FRONTIER_AHEAD placement of that
+    branch) trains exactly like the serial step: same
     losses and parameters (within rounding: the CSR fill order uses atomics),
     with look-ahead hits; a batch that is not the predicted one (here a
     caller-made batch) falls back to its own frontier first."""
@@ -366,6 +368,8 @@ def test_frontier_ahead_matches_serial_step():
                 tr.batch_size = 256
                 tr._fused = f = pt._FusedStep(tr)
                 f.ahead = ahead
+                f.ahead_mode = mode
+                f.autotune = False  # the same GEMM choices in both runs
                 torch.manual_seed(6)
                 losses = []
                 for s in range(6):

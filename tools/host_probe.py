@@ -1,4 +1,5 @@
-"""Is the train loop host-bound?  Times the C2 loop as bench.py does, then
+"""Is the train loop host-bound?  Times a config's loop (argv[1], default
+c2) as bench.py does, then
 again with an extra GPU sleep kernel of known length per step: if the step
 grows by the sleep, the GPU is the bottleneck (the host keeps ahead); if it
 does not, the host's enqueue rate is."""
@@ -15,7 +16,7 @@ import bench  # noqa: E402
 
 
 def main():
-    cfg = bench.CONFIGS["c2"]
+    cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
     import pinsage_training as pt
     pg, g, feats, pos = bench.build_problem(cfg)
     nbhds, _ = bench.precompute(g, cfg, "philox")
@@ -59,6 +60,21 @@ def main():
             dt = (time.perf_counter() - t0) / n * 1e6
             print(f"extra GPU sleep {sleep_us:4d} us: {dt:7.1f} us/step (host in train loop {th / n * 1e6:.1f} us)",
                   flush=True)
+        # the step graphs alone, back to back (no Python between replays):
+        # what the device + graph dispatch sustain without the host loop
+        f = tr._fused
+        if f is not None and f.graphs is not None:
+            torch.cuda.synchronize()
+            n = 200
+            t0 = time.perf_counter()
+            for i in range(n):
+                p = f.parity
+                f.graphs[p][2].replay()
+                f.parity ^= 1
+            th = (time.perf_counter() - t0) / n * 1e6
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n * 1e6
+            print(f"step graphs back to back: {dt:7.1f} us/step (host in replay {th:.1f} us)", flush=True)
         import cProfile
         import pstats
         pr = cProfile.Profile()
