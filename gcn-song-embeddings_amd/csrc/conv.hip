@@ -555,11 +555,19 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
 // dq_combine_kernel sums them in chunk order (deterministic, and no
 // device-scope float atomics: with per-XCD L2s those run at the memory side
 // and serialise on popular rows).
-template <int VEC>
+//
+// CM (chunk rows, the bottom layer): every chunk writes its MASKED partial,
+// lrelu'(q[u]) * sum over its occurrences, to part[ci] and its row's source
+// index q_src[u] to csrc[ci].  The mask is elementwise, so u's masked partials
+// add up to dpq[u]; the Q weight gradient dpq^T h[q_src] is then the same
+// GEMM over chunk rows (h gathered through csrc) and no combine is needed --
+// at the bottom layer nothing else reads dpq (no dh below the input features).
+template <int VEC, bool CM = false>
 __global__ __launch_bounds__(256) void dq_chunk_kernel(
     const int2* __restrict__ chunks, const int* __restrict__ nchunks, const int2* __restrict__ occ2,
     const float* __restrict__ dagg, int64_t ld_dagg, const float* __restrict__ q, int hid,
-    float* __restrict__ dpq, float* __restrict__ part) {
+    float* __restrict__ dpq, float* __restrict__ part, const int32_t* __restrict__ q_src = nullptr,
+    int32_t* __restrict__ csrc = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -577,7 +585,8 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
       if (lane < kDqChunk) oc_n = occ2[(ci + nw) * kDqChunk + lane];
     }
     const int u = dsc.x, n = dsc.y & 0xff;
-    const bool split = (dsc.y & kDqSplit) != 0;
+    const bool split = !CM && (dsc.y & kDqSplit) != 0;
+    if (CM && lane == 0) csrc[ci] = q_src[u];
     const int32_t my_row = oc.x;
     const float my_w = __int_as_float(oc.y);
     for (int c0 = 0; c0 < h4; c0 += 64 * VEC) {
@@ -624,7 +633,7 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
           }
         }
       }
-      float4* o = reinterpret_cast<float4*>(split ? part + ci * hid : dpq + (int64_t)u * hid);
+      float4* o = reinterpret_cast<float4*>(split || CM ? part + ci * hid : dpq + (int64_t)u * hid);
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         const int c = c0 + v * 64 + lane;
@@ -1367,11 +1376,23 @@ int64_t dq_split_capacity(int64_t S_max, int T) { return S_max * T / (kDqChunk +
 int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks, const int2* split,
                      const int* nsplit, int64_t max_split, const int* off, const int2* occ2,
                      const float* dagg, int64_t ld_dagg, const float* q,
-                     int hid, float* dpq, float* part, hipStream_t st) {
+                     int hid, float* dpq, float* part, hipStream_t st, const int32_t* q_src,
+                     int32_t* csrc) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
   // persistent waves (each prefetches its next chunk): PINSAGE_DQ_GRID overrides (A/B)
   static const int cap = getenv("PINSAGE_DQ_GRID") ? atoi(getenv("PINSAGE_DQ_GRID")) : 2048;
   const int grid = grid_for(max_chunks * 64, 256, std::max(1, cap));
+  if (csrc) {  // chunk rows: masked partials in part, no combine
+    PS_REQUIRE(q_src, kErrArg, "dq: chunk rows need the rows' source indices");
+    if (hid >= 512)
+      hipLaunchKernelGGL((dq_chunk_kernel<2, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg,
+                         ld_dagg, q, hid, dpq, part, q_src, csrc);
+    else
+      hipLaunchKernelGGL((dq_chunk_kernel<1, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg,
+                         ld_dagg, q, hid, dpq, part, q_src, csrc);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
   if (hid >= 512)
     hipLaunchKernelGGL((dq_chunk_kernel<2>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg, ld_dagg,
                        q, hid, dpq, part);

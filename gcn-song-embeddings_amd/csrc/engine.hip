@@ -48,7 +48,8 @@ int launch_csr_build(const int32_t*, const float*, const int*, int64_t, int, con
 int64_t dq_chunk_capacity(int64_t, int, int64_t);
 int64_t dq_split_capacity(int64_t, int);
 int launch_dq_chunks(const int2*, const int*, int64_t, const int2*, const int*, int64_t, const int*,
-                     const int2*, const float*, int64_t, const float*, int, float*, float*, hipStream_t);
+                     const int2*, const float*, int64_t, const float*, int, float*, float*, hipStream_t,
+                     const int32_t* q_src = nullptr, int32_t* csrc = nullptr);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
@@ -98,6 +99,7 @@ struct LayerBuf {
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
          occ2 = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
+  size_t csrc = 0;  // chunk rows' source indices (bottom layer, Engine::dq_chunk_rows)
   int64_t max_chunks = 0, max_split = 0;
   // parameter offsets (floats) into the flat param / grad buffers
   int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
@@ -138,6 +140,13 @@ struct Engine {
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
   bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
+  // PINSAGE_DQ_CHUNK_ROWS=1: the bottom layer's Q weight gradient over dq
+  // chunk rows (masked per-chunk partials, h gathered per chunk) instead of
+  // combined dpq rows, so the combine launch leaves the chain.  Measured (one
+  // session, ms/step, bwd.layer.l0 µs): C2 0.451 -> 0.454, 167 -> 169; C4
+  // 0.483 -> 0.476, 183 -> 179 -- the GEMM's K grows by the split rows' extra
+  // chunks (C2 Q0 wgrad 69 -> 79 µs) about as much as the combine saved.
+  bool dq_chunk_rows = getenv("PINSAGE_DQ_CHUNK_ROWS") && atoi(getenv("PINSAGE_DQ_CHUNK_ROWS")) != 0;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -380,6 +389,7 @@ static void layout(Engine& E) {
     lb.chunks = carve(cur, lb.max_chunks * 8);
     lb.nchunks = carve(cur, 16);
     lb.dqpart = carve(cur, lb.max_chunks * c.hid * 4);  // partials of split dq rows
+    lb.csrc = carve(cur, lb.max_chunks * 4);
     lb.max_split = dq_split_capacity(FS, (int)T);
     lb.split = carve(cur, lb.max_split * 8);
     lb.nsplit = carve(cur, 16);
@@ -936,25 +946,28 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
                            a.beta1, a.beta2, a.eps, s_w);
       }));
     }
+    const bool chunk_rows = l == 0 && E.dq_chunk_rows;
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
                             at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
                             at<int>(ws, lb.off), at<int2>(ws, lb.occ2),
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
-                            at<float>(ws, lb.dqpart), st));
+                            at<float>(ws, lb.dqpart), st, at<int32_t>(ws, lb.q_src),
+                            chunk_rows ? at<int32_t>(ws, lb.csrc) : nullptr));
     PS_TRY(run_pend(E));
     WGrad q_wgrad;
     {
-      // dQ = dpq^T h[q_src], dQb = colsum(dpq)
+      // dQ = dpq^T h[q_src], dQb = colsum(dpq); chunk rows: the same sums over
+      // the masked chunk partials, h gathered through csrc
       WGrad w;
-      w.A = at<float>(ws, lb.dpq);
+      w.A = at<float>(ws, chunk_rows ? lb.dqpart : lb.dpq);
       w.lda = hd;
       w.M = hd;
       w.B = h;
       w.ldb = ldh;
-      w.b_idx = at<int32_t>(ws, lb.q_src);
+      w.b_idx = at<int32_t>(ws, chunk_rows ? lb.csrc : lb.q_src);
       w.N = d;
-      w.K_dev = cnt(lb.N);
-      w.K_max = lb.N.cap;
+      w.K_dev = chunk_rows ? at<int>(ws, lb.nchunks) : cnt(lb.N);
+      w.K_max = chunk_rows ? lb.max_chunks : lb.N.cap;
       w.K_hint = lb.N.hint;
       w.dst = gr + lb.pQw;
       w.ld_dst = d;

@@ -391,12 +391,15 @@ def test_frontier_ahead_matches_serial_step(mode):
             os.chdir(cwd)
 
 
-def test_deferred_side_launches_match_immediate():
-    """PINSAGE_DEFER_SIDE (engine.hip fork_side / run_pend) only changes when the
-    backward's side launches and the loss monitors are enqueued, not what they
-    wait for: the graph-replayed step with them deferred (default) trains like
-    the one enqueuing them at their fork points -- same published losses (the
-    monitors' output) and parameters within rounding (CSR fill order, tuner)."""
+@pytest.mark.parametrize("var,a,b", [("PINSAGE_DEFER_SIDE", "0", "3"), ("PINSAGE_DQ_CHUNK_ROWS", "0", "1")])
+def test_engine_variants_train_alike(var, a, b):
+    """Engine variants that change only launch order or summation order train
+    alike -- same published losses (the monitors' output) and parameters within
+    rounding (CSR fill order), GEMM choices from the size model in both runs:
+    PINSAGE_DEFER_SIDE (engine.hip fork_side / run_pend: when the backward's
+    side launches and the loss monitors are enqueued, not what they wait for)
+    and PINSAGE_DQ_CHUNK_ROWS (the bottom layer's Q weight gradient summed
+    over masked dq chunk partials instead of combined dpq rows)."""
     import graph
     import pinsage_training as pt
     import synthetic
@@ -404,7 +407,7 @@ def test_deferred_side_launches_match_immediate():
     indptr, indices = pg.csr()
     feats = torch.from_numpy(synthetic.make_features(6000, 128, seed=42))
     pos = torch.from_numpy(synthetic.make_positives(pg, 30000, seed=43))
-    old = os.environ.get("PINSAGE_DEFER_SIDE")
+    old = {k: os.environ.get(k) for k in (var, "PINSAGE_AUTOTUNE")}
     with tempfile.TemporaryDirectory() as tmp:
         cwd = os.getcwd()
         os.chdir(tmp)
@@ -412,9 +415,10 @@ def test_deferred_side_launches_match_immediate():
             g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp,
                                         nbhds_path=os.path.join(tmp, "nb.pt"))
             pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
+            os.environ["PINSAGE_AUTOTUNE"] = "0"
 
             def run(mode):
-                os.environ["PINSAGE_DEFER_SIDE"] = mode  # read when the engine is built
+                os.environ[var] = mode  # read when the engine is built
                 torch.manual_seed(5)
                 tr = pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
                 tr.batch_size = 256
@@ -426,18 +430,19 @@ def test_deferred_side_launches_match_immediate():
                 torch.cuda.synchronize()
                 return losses, tr._fused.runner.flat.detach().clone()
 
-            l0, p0 = run("0")
-            l3, p3 = run("3")
+            l0, p0 = run(a)
+            l1, p1 = run(b)
             assert all(v > 0 for v in l0)
-            for a, b in zip(l0, l3):
-                assert abs(a - b) <= 1e-4 * abs(a) + 1e-7
-            assert ((p0 - p3).norm() / p0.norm()).item() < 1e-4
+            for x, y in zip(l0, l1):
+                assert abs(x - y) <= 1e-4 * abs(x) + 1e-7
+            assert ((p0 - p1).norm() / p0.norm()).item() < 1e-4
         finally:
             os.chdir(cwd)
-            if old is None:
-                os.environ.pop("PINSAGE_DEFER_SIDE", None)
-            else:
-                os.environ["PINSAGE_DEFER_SIDE"] = old
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
 
 
 def test_train_step_three_layers_fanout_50_vs_oracle():
