@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "aggw.h"
 #include "bf16split.h"
 #include "common.h"
 
@@ -205,6 +206,7 @@ constexpr int kAw32Rows = 32;     // rows per workgroup
 constexpr int kAw32Out = 128;     // out_dim (4 column groups of 32)
 constexpr int kAw32Threads = 1024;
 constexpr int kAw32TMax = 64;     // fanout held in LDS per row
+constexpr int kAw32Lq = kAw32Out + 4;  // LDS row of the y tile the next-layer Q projection reads
 
 // LDS: A tile [32][K + 4] floats (row stride = 4 mod 64 banks: b128 fragment
 // reads of 16 consecutive rows hit distinct banks), then the tile's slot lists.
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
     const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
     const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
     const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y,
-    float* __restrict__ nrm_out, float* __restrict__ agg) {
+    float* __restrict__ nrm_out, float* __restrict__ agg, AggNextQ nx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int K = d + hid, lda = aw32_lda(K);
   float* sA = lds;                                          // [32][lda]
@@ -381,10 +383,66 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
       const float nrm = sqrtf(s2);
+      const float4 yv = make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
       if (row < nrows) {
-        *reinterpret_cast<float4*>(y + (r0 + row) * kAw32Out + 4 * c4) =
-            make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
+        *reinterpret_cast<float4*>(y + (r0 + row) * kAw32Out + 4 * c4) = yv;
         if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
+      }
+      if (nx.q) {
+        // ---- the next layer's Q projection of these rows (AggNextQ): the y
+        //      tile goes to LDS (over red, once every thread has read it) with
+        //      each row's next-layer q row (-1: not a neighbour there)
+        float* sY = sA;  // [32][kAw32Lq]
+        int* sU = sLoc;  // [32]
+        __syncthreads();
+        *reinterpret_cast<float4*>(sY + row * kAw32Lq + 4 * c4) = yv;
+        if (c4 == 0) {
+          int u = -1;
+          if (row < nrows) {
+            const int64_t id = nx.S_mem[r0 + row];
+            if ((nx.bits[id >> 6] >> (id & 63)) & 1ull)
+              u = (int)(nx.pref[id >> 6] + __popcll(nx.bits[id >> 6] & ((1ull << (id & 63)) - 1ull)));
+          }
+          sU[row] = u;
+        }
+      }
+    }
+    if (nx.q) {
+      __syncthreads();
+      // wave w: output columns 32 cg .. for cg = w, w + 16, ...; K = 128 in
+      // eight 16-k steps, the same k assignment, product order and epilogue
+      // (bias, lrelu) as the GEMM's split-bf16 tile (gemm.hip), so q matches
+      // the next layer's own Q GEMM
+      const int l32 = lane & 31, hh = lane >> 5;
+      for (int cg = wave; cg < nx.hid / 32; cg += kAw32Threads / 64) {
+        const float* qrow = nx.Qw + (int64_t)(cg * 32 + l32) * kAw32Out + 8 * hh;
+        aw_f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        const float* ap = sA + l32 * kAw32Lq + 8 * hh;
+        // (Q fragments straight from L2, two steps per unrolled pair: a deeper
+        // explicit prefetch spilled ~90 VGPRs at this kernel's 128)
+#pragma unroll 2
+        for (int s = 0; s < 8; ++s) {
+          bf16x8 aH, aM, aL, bH, bM, bL;
+          split3(*reinterpret_cast<const float4*>(ap + 16 * s), *reinterpret_cast<const float4*>(ap + 16 * s + 4),
+                 aH, aM, aL);
+          split3(*reinterpret_cast<const float4*>(qrow + 16 * s), *reinterpret_cast<const float4*>(qrow + 16 * s + 4),
+                 bH, bM, bL);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
+        }
+        const int col = cg * 32 + l32;
+        const float bq = nx.Qb[col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int u = sLoc[(r & 3) + 8 * (r >> 2) + 4 * hh];
+          if (u >= 0) nx.q[(int64_t)u * nx.hid + col] = lrelu(acc[r] + bq);
+        }
       }
     }
     __syncthreads();  // LDS is reused by the next tile
@@ -411,8 +469,10 @@ int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
 // their blocks)
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
-                 const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st) {
+                 const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
+                 const AggNextQ* next, int* next_done) {
   PS_REQUIRE(agg_w_supported(d, hid, kAwOut, T), kErrArg, "agg_w: unsupported shape");
+  if (next_done) *next_done = 0;
   const int K = d + hid;
   const int lds = kAwRows * (K + 4) * 4 + 2 * kAwRows * kAwTMax * 4 + kAwRows * 4;
   static int prepared = 0;
@@ -446,8 +506,16 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
     }
     // ~24 rows per block (a 32-row tile with headroom) over every CU
     const int64_t g32 = std::max<int64_t>(1, std::min<int64_t>(cus, (S_max + 23) / 24));
+    AggNextQ nx;
+    if (next && next->q) {
+      PS_REQUIRE(next->hid > 0 && next->hid % 32 == 0 && next->S_mem && next->bits && next->pref &&
+                     next->Qw && next->Qb,
+                 kErrArg, "agg_w: next-layer Q projection needs hid % 32 == 0 and every pointer");
+      nx = *next;
+      if (next_done) *next_done = 1;
+    }
     hipLaunchKernelGGL(agg_w32_kernel, dim3((int)g32), dim3(kAw32Threads), lds32,
-                       st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm, agg);
+                       st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, nx);
   } else {
     hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
                        loc, wloc, T, nS, n_static, W, bias, y, nrm, agg);

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "aggw.h"
 #include "../../include/pinsage_hip.h"
 #include "common.h"
 #include "gemm.h"
@@ -36,9 +37,6 @@ int launch_mark_table_i64(unsigned long long*, const int64_t*, int64_t, const in
                           int, int64_t, int*, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
-int agg_w_supported(int64_t, int64_t, int64_t, int64_t);
-int launch_agg_w(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*, const float*, int,
-                 const int*, int64_t, int64_t, const float*, const float*, float*, float*, float*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_gather_rows(const float*, int64_t, int64_t, int, const int64_t*, int64_t, float*, int64_t,

@@ -21,6 +21,7 @@
 #include <string>
 #include <vector>
 
+#include "aggw.h"
 #include "common.h"
 #include "gemm.h"
 
@@ -56,10 +57,6 @@ int launch_loss(const float*, int, const int32_t*, int, float, const float*, int
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
                 float*, bool, hipStream_t);
 int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
-int agg_w_supported(int64_t, int64_t, int64_t, int64_t);
-int launch_agg_w(const float*, int64_t, int, const int32_t*, const float*, int, const int32_t*,
-                 const float*, int, const int*, int64_t, int64_t, const float*, const float*, float*, float*,
-                 float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
                 hipStream_t);
 int csr_prepare();
@@ -140,6 +137,9 @@ struct Engine {
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
   bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
+  // the next layer's Q projection inside the 32-row aggregation + W kernel
+  // (AggNextQ, aggw.h): one launch less per upper layer (PINSAGE_FUSED_NEXT_Q=0: off)
+  bool fused_next_q = !getenv("PINSAGE_FUSED_NEXT_Q") || atoi(getenv("PINSAGE_FUSED_NEXT_Q")) != 0;
   // PINSAGE_DQ_CHUNK_ROWS=1: the bottom layer's Q weight gradient over dq
   // chunk rows (masked per-chunk partials, h gathered per chunk) instead of
   // combined dpq rows, so the combine launch leaves the chain.  Measured (one
@@ -531,11 +531,13 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   const int Lc = (int)c.n_layers, T = (int)c.T;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
+  int q_done = 0;  // this layer's q rows came out of the layer below's kernel (AggNextQ)
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
     const int64_t ldh = l == 0 ? E.ld_f : c.out;
     // Q projection of the distinct neighbours: lrelu(h[u] Q^T + b)
+    if (!q_done) {
     GemmParams q;
     q.M_dev = cnt(lb.N);
     q.M_hint = (int)lb.N.hint;
@@ -566,6 +568,8 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       apply_choice(E, lname("fwd.q_gemm", l), q);
       PS_TRY(launch_gemm(q, st));
     }
+    }
+    q_done = 0;
     if (l == 0 && E.fork.stream) {  // the next batch's frontier beside the rest of the step
       PS_TRY(ensure_streams(E));
       PS_TRY(dep(E, st, E.fork.stream));
@@ -575,10 +579,21 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
       Timed taw(E, lname("fwd.aggw", l), st);
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
+      AggNextQ nx;
+      if (E.fused_next_q && l + 1 < Lc) {  // the next layer's neighbours are rows of this y
+        const LayerBuf& nb = E.L[(size_t)l + 1];
+        nx.S_mem = at<int32_t>(ws, lb.S.members);
+        nx.bits = at<unsigned long long>(ws, nb.N.bits);
+        nx.pref = at<uint32_t>(ws, nb.N.prefix);
+        nx.Qw = E.params + nb.pQw;
+        nx.Qb = E.params + nb.pQb;
+        nx.q = at<float>(ws, nb.q);
+        nx.hid = (int)c.hid;
+      }
       PS_TRY(launch_agg_w(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q),
                           (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0,
                           S_est, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
-                          at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st));
+                          at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st, nx.q ? &nx : nullptr, &q_done));
       continue;
     }
     Timed t_agg(E, lname("fwd.agg", l), st);

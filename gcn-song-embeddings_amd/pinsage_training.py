@@ -645,8 +645,10 @@ class _FusedStep:
 
                 # the next step's ids go to workspace 1-p, whose last user
                 # (the previous step) is done: graph launches are stream-ordered
-                self._stage(B, self.slot_next, 1 - p, p)
-                if split:  # the step alone; _call stages and forks the frontier
+                # (split: _call stages them eagerly and forks the frontier)
+                if not split:
+                    self._stage(B, self.slot_next, 1 - p, p)
+                if split:  # the step alone
                     self._main(B, p, with_adam=adam, stage=stage)
                 elif self.ahead_mode == "late":
                     # forked at the start like "start", but captured after

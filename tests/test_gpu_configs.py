@@ -125,6 +125,16 @@ def test_fixed_cotangent_reference_init(L, T):
     fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), L, T, seed=L * 10 + T)
 
 
+@pytest.mark.parametrize("L", [2, 3])
+def test_fixed_cotangent_fused_next_layer_q(L, monkeypatch):
+    """The 32-row aggregation + W kernel forced at every size
+    (PINSAGE_AGGW32_MIN_ROWS=0), so each upper layer's Q projection comes out
+    of the layer below's kernel (aggw.h AggNextQ) instead of its own GEMM:
+    the same fixed-cotangent check at 1e-4."""
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
+    test_fixed_cotangent_reference_init(L, 10)
+
+
 def test_fixed_cotangent_c1_shape():
     """The C1 flow's exact model shape (dataset_micro through dashboard.py:
     d_in 512, 1 layer, fanout 3, batch 32 -- 32 ids per call, repeats included)

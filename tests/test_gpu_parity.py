@@ -346,7 +346,12 @@ def test_frontier_ahead_matches_serial_step(mode):
     branch) trains exactly like the serial step: same
     losses and parameters (within rounding: the CSR fill order uses atomics),
     with look-ahead hits; a batch that is not the predicted one (here a
-    caller-made batch) falls back to its own frontier first."""
+    caller-made batch) falls back to its own frontier first.  Parameters:
+    Adam moves an element by at most lr per step, and an element whose
+    gradient is at rounding level moves by +-lr with a sign the rounding
+    picks, so the bound is 2 lr per step elementwise, and the relative norm of
+    the difference (such elements included) stays below 2e-4 (measured
+    0.9-1.2e-4 after six steps, differing between runs with the CSR order)."""
     import graph
     import pinsage_training as pt
     import synthetic
@@ -386,20 +391,24 @@ def test_frontier_ahead_matches_serial_step(mode):
             for a, b in zip(l0, l1):
                 assert abs(a - b) <= 1e-4 * abs(a) + 1e-7
             assert ((p0 - p1).abs() <= 2 * 1e-4 * 6 + 1e-7).all()
-            assert ((p0 - p1).norm() / p0.norm()).item() < 1e-4
+            assert ((p0 - p1).norm() / p0.norm()).item() < 2e-4
         finally:
             os.chdir(cwd)
 
 
-@pytest.mark.parametrize("var,a,b", [("PINSAGE_DEFER_SIDE", "0", "3"), ("PINSAGE_DQ_CHUNK_ROWS", "0", "1")])
-def test_engine_variants_train_alike(var, a, b):
+@pytest.mark.parametrize("var,a,b", [("PINSAGE_DEFER_SIDE", "0", "3"), ("PINSAGE_DQ_CHUNK_ROWS", "0", "1"),
+                                     ("PINSAGE_FUSED_NEXT_Q", "0", "1")])
+def test_engine_variants_train_alike(var, a, b, monkeypatch):
     """Engine variants that change only launch order or summation order train
     alike -- same published losses (the monitors' output) and parameters within
     rounding (CSR fill order), GEMM choices from the size model in both runs:
     PINSAGE_DEFER_SIDE (engine.hip fork_side / run_pend: when the backward's
     side launches and the loss monitors are enqueued, not what they wait for)
     and PINSAGE_DQ_CHUNK_ROWS (the bottom layer's Q weight gradient summed
-    over masked dq chunk partials instead of combined dpq rows)."""
+    over masked dq chunk partials instead of combined dpq rows) and
+    PINSAGE_FUSED_NEXT_Q (layer 1's Q projection inside layer 0's 32-row
+    aggregation + W kernel, that form forced here)."""
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
     import graph
     import pinsage_training as pt
     import synthetic
