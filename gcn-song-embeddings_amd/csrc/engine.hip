@@ -137,9 +137,13 @@ struct Engine {
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
   bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
-  // the next layer's Q projection inside the 32-row aggregation + W kernel
-  // (AggNextQ, aggw.h): one launch less per upper layer (PINSAGE_FUSED_NEXT_Q=0: off)
-  bool fused_next_q = !getenv("PINSAGE_FUSED_NEXT_Q") || atoi(getenv("PINSAGE_FUSED_NEXT_Q")) != 0;
+  // PINSAGE_FUSED_NEXT_Q=1: the next layer's Q projection inside the 32-row
+  // aggregation + W kernel (AggNextQ, aggw.h), one launch less per upper
+  // layer.  Measured slower (one session, ms/step): C2 0.439 -> 0.442 (layer
+  // 0's kernel 37.2 -> 49.7 us against the 24 us Q GEMM it replaces), C4
+  // 0.479 -> 0.485 (50.5 -> 76.0 us): each 32-row tile reads all of Q (256 KB)
+  // from L2 with little in flight per wave, so it is kept opt-in.
+  bool fused_next_q = getenv("PINSAGE_FUSED_NEXT_Q") && atoi(getenv("PINSAGE_FUSED_NEXT_Q")) != 0;
   // PINSAGE_DQ_CHUNK_ROWS=1: the bottom layer's Q weight gradient over dq
   // chunk rows (masked per-chunk partials, h gathered per chunk) instead of
   // combined dpq rows, so the combine launch leaves the chain.  Measured (one

@@ -128,10 +128,12 @@ def test_fixed_cotangent_reference_init(L, T):
 @pytest.mark.parametrize("L", [2, 3])
 def test_fixed_cotangent_fused_next_layer_q(L, monkeypatch):
     """The 32-row aggregation + W kernel forced at every size
-    (PINSAGE_AGGW32_MIN_ROWS=0), so each upper layer's Q projection comes out
+    (PINSAGE_AGGW32_MIN_ROWS=0) with PINSAGE_FUSED_NEXT_Q=1 (opt-in), so each
+    upper layer's Q projection comes out
     of the layer below's kernel (aggw.h AggNextQ) instead of its own GEMM:
     the same fixed-cotangent check at 1e-4."""
     monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
+    monkeypatch.setenv("PINSAGE_FUSED_NEXT_Q", "1")
     test_fixed_cotangent_reference_init(L, 10)
 
 
