@@ -14,7 +14,8 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpinsage_hip.so")
+# PINSAGE_LIB: another build of the same C-ABI (A/B runs of compile-time variants)
+LIB_PATH = os.environ.get("PINSAGE_LIB") or os.path.join(HERE, "libpinsage_hip.so")
 
 _lib = None
 

@@ -289,7 +289,10 @@ __global__ __launch_bounds__(1024) void csr_count_kernel(const int32_t* __restri
 // occurrences, never spanning two rows.  cnt is zeroed behind the read (kept
 // zero for the next step).  Multi-block form: one block per 1024 rows, each
 // block sums its predecessors' totals itself.
-constexpr int kDqChunk = 16;
+#ifndef PS_DQ_CHUNK
+#define PS_DQ_CHUNK 16
+#endif
+constexpr int kDqChunk = PS_DQ_CHUNK;  // <= 16 (the engine's pair blocks), a multiple of 4
 constexpr int kDqSplit = 0x100;  // chunk flag: the row's sum is split over several chunks
 constexpr int kScanB = 256, kScanPer = 4, kScanChunk = kScanB * kScanPer;
 __device__ __forceinline__ int n_chunks(int c) { return (c + kDqChunk - 1) / kDqChunk; }

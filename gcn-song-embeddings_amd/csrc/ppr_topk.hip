@@ -231,10 +231,24 @@ __global__ __launch_bounds__(64) void heap_topk_kernel(
         if (parent == 0) break;
       }
     }
-    // __heap_select over the sparse tail: pop_heap(first, middle, i) when *i > *first
-    for (; r < nr; ++r) {
-      const uint32_t v = (rs[r].y << 16) | (uint32_t)(k + r);
-      if (hgt(v, f[0])) h_adjust(f, 0, k, v);
+    // __heap_select over the sparse tail: pop_heap(first, middle, i) when *i > *first.
+    // The runs are read 8 at a time ahead of their comparisons (one load per
+    // run inside the loop left every iteration waiting on its own global
+    // load: with few sources per launch, as on the fly, that latency was the
+    // kernel) and the root stays in a register between adjustments.
+    uint32_t root = f[0];
+    for (; r < nr; r += 8) {
+      uint2 b[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = rs[min(r + i, nr - 1)];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t v = (b[i].y << 16) | (uint32_t)(k + r + i);
+        if (r + i < nr && hgt(v, root)) {
+          h_adjust(f, 0, k, v);
+          root = f[0];
+        }
+      }
     }
     // __sort_heap
     for (int len = k; len > 1;) {
@@ -307,6 +321,10 @@ int launch_heap_topk(const uint2* runs, const int* n_runs, int64_t n_src, int n_
   // fewer for large k (PersPageRank's k up to 1000)
   int G = 64;
   while (G > 1 && G * kp * 4 > 64 * 1024) G >>= 1;
+  // few sources (the on-the-fly sampler's nodesets): fewer lanes per block, so
+  // more CUs share the sources and a wave's divergent heap adjustments are the
+  // union over fewer lanes (each lane's replay is serial either way)
+  while (G > 1 && ceil_div(n_src, G) < 1024) G >>= 1;
   const int lds = G * kp * 4;
   PS_REQUIRE(lds <= 64 * 1024, kErrArg, "ppr_topk: k too large for the LDS heaps");
   hipLaunchKernelGGL(heap_topk_kernel, dim3((unsigned)ceil_div(n_src, G)), dim3(64), lds, st, runs,
