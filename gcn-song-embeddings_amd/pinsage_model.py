@@ -391,23 +391,27 @@ def relevant_nodes_per_layer(g, n_items, nodeset, n_layers, n_hops, alpha, T):
 class _FlyDraws:
     """One model call's on-the-fly draws, laid out for the engine.
 
-    ``tabs``: per-layer (nb int32 [n_items][T], wn f32 [n_items][T]) tables,
-    index 0 = bottom, rows of each layer's nodes written.  A node repeated in
-    the top nodeset keeps its LAST occurrence's row there: the reference's
+    ``tabs``: per-layer (nb int32 [rows][T], wn f32 [rows][T]) tables, index 0 =
+    bottom, rows of each layer's nodes written.  A node repeated in the top
+    nodeset keeps its LAST occurrence's row there: the reference's
     put_embeddings lets the last write win (pinsage_model.py:29), so the output
     rows of every repeat are the last one's.  ``uniq``/``inv``: the top
-    nodeset's distinct ids and each position's index into them.  ``repeats``:
-    for every earlier occurrence rank r = 1, 2, ... (counted from the last),
-    (index into uniq, ids, top-layer (nb, wn) table) of the positions holding
-    it.  Each occurrence walked its own neighbourhood, and index_put's backward
-    hands every occurrence's conv output the summed cotangent of its id
-    (pinsage_model.py:257-265), so their gradients are the reference's."""
+    nodeset's distinct ids and each position's index into them.  Every EARLIER
+    occurrence of a repeated id walked its own neighbourhood, and index_put's
+    backward hands its conv output the summed cotangent of its id
+    (pinsage_model.py:257-265), so it is computed too: as a virtual node
+    ``n_items + j`` (``ids_x[j]`` its real id, ``ui_x[j]`` its index into
+    uniq) whose top-layer row holds that occurrence's draws and whose rows in
+    the layers below (and feature row) are its real node's, so one engine
+    call computes every occurrence (rows = n_items + len(ids_x))."""
 
-    def __init__(self, tabs, uniq, inv, repeats):
-        self.tabs, self.uniq, self.inv, self.repeats = tabs, uniq, inv, repeats
+    def __init__(self, tabs, uniq, inv, ids_x, ui_x, n_items):
+        self.tabs, self.uniq, self.inv = tabs, uniq, inv
+        self.ids_x, self.ui_x, self.n_items = ids_x, ui_x, int(n_items)
 
-    def with_top(self, top):
-        return self.tabs[:-1] + [top]
+    @property
+    def n_extra(self):
+        return int(self.ids_x.shape[0])
 
 
 def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
@@ -422,6 +426,7 @@ def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
     T = int(T)
     tabs = []
     cur = nodeset_dev
+    rows = int(n_items)
     top_info = None
     for layer in range(n_layers):
         _, _, wn, nb32 = _ppr_topk_device(g, cur, n_hops, alpha, T, t_norm=T, want_ref=False)
@@ -439,26 +444,29 @@ def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
         last = torch.empty(uniq.shape[0], dtype=torch.int64, device=dev)
         sel = rank == 0
         last[inv[sel]] = torch.arange(n, device=dev)[sel]
-        nbt = torch.empty((n_items, T), dtype=torch.int32, device=dev)
-        wnt = torch.empty((n_items, T), dtype=torch.float32, device=dev)
+        if layer == 0:  # the top layer: earlier occurrences become virtual nodes
+            pos_x = torch.nonzero(rank > 0).reshape(-1)
+            rows = int(n_items) + int(pos_x.shape[0])
+            top_info = (uniq, inv, pos_x)
+        nbt = torch.empty((rows, T), dtype=torch.int32, device=dev)
+        wnt = torch.empty((rows, T), dtype=torch.float32, device=dev)
         nbt[uniq] = nb32[last]
         wnt[uniq] = wn[last]
+        if layer == 0 and rows > n_items:
+            nbt[n_items:] = nb32[top_info[2]]
+            wnt[n_items:] = wn[top_info[2]]
         tabs.insert(0, (nbt, wnt))
-        if layer == 0:
-            top_info = (uniq, inv, rank, nb32, wn)
         cur = torch.unique(torch.cat([nb32.reshape(-1).to(torch.int64), cur]))
-    uniq, inv, rank, nb32, wn = top_info
-    repeats = []
-    n_rank = int(rank.max()) + 1 if rank.numel() else 1
-    for r in range(1, n_rank):
-        pos_r = torch.nonzero(rank == r).reshape(-1)
-        ids_r = nodeset_dev[pos_r]
-        nbt = torch.empty((n_items, T), dtype=torch.int32, device=dev)
-        wnt = torch.empty((n_items, T), dtype=torch.float32, device=dev)
-        nbt[ids_r] = nb32[pos_r]
-        wnt[ids_r] = wn[pos_r]
-        repeats.append((inv[pos_r], ids_r, (nbt, wnt)))
-    return _FlyDraws(tabs, uniq, inv, repeats)
+    uniq, inv, pos_x = top_info
+    ids_x = nodeset_dev[pos_x]
+    if rows > n_items:
+        # below the top, a virtual node is its real node (that node is in every
+        # lower nodeset: each layer's nodeset contains the one above it)
+        for l in range(n_layers - 1):
+            nbt, wnt = tabs[l]
+            nbt[n_items:] = nbt[ids_x]
+            wnt[n_items:] = wnt[ids_x]
+    return _FlyDraws(tabs, uniq, inv, ids_x, inv[pos_x], n_items)
 
 
 class _DeviceTable:
@@ -744,7 +752,10 @@ class _EngineRunner:
         need = max(n_pos, 1)
         if self.engine is None or self.engine.cfg.max_pos < need:
             cap = max(need, self.engine.cfg.max_pos * 2 if self.engine else need)
-            self.engine = _Engine(m.n_items, m.in_dim, m.hidden_dim, m.out_dim, m.n_layers, m.T, cap)
+            # on the fly, ids n_items .. n_items + cap - 1 are the earlier
+            # occurrences of repeated ids (_FlyDraws)
+            n_eng = m.n_items + (cap if m.sample_on_the_fly else 0)
+            self.engine = _Engine(n_eng, m.in_dim, m.hidden_dim, m.out_dim, m.n_layers, m.T, cap)
             self._ws = None
         return self.engine
 
@@ -787,7 +798,7 @@ class _EngineRunner:
         draws = self.fly_tables(ids)
         tabs = draws.tabs if draws is not None else None
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.params())
-        if need_grad and draws is not None and draws.repeats:
+        if need_grad and draws is not None and draws.n_extra:
             out = self._fly_with_repeats(feats, draws)
         elif need_grad:
             out = _EngineFn.apply(self, feats, table, ids, tabs, *self.params())
@@ -807,17 +818,28 @@ class _EngineRunner:
 
 
     def _fly_with_repeats(self, feats, draws):
-        """Autograd forward of an on-the-fly call whose nodeset repeats ids.
-        The distinct ids run with their last occurrence's draws (the output
-        rows); every earlier occurrence rank runs again with its own top-layer
-        draws and enters the output as (o - o.detach()), an exact zero in the
-        forward through which each occurrence's conv output receives its id's
-        summed cotangent -- index_put's backward (pinsage_model.py:257-265)."""
+        """Autograd forward of an on-the-fly call whose nodeset repeats ids, in
+        ONE engine call: the distinct ids (their last occurrence's draws: the
+        output rows) and every earlier occurrence as a virtual node (its own
+        top-layer draws, _FlyDraws).  An earlier occurrence enters the output as
+        (o - o.detach()), an exact zero in the forward through which its conv
+        output receives its id's summed cotangent -- index_put's backward
+        (pinsage_model.py:257-265).  The virtual nodes' feature rows are copies
+        of their real nodes' in this call's own feature buffer (the backward of
+        every pending call reads its own)."""
         ps = self.params()
-        out_u = _EngineFn.apply(self, feats, None, draws.uniq, draws.tabs, *ps)
-        for ui, ids_r, top in draws.repeats:
-            o = _EngineFn.apply(self, feats, None, ids_r, draws.with_top(top), *ps)
-            out_u = out_u.index_add(0, ui, o - o.detach())
+        n_u, n_x, n_items = int(draws.uniq.shape[0]), draws.n_extra, draws.n_items
+        if n_items + n_x > int(self.engine.cfg.n_items):
+            raise RuntimeError("on-the-fly repeats exceed the engine's virtual rows")
+        fx = torch.empty((n_items + n_x, feats.shape[1]), dtype=feats.dtype, device=feats.device)
+        nf = min(int(feats.shape[0]), n_items)
+        fx[:nf] = feats[:nf]
+        fx[n_items:] = feats[draws.ids_x]
+        ids = torch.cat([draws.uniq, torch.arange(n_items, n_items + n_x, dtype=torch.int64,
+                                                  device=draws.uniq.device)])
+        out = _EngineFn.apply(self, fx, None, ids, draws.tabs, *ps)
+        o = out[n_u:]
+        out_u = out[:n_u].index_add(0, draws.ui_x, o - o.detach())
         return out_u[draws.inv]
 
 
