@@ -430,33 +430,40 @@ def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
     top_info = None
     for layer in range(n_layers):
         _, _, wn, nb32 = _ppr_topk_device(g, cur, n_hops, alpha, T, t_norm=T, want_ref=False)
-        if nb32.numel() and int(nb32.max()) >= n_items:
-            # the reference's h[nb] (features of tracks only) raises here
-            raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
-                             "zero-weight tail: the reference's h[nb] raises IndexError)")
-        n = int(cur.shape[0])
-        uniq, inv = torch.unique(cur, return_inverse=True)
-        # occurrence rank of each position counted from its id's last one
-        order = torch.argsort(inv, stable=True)
-        ends = torch.cumsum(torch.bincount(inv, minlength=uniq.shape[0]), 0)
-        rank = torch.empty(n, dtype=torch.int64, device=dev)
-        rank[order] = ends[inv[order]] - 1 - torch.arange(n, device=dev)
-        last = torch.empty(uniq.shape[0], dtype=torch.int64, device=dev)
-        sel = rank == 0
-        last[inv[sel]] = torch.arange(n, device=dev)[sel]
-        if layer == 0:  # the top layer: earlier occurrences become virtual nodes
+        if layer == 0:
+            # the top nodeset may repeat ids: occurrence rank of each position
+            # counted from its id's last one; the earlier occurrences become
+            # virtual nodes
+            n = int(cur.shape[0])
+            uniq, inv = torch.unique(cur, return_inverse=True)
+            order = torch.argsort(inv, stable=True)
+            ends = torch.cumsum(torch.bincount(inv, minlength=uniq.shape[0]), 0)
+            rank = torch.empty(n, dtype=torch.int64, device=dev)
+            rank[order] = ends[inv[order]] - 1 - torch.arange(n, device=dev)
+            last = torch.empty(uniq.shape[0], dtype=torch.int64, device=dev)
+            sel = rank == 0
+            last[inv[sel]] = torch.arange(n, device=dev)[sel]
             pos_x = torch.nonzero(rank > 0).reshape(-1)
             rows = int(n_items) + int(pos_x.shape[0])
             top_info = (uniq, inv, pos_x)
         nbt = torch.empty((rows, T), dtype=torch.int32, device=dev)
         wnt = torch.empty((rows, T), dtype=torch.float32, device=dev)
-        nbt[uniq] = nb32[last]
-        wnt[uniq] = wn[last]
-        if layer == 0 and rows > n_items:
-            nbt[n_items:] = nb32[top_info[2]]
-            wnt[n_items:] = wn[top_info[2]]
+        if layer == 0:
+            nbt[uniq] = nb32[last]
+            wnt[uniq] = wn[last]
+            if rows > n_items:
+                nbt[n_items:] = nb32[pos_x]
+                wnt[n_items:] = wn[pos_x]
+        else:  # lower nodesets are torch.unique outputs: one row per id already
+            nbt[cur] = nb32
+            wnt[cur] = wn
         tabs.insert(0, (nbt, wnt))
         cur = torch.unique(torch.cat([nb32.reshape(-1).to(torch.int64), cur]))
+        # sorted: its last id is the largest drawn (before any table indexes it)
+        if cur.numel() and int(cur[-1]) >= n_items:
+            # the reference's h[nb] (features of tracks only) raises here
+            raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
+                             "zero-weight tail: the reference's h[nb] raises IndexError)")
     uniq, inv, pos_x = top_info
     ids_x = nodeset_dev[pos_x]
     if rows > n_items:
@@ -790,7 +797,8 @@ class _EngineRunner:
         if n == 0:
             return torch.empty((0, m.out_dim), device=out_dev)
         n_valid = min(int(feats.shape[0]), int(m.n_items))
-        if int(ids.min()) < 0 or int(ids.max()) >= n_valid:
+        lo, hi = (int(v) for v in torch.stack(torch.aminmax(ids)).tolist())
+        if lo < 0 or hi >= n_valid:
             # the reference's features[nodeset] / all_w[nodeset] raise the same way
             raise IndexError(f"node ids out of range for {n_valid} items")
         self.pack()
