@@ -624,6 +624,20 @@ class _Engine:
         except Exception:
             pass
 
+    def acquire_workspace(self, dev):
+        """A workspace for an autograd call: one whose backward has run (its
+        kernels left the zero-kept regions zero, so it needs no re-init), or a
+        new one."""
+        pool = self.__dict__.setdefault("_pool", [])
+        return pool.pop() if pool else self.new_workspace(dev)
+
+    def release_workspace(self, ws):
+        """Back to the pool after its backward was enqueued (stream order keeps
+        the next call's kernels behind it); at most 4 kept."""
+        pool = self.__dict__.setdefault("_pool", [])
+        if len(pool) < 4:
+            pool.append(ws)
+
     def new_workspace(self, dev):
         ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=dev)
         nat.check(nat.lib().pinsage_engine_init_workspace(self.h, nat.ptr(ws), nat.stream_ptr()),
@@ -857,7 +871,7 @@ class _EngineFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, runner, feats, table, ids, tabs, *params):
         e = runner.engine
-        ws = e.new_workspace(runner.dev)
+        ws = e.acquire_workspace(runner.dev)
         runner.bind(feats, table, tabs=tabs)
         runner.set_layer_tables(tabs)
         try:
@@ -869,7 +883,7 @@ class _EngineFn(torch.autograd.Function):
         nat.check(nat.lib().pinsage_engine_gather_output(e.h, nat.ptr(ws), n, nat.ptr(out),
                                                          nat.stream_ptr()), "gather")
         ctx.runner, ctx.ws, ctx.feats, ctx.table, ctx.n = runner, ws, feats, table, n
-        runner.last_ws = ws  # (bench.py reads the last call's frontier sizes)
+        runner.last_ws = ws  # (bench.py reads frontier sizes from it: the last call to use it)
         ctx.tabs = tabs  # the frontier's tables stay alive with the workspace
         ctx.engine = e
         return out
@@ -883,6 +897,8 @@ class _EngineFn(torch.autograd.Function):
         nat.check(nat.lib().pinsage_engine_set_output_grad(e.h, nat.ptr(ws), nat.ptr(dout), ctx.n,
                                                            nat.stream_ptr()), "set_output_grad")
         nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(ws), nat.stream_ptr()), "backward")
+        e.release_workspace(ws)
+        ctx.ws = None
         out = []
         off = 0
         for p in runner.params():
