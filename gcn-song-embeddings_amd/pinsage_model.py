@@ -388,6 +388,9 @@ def relevant_nodes_per_layer(g, n_items, nodeset, n_layers, n_hops, alpha, T):
     return S
 
 
+_FLY_CALLS = 3  # model calls per train step (q, pos, neg) that fly_calls runs as one
+
+
 class _FlyDraws:
     """One model call's on-the-fly draws, laid out for the engine.
 
@@ -775,7 +778,8 @@ class _EngineRunner:
             cap = max(need, self.engine.cfg.max_pos * 2 if self.engine else need)
             # on the fly, ids n_items .. n_items + cap - 1 are the earlier
             # occurrences of repeated ids (_FlyDraws)
-            n_eng = m.n_items + (cap if m.sample_on_the_fly else 0)
+            # (and fly_calls puts call c's nodes at c * n_items + id)
+            n_eng = (_FLY_CALLS * m.n_items + cap) if m.sample_on_the_fly else m.n_items
             self.engine = _Engine(n_eng, m.in_dim, m.hidden_dim, m.out_dim, m.n_layers, m.T, cap)
             self._ws = None
         return self.engine
@@ -838,6 +842,79 @@ class _EngineRunner:
                                                              nat.ptr(out), nat.stream_ptr()), "gather")
         return out.to(out_dev)
 
+
+    def fly_calls(self, initial_h, nodesets):
+        """The train step's model calls (q, pos, neg: pinsage_training.py:183-185)
+        with on-the-fly sampling, in ONE engine call: each call draws its own
+        layers' neighbourhoods in the reference's order (fly_tables), then call c's
+        nodes become c * n_items + id (its tables' rows and neighbour ids moved by
+        c * n_items, its repeated ids' earlier occurrences virtual nodes above
+        len(nodesets) * n_items), so one forward / backward computes what the
+        calls compute one by one.  Returns each call's output (autograd)."""
+        m = self.model
+        C = len(nodesets)
+        if C > _FLY_CALLS or not m.sample_on_the_fly:
+            return [self(initial_h, ns, None) for ns in nodesets]
+        feats = self.features(initial_h)
+        n_items = int(m.n_items)
+        n_valid = min(int(feats.shape[0]), n_items)
+        ids_c = [torch.as_tensor(ns).reshape(-1).to(self.dev, torch.int64).contiguous() for ns in nodesets]
+        lohi = torch.stack([torch.stack(torch.aminmax(i)) for i in ids_c]).tolist()
+        if any(lo < 0 or hi >= n_valid for lo, hi in lohi):
+            raise IndexError(f"node ids out of range for {n_valid} items")
+        self.pack()
+        n_all = sum(int(i.shape[0]) for i in ids_c)
+        self.ensure_engine(n_all)
+        draws = [self.fly_tables(i) for i in ids_c]
+        n_x = [d.n_extra for d in draws]
+        base_x = C * n_items
+        rows = base_x + sum(n_x)
+        if rows > int(self.engine.cfg.n_items):
+            raise RuntimeError("on-the-fly calls exceed the engine's node rows")
+        T = int(m.T)
+        tabs = []
+        for l in range(m.n_layers):
+            nbt = torch.empty((rows, T), dtype=torch.int32, device=self.dev)
+            wnt = torch.empty((rows, T), dtype=torch.float32, device=self.dev)
+            xo = base_x
+            for c, d in enumerate(draws):
+                nb, wn = d.tabs[l]
+                torch.add(nb[:n_items], c * n_items, out=nbt[c * n_items:(c + 1) * n_items])
+                wnt[c * n_items:(c + 1) * n_items] = wn[:n_items]
+                if n_x[c]:
+                    torch.add(nb[n_items:], c * n_items, out=nbt[xo:xo + n_x[c]])
+                    wnt[xo:xo + n_x[c]] = wn[n_items:]
+                xo += n_x[c]
+            tabs.append((nbt, wnt))
+        # feature rows: call c's copy of the table at c * n_items (made once per
+        # feature tensor), the virtual rows written per call group
+        key = (id(feats), feats.data_ptr(), getattr(feats, "_version", 0), C, int(self.engine.cfg.n_items))
+        if getattr(self, "_fly_feat_key", None) != key:
+            fx = torch.empty((int(self.engine.cfg.n_items), feats.shape[1]), dtype=feats.dtype, device=self.dev)
+            for c in range(C):
+                fx[c * n_items:c * n_items + n_valid] = feats[:n_valid]
+            self._fly_feat, self._fly_feat_key = fx, key
+        fx = self._fly_feat
+        parts, xo = [], base_x
+        for c, d in enumerate(draws):
+            parts.append(d.uniq + c * n_items)
+            if n_x[c]:
+                fx[xo:xo + n_x[c]] = feats[d.ids_x]
+                parts.append(torch.arange(xo, xo + n_x[c], dtype=torch.int64, device=self.dev))
+            xo += n_x[c]
+        ids = torch.cat(parts)
+        out = _EngineFn.apply(self, fx, None, ids, tabs, *self.params())
+        outs, o0 = [], 0
+        for c, d in enumerate(draws):
+            n_u = int(d.uniq.shape[0])
+            out_u = out[o0:o0 + n_u]
+            o0 += n_u
+            if n_x[c]:
+                o = out[o0:o0 + n_x[c]]
+                o0 += n_x[c]
+                out_u = out_u.index_add(0, d.ui_x, o - o.detach())
+            outs.append(out_u[d.inv].to(initial_h.device))
+        return outs
 
     def _fly_with_repeats(self, feats, draws):
         """Autograd forward of an on-the-fly call whose nodeset repeats ids, in

@@ -942,9 +942,23 @@ class PinSage:
         generator as the reference does -- max_margin_loss, the engine's HIP
         backward per call (autograd), torch's Adam."""
         batch = torch.as_tensor(batch)
-        h_q = self.model(self.features, batch[:, 0])
-        h_pos = self.model(self.features, batch[:, 1])
-        h_neg = self.model(self.features, batch[:, 2])
+        model = self.model
+        if model._forward_pre_hooks or model._forward_hooks_with_kwargs:
+            h_q = model(self.features, batch[:, 0])
+            h_pos = model(self.features, batch[:, 1])
+            h_neg = model(self.features, batch[:, 2])
+        else:
+            # the three calls' draws in the reference's order, then one engine
+            # call for all of them (pinsage_model._EngineRunner.fly_calls); a
+            # caller's forward hooks see each call as model(features, ids)
+            calls = [batch[:, 0], batch[:, 1], batch[:, 2]]
+            outs = model.runner().fly_calls(self.features, calls)
+            for c, ids in enumerate(calls):
+                for hook in list(model._forward_hooks.values()):
+                    r = hook(model, (self.features, ids), outs[c])
+                    if r is not None:
+                        outs[c] = r
+            h_q, h_pos, h_neg = outs
         loss = max_margin_loss(h_q, h_pos, h_neg, self.margin)
         self.optimizer.zero_grad()
         loss.backward()
