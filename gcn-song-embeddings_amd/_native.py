@@ -68,6 +68,8 @@ _SIGS = {
     "pinsage_engine_set_layer_table": (ctypes.c_int, [vp, i64, vp, vp, i64]),
     "pinsage_ppr_topk": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, f32, i64, vp, u64, u32, i64, vp, i64,
                                         vp, vp, vp, vp, i64, vp]),
+    "pinsage_ppr_topk_segments": (ctypes.c_int, [vp, vp, i64, vp, i64, vp, vp, vp, i64, f32, i64, u32, vp,
+                                                 i64, vp, vp, vp, vp, i64, vp]),
     "pinsage_visit_dense": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, vp]),
     "pinsage_frontier_workspace": (i64, [i64]),
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),

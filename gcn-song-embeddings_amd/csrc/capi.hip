@@ -356,6 +356,55 @@ int pinsage_ppr_topk(const int64_t* indptr, const int32_t* indices, int64_t n_al
   return kOk;
 }
 
+int pinsage_ppr_topk_segments(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                              const int64_t* sources, int64_t n_seg, const int64_t* seg_start,
+                              const uint64_t* seg_seed, const int64_t* seg_base, int64_t n_hops,
+                              float alpha, int64_t k, uint32_t offset, void* ws, int64_t ws_bytes,
+                              double* w_out, int64_t* nb_out, float* wn_out, int32_t* nb32_out,
+                              int64_t t_norm, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  PS_REQUIRE(n_seg >= 1 && seg_start && seg_seed && seg_base && seg_start[0] == 0, kErrArg,
+             "ppr_topk_segments: bad segment table");
+  for (int64_t i = 0; i < n_seg; ++i)
+    PS_REQUIRE(seg_start[i + 1] >= seg_start[i], kErrArg, "ppr_topk_segments: segments out of order");
+  const int64_t n_src = seg_start[n_seg];
+  PS_REQUIRE(n_hops > 0 && n_all > 0, kErrArg, "ppr_topk: bad sizes");
+  PS_REQUIRE(k >= 1 && k <= n_all, kErrArg, "ppr_topk: k out of range (torch: selected index k out of range)");
+  PS_REQUIRE(k * 64 <= n_all, kErrArg,
+             "ppr_topk: the nth_element regime (k * 64 > n_all) needs pinsage_visit_topk");
+  PS_REQUIRE(n_hops < 65536 && k + n_hops < 65536, kErrArg, "ppr_topk: n_hops / k too large");
+  PS_REQUIRE(n_hops <= 8192, kErrArg, "ppr_topk: n_hops too large for the LDS sort");
+  PS_REQUIRE(n_all < (int64_t)0xFFFFFFFF, kErrArg, "ppr_topk: n_all must fit 32 bits");
+  PS_REQUIRE(!wn_out || (t_norm >= 1 && t_norm <= k), kErrArg, "ppr_topk: t_norm must be in [1, k]");
+  if (n_src == 0) return kOk;
+  char* base = static_cast<char*>(ws);
+  const int64_t fixed = ppr_fixed_bytes();
+  int* err_dev = reinterpret_cast<int*>(base + fixed - 256);
+  const int64_t room = (ws_bytes - fixed - 3 * 256) / ppr_round_bytes(n_hops, false);
+  PS_REQUIRE(room >= n_src, kErrWorkspace,
+             "ppr_topk_segments: workspace below pinsage_ppr_topk_workspace(n_src, n_hops, 0)");
+  int* nr_dev = reinterpret_cast<int*>(base + fixed);
+  uint2* runs_dev = reinterpret_cast<uint2*>(base + fixed + align_up(n_src * 4, 256));
+  PS_CHECK_HIP(hipMemsetAsync(err_dev, 0x7f, 4, st));
+  // one walk launch per segment (its own key and source numbering), one top-k
+  // pass over every segment's runs, one zero-degree check
+  for (int64_t i = 0; i < n_seg; ++i) {
+    const int64_t s0 = seg_start[i], ns = seg_start[i + 1] - s0;
+    PS_TRY(launch_walk_runs(indptr, indices, sources + s0, ns, (int)n_hops, alpha, nullptr, seg_seed[i],
+                            offset, seg_base[i], runs_dev + s0 * n_hops, nr_dev + s0, err_dev, st));
+  }
+  PS_TRY(launch_heap_topk(runs_dev, nr_dev, n_src, (int)n_hops, (int)k, w_out, nb_out, wn_out, nb32_out,
+                          (int)t_norm, st));
+  int err = 0;
+  PS_CHECK_HIP(hipMemcpyAsync(&err, err_dev, 4, hipMemcpyDeviceToHost, st));
+  PS_CHECK_HIP(hipStreamSynchronize(st));
+  if (err != 0x7f7f7f7f) {
+    set_error("walk: zero-degree node met (the reference's torch.randint(0) raises here)");
+    return kErrGraph;
+  }
+  return kOk;
+}
+
 // ------------------------------------------------------------------ visits / top-k
 int64_t pinsage_visit_topk_scratch(int64_t n_src, int64_t n_all, int64_t k) {
   return (k * 64 <= n_all) ? 0 : n_src * n_all * 8;

@@ -479,6 +479,97 @@ def _fly_layer_tables(g, n_items, nodeset_dev, n_layers, n_hops, alpha, T):
     return _FlyDraws(tabs, uniq, inv, ids_x, inv[pos_x], n_items)
 
 
+def _fly_tables_merged(g, n_items, ids_c, n_layers, n_hops, alpha, T):
+    """_fly_layer_tables for C model calls at once (Philox mode): the calls'
+    seeds are drawn in the per-call order (call c, layer l: the (c * L + l)-th
+    pair of words, as C sequential calls draw them), and each layer walks every
+    call's nodeset in one pinsage_ppr_topk_segments call, so the tables are the
+    per-call path's.  Call c's node v is c * n_items + v everywhere (rows and
+    neighbour ids), earlier occurrences of repeated top ids are virtual nodes
+    from C * n_items.  Returns (tabs, uniq, inv, ids_x, ui_x): uniq / inv over
+    the concatenated nodesets, ids_x the virtual nodes' real ids."""
+    L = nat.lib()
+    gc = _as_csr(g)
+    n_all = gc.number_of_nodes()
+    indptr, indices = gc.device_csr(nat.device())
+    C, n = len(ids_c), int(n_items)
+    T = int(T)
+    dev = ids_c[0].device
+    with nat.torch_rng() as mt:
+        d = [int(x) for x in mt.draws(2 * C * n_layers)]
+    seed = [[(d[2 * (c * n_layers + l)] << 32) | d[2 * (c * n_layers + l) + 1] for l in range(n_layers)]
+            for c in range(C)]
+    alpha32 = float(np.float32(alpha))
+    lens = [int(i.shape[0]) for i in ids_c]
+    src = torch.cat(ids_c)
+    off = torch.cat([torch.full((m,), c * n, dtype=torch.int64, device=dev) for c, m in enumerate(lens)])
+    cur = src + off  # top layer: the nodesets as given (repeats included), offset per call
+    tabs = []
+    rows = C * n
+    top = None
+    for layer in range(n_layers):
+        starts = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        n_src = int(starts[-1])
+        wn = torch.empty((n_src, T), dtype=torch.float32, device=dev)
+        nb32 = torch.empty((n_src, T), dtype=torch.int32, device=dev)
+        need = L.pinsage_ppr_topk_workspace(n_src, int(n_hops), 0)
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        seeds = np.array([seed[c][layer] for c in range(C)], dtype=np.uint64)
+        bases = np.zeros(C, dtype=np.int64)
+        nat.check(L.pinsage_ppr_topk_segments(
+            nat.ptr(indptr), nat.ptr(indices), n_all, nat.ptr(src), C, starts.ctypes.data,
+            seeds.ctypes.data, bases.ctypes.data, int(n_hops), alpha32, T, 0, nat.ptr(ws), ws.numel(),
+            None, None, nat.ptr(wn), nat.ptr(nb32), T, nat.stream_ptr()), "ppr_topk_segments")
+        nbo = nb32 + off[:, None].to(torch.int32)  # neighbour ids in their call's range
+        if layer == 0:
+            m = int(cur.shape[0])
+            uniq, inv = torch.unique(cur, return_inverse=True)
+            order = torch.argsort(inv, stable=True)
+            ends = torch.cumsum(torch.bincount(inv, minlength=uniq.shape[0]), 0)
+            rank = torch.empty(m, dtype=torch.int64, device=dev)
+            rank[order] = ends[inv[order]] - 1 - torch.arange(m, device=dev)
+            last = torch.empty(uniq.shape[0], dtype=torch.int64, device=dev)
+            sel = rank == 0
+            last[inv[sel]] = torch.arange(m, device=dev)[sel]
+            pos_x = torch.nonzero(rank > 0).reshape(-1)
+            rows = C * n + int(pos_x.shape[0])
+            top = (uniq, inv, pos_x)
+        nbt = torch.empty((rows, T), dtype=torch.int32, device=dev)
+        wnt = torch.empty((rows, T), dtype=torch.float32, device=dev)
+        if layer == 0:
+            nbt[uniq] = nbo[last]
+            wnt[uniq] = wn[last]
+            if rows > C * n:
+                nbt[C * n:] = nbo[pos_x]
+                wnt[C * n:] = wn[pos_x]
+        else:
+            nbt[cur] = nbo
+            wnt[cur] = wn
+        tabs.insert(0, (nbt, wnt))
+        nxt = torch.unique(torch.cat([nbo.reshape(-1).to(torch.int64), cur]))
+        # one sync: the largest drawn id (before offsets) and the calls' boundaries
+        bounds = torch.searchsorted(nxt, torch.arange(1, C, device=dev, dtype=torch.int64) * n)
+        info = torch.cat([nb32.max().reshape(1).to(torch.int64), bounds]).tolist()
+        if info[0] >= n_items:
+            raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
+                             "zero-weight tail: the reference's h[nb] raises IndexError)")
+        edges = [0] + info[1:] + [int(nxt.shape[0])]
+        lens = [edges[c + 1] - edges[c] for c in range(C)]
+        cur = nxt
+        off = torch.cat([torch.full((m,), c * n, dtype=torch.int64, device=dev) for c, m in enumerate(lens)])
+        src = cur - off
+    uniq, inv, pos_x = top
+    top_ids = torch.cat(ids_c) + torch.cat([torch.full((m,), c * n, dtype=torch.int64, device=dev)
+                                            for c, m in enumerate(int(i.shape[0]) for i in ids_c)])
+    ids_xo = top_ids[pos_x]  # virtual nodes' ids in their call's range
+    if rows > C * n:
+        for l in range(n_layers - 1):
+            nbt, wnt = tabs[l]
+            nbt[C * n:] = nbt[ids_xo]
+            wnt[C * n:] = wnt[ids_xo]
+    return tabs, uniq, inv, ids_xo % n, inv[pos_x]
+
+
 class _DeviceTable:
     """Device mirror of a precomputed (weights, nodes) table: first T columns,
     nodes int32, weights f32 normalised by their f64 row sum."""
@@ -865,6 +956,11 @@ class _EngineRunner:
         self.pack()
         n_all = sum(int(i.shape[0]) for i in ids_c)
         self.ensure_engine(n_all)
+        gc = _as_csr(m.g)
+        if (_RNG_MODE != "mt19937" and os.environ.get("PINSAGE_FLY_MERGE", "1") != "0"
+                and int(m.T) * 64 <= gc.number_of_nodes() and int(m.n_hops) <= 8192
+                and int(m.n_hops) + int(m.T) < 65536):
+            return self._fly_calls_merged(initial_h, feats, ids_c, n_items, n_valid)
         draws = [self.fly_tables(i) for i in ids_c]
         n_x = [d.n_extra for d in draws]
         base_x = C * n_items
@@ -888,13 +984,7 @@ class _EngineRunner:
             tabs.append((nbt, wnt))
         # feature rows: call c's copy of the table at c * n_items (made once per
         # feature tensor), the virtual rows written per call group
-        key = (id(feats), feats.data_ptr(), getattr(feats, "_version", 0), C, int(self.engine.cfg.n_items))
-        if getattr(self, "_fly_feat_key", None) != key:
-            fx = torch.empty((int(self.engine.cfg.n_items), feats.shape[1]), dtype=feats.dtype, device=self.dev)
-            for c in range(C):
-                fx[c * n_items:c * n_items + n_valid] = feats[:n_valid]
-            self._fly_feat, self._fly_feat_key = fx, key
-        fx = self._fly_feat
+        fx = self._fly_feats(feats, C, n_items, n_valid)
         parts, xo = [], base_x
         for c, d in enumerate(draws):
             parts.append(d.uniq + c * n_items)
@@ -914,6 +1004,46 @@ class _EngineRunner:
                 o0 += n_x[c]
                 out_u = out_u.index_add(0, d.ui_x, o - o.detach())
             outs.append(out_u[d.inv].to(initial_h.device))
+        return outs
+
+    def _fly_feats(self, feats, C, n_items, n_valid):
+        """Feature rows of fly_calls' node ids: call c's copy of the table at
+        c * n_items (made once per feature tensor); rows from C * n_items are
+        the virtual nodes', written per call group."""
+        key = (id(feats), feats.data_ptr(), getattr(feats, "_version", 0), C, int(self.engine.cfg.n_items))
+        if getattr(self, "_fly_feat_key", None) != key:
+            fx = torch.empty((int(self.engine.cfg.n_items), feats.shape[1]), dtype=feats.dtype, device=self.dev)
+            for c in range(C):
+                fx[c * n_items:c * n_items + n_valid] = feats[:n_valid]
+            self._fly_feat, self._fly_feat_key = fx, key
+        return self._fly_feat
+
+    def _fly_calls_merged(self, initial_h, feats, ids_c, n_items, n_valid):
+        """fly_calls with the calls' walks merged per layer (_fly_tables_merged)."""
+        m = self.model
+        C = len(ids_c)
+        tabs, uniq, inv, ids_x, ui_x = _fly_tables_merged(m.g, n_items, ids_c, m.n_layers, m.n_hops,
+                                                          m.alpha, m.T)
+        n_x = int(ids_x.shape[0])
+        base_x = C * n_items
+        if base_x + n_x > int(self.engine.cfg.n_items):
+            raise RuntimeError("on-the-fly calls exceed the engine's node rows")
+        fx = self._fly_feats(feats, C, n_items, n_valid)
+        ids = uniq
+        if n_x:
+            fx[base_x:base_x + n_x] = feats[ids_x]
+            ids = torch.cat([uniq, torch.arange(base_x, base_x + n_x, dtype=torch.int64, device=self.dev)])
+        out = _EngineFn.apply(self, fx, None, ids, tabs, *self.params())
+        n_u = int(uniq.shape[0])
+        out_u = out[:n_u]
+        if n_x:
+            o = out[n_u:]
+            out_u = out_u.index_add(0, ui_x, o - o.detach())
+        full = out_u[inv]
+        outs, p0 = [], 0
+        for i in ids_c:
+            outs.append(full[p0:p0 + int(i.shape[0])].to(initial_h.device))
+            p0 += int(i.shape[0])
         return outs
 
     def _fly_with_repeats(self, feats, draws):

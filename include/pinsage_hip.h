@@ -136,6 +136,21 @@ int pinsage_ppr_topk(const int64_t* indptr, const int32_t* indices, int64_t n_al
                      void* mt, uint64_t seed, uint32_t offset, int64_t src_base, void* ws,
                      int64_t ws_bytes, double* w_out, int64_t* nb_out, float* wn_out,
                      int32_t* nb32_out, int64_t t_norm, void* stream);
+/* pinsage_ppr_topk (Philox mode) over n_seg consecutive segments of sources in
+ * one call: segment i = sources[seg_start[i] .. seg_start[i+1]) is keyed by
+ * (seg_seed[i], hop, seg_base[i] + j, offset), so each segment draws exactly
+ * what its own pinsage_ppr_topk call would.  Serves the train step's model
+ * calls on the fly (pinsage_model.py:142-154, called at :183-185 once per
+ * call), one walk per segment and one top-k pass and zero-degree check for
+ * all.  seg_start / seg_seed / seg_base are host arrays (n_seg + 1, n_seg,
+ * n_seg); ws >= pinsage_ppr_topk_workspace(seg_start[n_seg], n_hops, 0).
+ * Synchronises the stream. */
+int pinsage_ppr_topk_segments(const int64_t* indptr, const int32_t* indices, int64_t n_all,
+                              const int64_t* sources, int64_t n_seg, const int64_t* seg_start,
+                              const uint64_t* seg_seed, const int64_t* seg_base, int64_t n_hops,
+                              float alpha, int64_t k, uint32_t offset, void* ws, int64_t ws_bytes,
+                              double* w_out, int64_t* nb_out, float* wn_out, int32_t* nb32_out,
+                              int64_t t_norm, void* stream);
 /* sample_neighborhood (pinsage_model.py:88-101): dense f64 [n_src][n_all]. */
 int pinsage_visit_dense(const int32_t* trace, const int64_t* sources, int64_t n_src,
                         int64_t n_hops, int64_t n_all, double* dense, void* stream);

@@ -181,3 +181,58 @@ def test_train_step_on_the_fly_vs_oracle(margin, repeats):
                     assert parity_util.rel(prm.grad.cpu().numpy(), pc[k].grad.numpy()) <= 1e-4, (c, k)
         finally:
             os.chdir(cwd)
+
+
+def test_philox_merged_calls_match_per_call_walks():
+    """Philox mode: the train step's three calls walk each layer in ONE
+    pinsage_ppr_topk_segments call (per-call seeds drawn in the per-call order,
+    pinsage_model._fly_tables_merged) -- the same draws, losses and parameters
+    as walking call by call (PINSAGE_FLY_MERGE=0), and the generator ends in
+    the same state; repeated ids inside and across calls."""
+    import pinsage_model as pm
+    import pinsage_training as pt
+    pm.set_rng_mode("philox")
+    old = os.environ.get("PINSAGE_FLY_MERGE")
+    try:
+        with tempfile.TemporaryDirectory() as tmp:
+            cwd = os.getcwd()
+            os.chdir(tmp)
+            try:
+                pg, g, indptr, indices, feats, pos = _problem(tmp)
+                rng = np.random.default_rng(17)
+                batches = []
+                for _ in range(3):
+                    b = np.stack([rng.integers(0, N, 96) for _ in range(3)], 1).astype(np.int64)
+                    b[3, 0] = b[10, 0] = b[20, 0]
+                    b[7, 1] = b[8, 1]
+                    b[30, 2] = b[0, 0]
+                    batches.append(torch.from_numpy(b))
+
+                def run(merge):
+                    os.environ["PINSAGE_FLY_MERGE"] = merge
+                    torch.manual_seed(1)
+                    tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+                    torch.manual_seed(2)
+                    tr.model = pm.PinSageModel(g, N, 2, tr.dimensions, 200, 0.85, 5, None)
+                    tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+                    tr.margin = 3.0
+                    torch.manual_seed(99)
+                    losses = [float(tr.train_batch(b)[0]) for b in batches]
+                    torch.cuda.synchronize()
+                    flat = torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu()
+                    return losses, flat, torch.get_rng_state()
+
+                l0, p0, s0 = run("0")
+                l1, p1, s1 = run("1")
+                assert torch.equal(s0, s1)
+                for a, b in zip(l0, l1):
+                    assert abs(a - b) <= 1e-6 * abs(a) + 1e-9, (l0, l1)
+                assert ((p0 - p1).norm() / p0.norm()).item() < 1e-6
+            finally:
+                os.chdir(cwd)
+    finally:
+        pm.set_rng_mode("mt19937")
+        if old is None:
+            os.environ.pop("PINSAGE_FLY_MERGE", None)
+        else:
+            os.environ["PINSAGE_FLY_MERGE"] = old
