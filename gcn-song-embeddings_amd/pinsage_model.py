@@ -697,10 +697,20 @@ def _param_order(module_like_n_layers):
     return names + ["G1.weight", "G1.bias", "G2.weight"]
 
 
+_DEFERRED_DESTROY = []
+
+
+def _destroy_deferred():
+    while _DEFERRED_DESTROY:
+        nat.lib().pinsage_engine_destroy(_DEFERRED_DESTROY.pop())
+
+
 class _Engine:
     """Owns a native engine handle for one configuration."""
 
     def __init__(self, n_items, d_in, hid, out, n_layers, T, max_pos):
+        if not torch.cuda.is_current_stream_capturing():
+            _destroy_deferred()
         self.cfg = nat.EngineConfig(n_items, d_in, hid, out, n_layers, T, max_pos)
         h = ctypes.c_void_p()
         nat.check(nat.lib().pinsage_engine_create(ctypes.byref(self.cfg), ctypes.byref(h)),
@@ -712,9 +722,15 @@ class _Engine:
         nat.lib().pinsage_engine_offsets(h, ctypes.byref(self.off))
 
     def __del__(self):
+        # an engine finalised while a stream is capturing is destroyed later
+        # (its streams / events must not be released inside a capture)
         try:
             if getattr(self, "h", None):
-                nat.lib().pinsage_engine_destroy(self.h)
+                if torch.cuda.is_current_stream_capturing():
+                    _DEFERRED_DESTROY.append(self.h)
+                else:
+                    _destroy_deferred()
+                    nat.lib().pinsage_engine_destroy(self.h)
         except Exception:
             pass
 

@@ -14,6 +14,7 @@ slice; gradients are averaged with one RCCL all-reduce of the flat buffer.
 from __future__ import annotations
 
 import ctypes
+import gc
 import os
 import time
 
@@ -601,7 +602,20 @@ class _FusedStep:
         """Per workspace p: the frontier graph (stage this step's ids, frontier),
         the step graph (stage coefficients, layers ... Adam, publish), and the
         step graph whose branch stages the predicted next ids into workspace
-        1-p and computes their frontier there."""
+        1-p and computes their frontier there.  The cyclic garbage collector is
+        off while capturing: an unreachable engine it finalised mid-capture
+        would release HIP streams / events inside the capture (the process
+        aborted in test_engine_variants_train_alike)."""
+        was = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        try:
+            return self._capture_graphs(B, sig)
+        finally:
+            if was:
+                gc.enable()
+
+    def _capture_graphs(self, B, sig):
         adam = not self.dist
         staged = self.dist and self.dp_buckets  # DP: backward stage 1 in its own graph (g2)
         stage = 0 if staged else None
