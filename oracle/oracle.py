@@ -382,7 +382,7 @@ class RefTrainer:
                                 self.out) for c in range(3)]
             loss = max_margin_loss(*hs, self.margin)
             (loss / world).backward()
-            losses.append(float(loss))
+            losses.append(float(loss.detach()))
         self.opt.step()
         return losses
 
