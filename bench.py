@@ -54,6 +54,8 @@ CONFIGS = {
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak
+PEAK_BF16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
+SPLIT_BF16_CEIL_TFLOPS = PEAK_BF16_TFLOPS / 6  # fp32 products at six bf16 MFMAs each
 
 
 def log(*a):
@@ -455,6 +457,9 @@ def main():
                      "arithmetic": gemm_arith,
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                     # the ceiling of the arithmetic it runs: six bf16 MFMAs per fp32 product
+                     "split_bf16_ceiling": SPLIT_BF16_CEIL_TFLOPS,
+                     "frac_split_bf16_ceiling": achieved_tf / SPLIT_BF16_CEIL_TFLOPS,
                      "traffic_source": traffic_src, "mfma_busy_pmc": mfma_busy,
                      "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg,
                      "algorithmic_bytes_per_launch": 4.0 * (U0 * d + d * hid + U0 * hid)},
@@ -471,6 +476,14 @@ def main():
                           "mfma_flops": agg_flops,
                           "mfma_frac": (agg_flops / (a_avg * 1e-3) / 1e12 / PEAK_FP32_TFLOPS
                                         if a_avg > 0 else 0.0),
+                          # floors: algorithmic bytes at HBM peak, its projection at the fp32 MFMA
+                          # peak; "frac_of_floor" = the larger floor (perfect overlap) / measured
+                          "floor_hbm_ms": agg_bytes / PEAK_HBM_GBS / 1e6,
+                          "floor_mfma_ms": agg_flops / PEAK_FP32_TFLOPS / 1e9,
+                          "frac_of_floor": (max(agg_bytes / PEAK_HBM_GBS / 1e6, agg_flops / PEAK_FP32_TFLOPS / 1e9)
+                                            / a_avg if a_avg > 0 else 0.0),
+                          "frac_of_serial_floor": ((agg_bytes / PEAK_HBM_GBS / 1e6 + agg_flops / PEAK_FP32_TFLOPS / 1e9)
+                                                   / a_avg if a_avg > 0 else 0.0),
                           "note": "algorithmic = unique q rows + index/weight + agg"
                                   + (" + self rows + W + y/norm outputs" if fused else "")
                                   + "; logical counts every (row, slot) read, most served by L2 / "
