@@ -73,6 +73,7 @@ _SIGS = {
     "pinsage_visit_dense": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, vp]),
     "pinsage_frontier_workspace": (i64, [i64]),
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),
+    "pinsage_frontier_local_idx": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "pinsage_linear": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, ctypes.c_int, vp, i64, vp]),
     "pinsage_gemm_ex": (ctypes.c_int, [i64, i64, i64, ctypes.c_int, ctypes.c_int, vp, i64, vp, vp, i64,
                                        vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -98,6 +99,7 @@ _SIGS = {
     "pinsage_knn_cosine": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, i64, f32, vp, i64, vp, vp, vp]),
     "pinsage_engine_create": (ctypes.c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(vp)]),
     "pinsage_engine_destroy": (None, [vp]),
+    "pinsage_engine_live_count": (i64, []),
     "pinsage_engine_workspace_bytes": (i64, [vp]),
     "pinsage_engine_init_workspace": (i32, [vp, vp, vp]),
     "pinsage_engine_num_params": (i64, [vp]),
@@ -112,6 +114,7 @@ _SIGS = {
     "pinsage_engine_loss": (ctypes.c_int, [vp, vp, i64, f32, ctypes.c_int, vp]),
     "pinsage_engine_set_output_grad": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_backward": (ctypes.c_int, [vp, vp, vp]),
+    "pinsage_engine_reset_backward": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_backward_stage": (ctypes.c_int, [vp, vp, ctypes.c_int, vp]),
     "pinsage_engine_adam": (ctypes.c_int, [vp, vp, f32, f32, f32, vp]),
     "pinsage_engine_backward_adam": (ctypes.c_int, [vp, vp, vp, f32, f32, f32, vp]),

@@ -22,11 +22,23 @@ struct AggNextQ {
 };
 
 int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
+// the fragment form (agg_wf_kernel): d, hid multiples of 32, out 128, T <= 64
+int agg_wf_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
+// bytes of W's fragment-order bf16 planes (3 x 128 x (d + hid) x 2)
+int64_t agg_wf_planes_bytes(int64_t d, int64_t hid);
+// the fragment form's rows per tile (16 or 32) for an expected row count
+int agg_wf_rows(int64_t S_max);
+// W [128][K] -> fragment-order planes for the rows form `rows`
+int launch_split_wfrag(const float* W, int64_t ldw, int K, int rows, uint16_t* planes, hipStream_t st);
 // next (optional): fuse the next layer's Q projection; *next_done is set to 1
-// when the chosen kernel form did it (the 32-row form), else 0
+// when the chosen kernel form did it (the 32-row form), else 0.
+// planes (optional, agg_wf_planes_bytes): run the fragment form (unless next
+// is set or PINSAGE_AGGW_FORM=0); planes_rows 0: split W into them first,
+// 16 / 32: they already hold W split for that rows form (launch_split_wfrag)
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
-                 const AggNextQ* next = nullptr, int* next_done = nullptr);
+                 const AggNextQ* next = nullptr, int* next_done = nullptr, uint16_t* planes = nullptr,
+                 int planes_rows = 0);
 
 }  // namespace ps

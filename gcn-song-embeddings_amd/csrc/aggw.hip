@@ -449,6 +449,342 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
   }
 }
 
+// ---------------------------------------------------------------- fragment form
+// The default form (round 4).  W is split ONCE per forward (split_wfrag_kernel)
+// into its bf16 hi / mid / lo planes, stored in MFMA fragment order: every B
+// fragment a wave needs is one coalesced 1 KiB load, and no wave converts W
+// (the LDS-tile forms above re-split W in every workgroup, and their per-lane
+// W reads touch a different 64-B segment per lane).  Per tile of ROWS rows:
+//   1. [h_self || agg] staged in LDS as before (coalesced row reads; the
+//      aggregate is the fma chain in slot order t = 0, 1, ..., bitwise
+//      agg_kernel's, and is written out once);
+//   2. the projection: K is cut into KS-wide MFMA steps dealt round-robin to
+//      the 8 waves (step s to wave s % 8), and each wave accumulates ALL 128
+//      output columns over its steps (4 accumulators of 32x32, or 8 of
+//      16x16), so one A fragment (read from LDS, split once) feeds 24 MFMAs;
+//      the wave's next step's B fragments load while the current step runs;
+//   3. the 8 partial tiles meet in LDS in wave order, then bias, LeakyReLU
+//      and the row L2 norm.
+//   ROWS 32: v_mfma_f32_32x32x16_bf16, KS 16: lane (row l % 32, half l / 32)
+//            supplies k = 16 s + 8 (l / 32) + [0, 8);
+//   ROWS 16: v_mfma_f32_16x16x32_bf16, KS 32: lane (row l % 16, quarter
+//            l / 16) supplies k = 32 s + 8 (l / 16) + [0, 8).
+template <int ROWS>
+struct WfGeom;
+template <>
+struct WfGeom<32> {
+  static constexpr int CW = 32, NCG = 4, KS = 16, NJ = 8;  // NJ: float4 columns per thread per gather pass
+  typedef float acc_t __attribute__((ext_vector_type(16)));
+};
+template <>
+struct WfGeom<16> {
+  static constexpr int CW = 16, NCG = 8, KS = 32, NJ = 4;
+  typedef float acc_t __attribute__((ext_vector_type(4)));
+};
+
+constexpr int kWfThreads = 512;
+constexpr int kWfWaves = kWfThreads / 64;
+constexpr int kWfOut = 128;   // out_dim
+constexpr int kWfTMax = 64;   // fanout held in LDS per row
+constexpr int kWfRed = kWfOut + 4;  // LDS row of a partial output tile
+
+template <int ROWS>
+int64_t wf_lds_bytes(int64_t K) {
+  const int64_t tile = std::max<int64_t>((int64_t)ROWS * (K + 4), (int64_t)kWfWaves * ROWS * kWfRed);
+  return (tile + 2 * ROWS * kWfTMax + ROWS) * 4;
+}
+
+// Fragment-order planes of W [128][K] (row stride ldw): chunk c = (s, cg,
+// lane) of 8 bf16 at planes[((c >> 6) * 3 + p) * 512 + (c & 63) * 8], holding
+// plane p of W[CW cg + lane % CW][KS s + 8 (lane / CW) + i], i < 8 -- the B
+// fragment lane `lane` supplies in step s for column group cg.  The split is
+// split3's (bf16split.h), so the products equal the GEMM's.
+template <int ROWS>
+__global__ __launch_bounds__(256) void split_wfrag_kernel(const float* __restrict__ W, int64_t ldw, int K,
+                                                          uint16_t* __restrict__ planes) {
+  using Gm = WfGeom<ROWS>;
+  const int64_t n = (int64_t)K * kWfOut / 8;  // chunks
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const int lane = (int)(c & 63);
+  const int64_t rest = c >> 6;
+  const int cg = (int)(rest % Gm::NCG), s = (int)(rest / Gm::NCG);
+  const int col = Gm::CW * cg + lane % Gm::CW, k = Gm::KS * s + 8 * (lane / Gm::CW);
+  const float* src = W + (int64_t)col * ldw + k;
+  bf16x8 H, M, L;
+  split3(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 4), H, M, L);
+  uint16_t* o = planes + (rest * 3) * 512 + lane * 8;
+  *reinterpret_cast<bf16x8*>(o) = H;
+  *reinterpret_cast<bf16x8*>(o + 512) = M;
+  *reinterpret_cast<bf16x8*>(o + 1024) = L;
+}
+
+template <int ROWS>
+__global__ __launch_bounds__(kWfThreads) void agg_wf_kernel(
+    const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
+    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc, const float* __restrict__ wloc,
+    int T, const int* __restrict__ nS, int64_t n_static, const uint16_t* __restrict__ planes,
+    const float* __restrict__ bias, float* __restrict__ y, float* __restrict__ nrm_out, float* __restrict__ agg) {
+  using Gm = WfGeom<ROWS>;
+  using acc_t = typename Gm::acc_t;
+  constexpr int NA = (int)(sizeof(acc_t) / 4);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int K = d + hid, lda = K + 4;  // row stride 4 mod 64 banks: b128 fragment reads spread
+  const int64_t tile_f = std::max<int64_t>((int64_t)ROWS * lda, (int64_t)kWfWaves * ROWS * kWfRed);
+  float* sA = lds;   // [ROWS][lda]; the partial output tiles [waves][ROWS][kWfRed] after the products
+  float* red = lds;
+  int* sLoc = reinterpret_cast<int*>(lds + tile_f);           // [ROWS][kWfTMax]
+  float* sW = reinterpret_cast<float*>(sLoc + ROWS * kWfTMax);  // [ROWS][kWfTMax]
+  int* sSelf = reinterpret_cast<int*>(sW + ROWS * kWfTMax);     // [ROWS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int S = K / Gm::KS;
+  const int lr = lane % ROWS, kq = lane / ROWS;
+  // B fragments of step s: 3 planes x NCG column groups, 1 KiB each
+  auto load_b = [&](int s, bf16x8 (&bH)[Gm::NCG], bf16x8 (&bM)[Gm::NCG], bf16x8 (&bL)[Gm::NCG])
+      __attribute__((always_inline)) {
+    const bf16x8* bp = reinterpret_cast<const bf16x8*>(planes + ((int64_t)(s * Gm::NCG) * 3 * 64 + lane) * 8);
+#pragma unroll
+    for (int c = 0; c < Gm::NCG; ++c) {
+      bH[c] = bp[(c * 3 + 0) * 64];
+      bM[c] = bp[(c * 3 + 1) * 64];
+      bL[c] = bp[(c * 3 + 2) * 64];
+    }
+  };
+  // rows dealt in contiguous ranges: block b of G owns [F b / G, F (b+1) / G)
+  // in near-equal tiles of <= ROWS rows
+  const int64_t F = nS ? (int64_t)*nS : n_static;
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / nb, len = F * (b + 1) / nb - rb;
+  const int ntile = (int)((len + ROWS - 1) / ROWS);
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int64_t r0 = rb + len * tile / ntile;
+    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
+    // ---- slot lists and self-row indices of the tile
+    for (int i = tid; i < ROWS * T; i += kWfThreads) {
+      const int row = i / T, t = i - row * T;
+      const bool ok = row < nrows;
+      sLoc[row * kWfTMax + t] = ok ? loc[(r0 + row) * T + t] : 0;
+      sW[row * kWfTMax + t] = ok ? wloc[(r0 + row) * T + t] : 0.f;
+    }
+    if (tid < ROWS) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : 0;
+    __syncthreads();
+    // ---- self rows -> A[:, 0:d)
+    {
+      const int d4 = d >> 2;
+      for (int i = tid; i < ROWS * d4; i += kWfThreads) {
+        const int row = i / d4, c4 = i - row * d4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nrows) v = *reinterpret_cast<const float4*>(h + (int64_t)sSelf[row] * ldh + 4 * c4);
+        *reinterpret_cast<float4*>(sA + row * lda + 4 * c4) = v;
+      }
+    }
+    // ---- aggregate -> A[:, d:K) and agg: thread (row tid / TPR, float4
+    //      columns (tid % TPR) + TPR j); four slots' rows in flight per round
+    {
+      constexpr int TPR = kWfThreads / ROWS, NJ = Gm::NJ;
+      const int row = tid / TPR, c0 = tid % TPR, h4 = hid >> 2;
+      const int* sl = sLoc + row * kWfTMax;
+      const float* sw = sW + row * kWfTMax;
+      for (int j0 = 0; j0 < h4; j0 += TPR * NJ) {
+        float4 a[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nrows) {
+          int t = 0;
+          for (; t + 4 <= T; t += 4) {
+            float4 x[4][NJ];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sl[t + u] * hid);
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) x[u][j] = qr[min(j0 + c0 + TPR * j, h4 - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float w = sw[t + u];
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) {
+                a[j].x = fmaf(w, x[u][j].x, a[j].x);
+                a[j].y = fmaf(w, x[u][j].y, a[j].y);
+                a[j].z = fmaf(w, x[u][j].z, a[j].z);
+                a[j].w = fmaf(w, x[u][j].w, a[j].w);
+              }
+            }
+          }
+          for (; t < T; ++t) {
+            const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sl[t] * hid);
+            const float w = sw[t];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const float4 x = qr[min(j0 + c0 + TPR * j, h4 - 1)];
+              a[j].x = fmaf(w, x.x, a[j].x);
+              a[j].y = fmaf(w, x.y, a[j].y);
+              a[j].z = fmaf(w, x.z, a[j].z);
+              a[j].w = fmaf(w, x.w, a[j].w);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = j0 + c0 + TPR * j;
+          if (c < h4) {
+            *reinterpret_cast<float4*>(sA + row * lda + d + 4 * c) = a[j];
+            if (row < nrows) *reinterpret_cast<float4*>(agg + (r0 + row) * hid + 4 * c) = a[j];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- projection: wave w, steps s = w, w + 8, ..., all 128 columns
+    acc_t acc[Gm::NCG];
+#pragma unroll
+    for (int c = 0; c < Gm::NCG; ++c)
+#pragma unroll
+      for (int e = 0; e < NA; ++e) acc[c][e] = 0.f;
+    if (wave < S) {
+      bf16x8 bH[Gm::NCG], bM[Gm::NCG], bL[Gm::NCG];
+      load_b(wave, bH, bM, bL);
+      const float* arow = sA + lr * lda + 8 * kq;
+      for (int s = wave; s < S; s += kWfWaves) {
+        const int sn = s + kWfWaves < S ? s + kWfWaves : s;  // (the last step reloads itself: no branch)
+        bf16x8 nH[Gm::NCG], nM[Gm::NCG], nL[Gm::NCG];
+        load_b(sn, nH, nM, nL);
+        bf16x8 aH, aM, aL;
+        const float* ap = arow + Gm::KS * s;
+        split3(*reinterpret_cast<const float4*>(ap), *reinterpret_cast<const float4*>(ap + 4), aH, aM, aL);
+#define PS_WF_ALL(X, Y)                                                                                   \
+  _Pragma("unroll") for (int c = 0; c < Gm::NCG; ++c) {                                                   \
+    if constexpr (ROWS == 32) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, Y[c], acc[c], 0, 0, 0); \
+    else acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X, Y[c], acc[c], 0, 0, 0);                    \
+  }
+        PS_WF_ALL(aL, bH)
+        PS_WF_ALL(aH, bL)
+        PS_WF_ALL(aM, bM)
+        PS_WF_ALL(aM, bH)
+        PS_WF_ALL(aH, bM)
+        PS_WF_ALL(aH, bH)
+#undef PS_WF_ALL
+#pragma unroll
+        for (int c = 0; c < Gm::NCG; ++c) {
+          bH[c] = nH[c];
+          bM[c] = nM[c];
+          bL[c] = nL[c];
+        }
+      }
+    }
+    __syncthreads();  // every wave is done reading the A tile
+    // ---- the waves' partial tiles -> LDS (over the A tile), summed in wave order
+    float* rw = red + wave * ROWS * kWfRed;
+#pragma unroll
+    for (int c = 0; c < Gm::NCG; ++c)
+#pragma unroll
+      for (int e = 0; e < NA; ++e) {
+        const int row = ROWS == 32 ? (e & 3) + 8 * (e >> 2) + 4 * kq : 4 * kq + e;
+        rw[row * kWfRed + Gm::CW * c + lane % Gm::CW] = acc[c][e];
+      }
+    __syncthreads();
+    {
+      // thread: row tid / TPR, columns CPT (tid % TPR) .. + CPT - 1
+      constexpr int TPR = kWfThreads / ROWS, CPT = kWfOut / TPR, NQ = CPT / 4;
+      const int row = tid / TPR, c0 = CPT * (tid % TPR);
+      float4 sm[NQ];
+#pragma unroll
+      for (int qv = 0; qv < NQ; ++qv) sm[qv] = *reinterpret_cast<const float4*>(red + row * kWfRed + c0 + 4 * qv);
+      for (int w = 1; w < kWfWaves; ++w)
+#pragma unroll
+        for (int qv = 0; qv < NQ; ++qv) {
+          const float4 p = *reinterpret_cast<const float4*>(red + (w * ROWS + row) * kWfRed + c0 + 4 * qv);
+          sm[qv].x += p.x;
+          sm[qv].y += p.y;
+          sm[qv].z += p.z;
+          sm[qv].w += p.w;
+        }
+      float s2 = 0.f;
+#pragma unroll
+      for (int qv = 0; qv < NQ; ++qv) {
+        const float4 bv = *reinterpret_cast<const float4*>(bias + c0 + 4 * qv);
+        sm[qv].x = lrelu(sm[qv].x + bv.x);
+        sm[qv].y = lrelu(sm[qv].y + bv.y);
+        sm[qv].z = lrelu(sm[qv].z + bv.z);
+        sm[qv].w = lrelu(sm[qv].w + bv.w);
+        s2 += sm[qv].x * sm[qv].x + sm[qv].y * sm[qv].y + sm[qv].z * sm[qv].z + sm[qv].w * sm[qv].w;
+      }
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+      const float nrm = sqrtf(s2);
+      if (row < nrows) {
+#pragma unroll
+        for (int qv = 0; qv < NQ; ++qv)
+          *reinterpret_cast<float4*>(y + (r0 + row) * kWfOut + c0 + 4 * qv) =
+              make_float4(sm[qv].x / nrm, sm[qv].y / nrm, sm[qv].z / nrm, sm[qv].w / nrm);
+        if (tid % TPR == 0 && nrm_out) nrm_out[r0 + row] = nrm;
+      }
+    }
+    __syncthreads();  // LDS is reused by the next tile
+  }
+}
+
+int agg_wf_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
+  // PINSAGE_AGGW_FORM=0: the LDS-tile forms (A/B)
+  if (getenv("PINSAGE_AGGW_FORM") && atoi(getenv("PINSAGE_AGGW_FORM")) != 1) return 0;
+  return out == kWfOut && d > 0 && hid > 0 && d % 32 == 0 && hid % 32 == 0 && T >= 1 && T <= kWfTMax &&
+         wf_lds_bytes<32>(d + hid) <= 160 * 1024;
+}
+
+int64_t agg_wf_planes_bytes(int64_t d, int64_t hid) { return 3 * kWfOut * (d + hid) * 2; }
+
+// the rows form of an expected row count (the planes' fragment order follows it)
+int agg_wf_rows(int64_t S_max) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int64_t min32 =
+      getenv("PINSAGE_AGGWF32_MIN_ROWS") ? atoll(getenv("PINSAGE_AGGWF32_MIN_ROWS")) : 16 * (int64_t)cus;
+  return S_max >= min32 ? 32 : 16;
+}
+
+int launch_split_wfrag(const float* W, int64_t ldw, int K, int rows, uint16_t* planes, hipStream_t st) {
+  PS_REQUIRE(K % 32 == 0 && (rows == 16 || rows == 32) && ldw >= K && ldw % 4 == 0, kErrArg,
+             "split_wfrag: K % 32 == 0, rows form 16 or 32");
+  const int64_t n = (int64_t)K * kWfOut / 8;
+  if (rows == 32)
+    hipLaunchKernelGGL(split_wfrag_kernel<32>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, ldw, K, planes);
+  else
+    hipLaunchKernelGGL(split_wfrag_kernel<16>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, ldw, K, planes);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+static int launch_agg_wf(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
+                         const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
+                         int rows, const uint16_t* planes, const float* bias, float* y, float* nrm, float* agg,
+                         hipStream_t st) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  static bool prepared = false;
+  if (!prepared) {
+    PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_wf_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_wf_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024));
+    prepared = true;
+  }
+  // ~3/4 of a tile per block over every CU (one block per CU)
+  const int64_t per = rows * 3 / 4;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (S_max + per - 1) / per));
+  if (rows == 32)
+    hipLaunchKernelGGL((agg_wf_kernel<32>), dim3(grid), dim3(kWfThreads), (unsigned)wf_lds_bytes<32>(d + hid), st, h,
+                       ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, planes, bias, y, nrm, agg);
+  else
+    hipLaunchKernelGGL((agg_wf_kernel<16>), dim3(grid), dim3(kWfThreads), (unsigned)wf_lds_bytes<16>(d + hid), st, h,
+                       ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, planes, bias, y, nrm, agg);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 static int agg_w32_supported(int64_t d, int64_t hid, int64_t T) {
   const int64_t K = d + hid;
   const int64_t lds = (int64_t)kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
@@ -470,9 +806,20 @@ int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
-                 const AggNextQ* next, int* next_done) {
-  PS_REQUIRE(agg_w_supported(d, hid, kAwOut, T), kErrArg, "agg_w: unsupported shape");
+                 const AggNextQ* next, int* next_done, uint16_t* planes, int planes_rows) {
   if (next_done) *next_done = 0;
+  if (planes && !(next && next->q) && agg_wf_supported(d, hid, kWfOut, T)) {
+    if (S_max <= 0) return kOk;
+    int rows = planes_rows;
+    if (rows == 0) {  // split W here (the engine splits once per forward, ahead)
+      rows = agg_wf_rows(S_max);
+      PS_TRY(launch_split_wfrag(W, d + hid, d + hid, rows, planes, st));
+    }
+    PS_REQUIRE(rows == 16 || rows == 32, kErrArg, "agg_w: planes_rows must be 0, 16 or 32");
+    return launch_agg_wf(h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, S_max, rows, planes, bias, y,
+                         nrm, agg, st);
+  }
+  PS_REQUIRE(agg_w_supported(d, hid, kAwOut, T), kErrArg, "agg_w: unsupported shape");
   const int K = d + hid;
   const int lds = kAwRows * (K + 4) * 4 + 2 * kAwRows * kAwTMax * 4 + kAwRows * 4;
   static int prepared = 0;

@@ -41,6 +41,9 @@ int launch_agg(const float*, int, const int32_t*, const float*, int, const int*,
                hipStream_t);
 int launch_gather_rows(const float*, int64_t, int64_t, int, const int64_t*, int64_t, float*, int64_t,
                        hipStream_t);
+int launch_l2norm_rows(float* y, int64_t n, int out, float* norms, hipStream_t st);
+int launch_set_rank_table(const int64_t*, int64_t, const int32_t*, int64_t, int, const unsigned long long*,
+                          const uint32_t*, int32_t*, hipStream_t);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t, float*, float*,
                           int, const int*, int*, int64_t, hipStream_t);
 int64_t knn_scratch_bytes(int64_t, int64_t);
@@ -461,6 +464,19 @@ int pinsage_frontier_step(const int64_t* nodeset, int64_t n, const int32_t* nb_t
   return kOk;
 }
 
+int pinsage_frontier_local_idx(const int64_t* nodeset, int64_t n, const int32_t* nb_table, int64_t ld, int64_t T,
+                               int64_t n_items, const void* ws, int32_t* local_idx, void* stream) {
+  if (n < 0 || T <= 0 || ld < T || n_items <= 0 || !ws) {
+    set_error("frontier_local_idx: bad sizes");
+    return kErrArg;
+  }
+  const int64_t nw = bitset_words(n_items);
+  const char* b = static_cast<const char*>(ws);
+  const auto* bits = reinterpret_cast<const unsigned long long*>(b);
+  const auto* prefix = reinterpret_cast<const uint32_t*>(b + align_up(nw * 8, 256));
+  return launch_set_rank_table(nodeset, n, nb_table, ld, (int)T, bits, prefix, local_idx, (hipStream_t)stream);
+}
+
 // ------------------------------------------------------------------ single kernels
 int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
                    const float* W, const float* bias, int64_t N, int act, float* C, int64_t ldc,
@@ -602,17 +618,19 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
                              const float* w, int64_t n_rows, int64_t T, const float* W,
                              const float* bias, int64_t out, uint16_t* W_planes, float* y,
                              float* norms, float* agg, void* stream) {
-  (void)W_planes;  // (scratch of an earlier kernel form; unused)
-  if (!agg_w_supported(d, hid, out, T) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX || ldh < d ||
+  const bool wf = W_planes && agg_wf_supported(d, hid, out, T);
+  if (!(wf || agg_w_supported(d, hid, out, T)) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX || ldh < d ||
       ldh % 4 != 0) {
-    set_error("conv_agg_project: out_dim must be 128, d + hid a multiple of 64, d and hid multiples of 4, "
-              "1 <= T <= 64");
+    set_error("conv_agg_project: out_dim must be 128, 1 <= T <= 64, and d, hid multiples of 32 (with W_planes) "
+              "or d + hid a multiple of 64 and d, hid multiples of 4");
     return kErrArg;
   }
   if (n_rows == 0) return kOk;
   // the engine's kernel (aggw.hip): the form by row count, rows from n_rows
+  // (W_planes: scratch of agg_wf_planes_bytes for the fragment form, which
+  // splits W into it first; null runs the LDS-tile forms)
   return launch_agg_w(h, ldh, (int)d, self_src, q, (int)hid, loc, w, (int)T, nullptr, n_rows, n_rows, W, bias, y,
-                      norms, agg, (hipStream_t)stream);
+                      norms, agg, (hipStream_t)stream, nullptr, nullptr, W_planes, 0);
 }
 
 int pinsage_gather_rows(const float* h, int64_t ldh, int64_t n_h, int64_t d, const int64_t* idx, int64_t n,
@@ -627,12 +645,35 @@ int pinsage_gather_rows(const float* h, int64_t ldh, int64_t n_h, int64_t d, con
 int pinsage_concat_linear_l2norm(const float* h, int64_t ldh, const int32_t* self_idx, int64_t n, int64_t d,
                                  const float* agg, int64_t ld_agg, int64_t hid, const float* W,
                                  const float* bias, int64_t out, float* y, float* norms, void* stream) {
-  if (n < 0 || n > INT32_MAX || d <= 0 || hid <= 0 || d + hid > INT32_MAX || out <= 0 || out > 128 ||
-      ldh < d || ld_agg < hid) {
-    set_error("concat_linear_l2norm: bad sizes (0 < out <= 128)");
+  if (n < 0 || n > INT32_MAX || d <= 0 || hid <= 0 || d + hid > INT32_MAX || out <= 0 || out > INT32_MAX ||
+      ldh < d || ld_agg < hid || d % 4 != 0) {
+    set_error("concat_linear_l2norm: bad sizes");
     return kErrArg;
   }
   if (n == 0) return kOk;
+  if (out > 128) {
+    // wider than the fused L2-norm epilogue: the GEMM with bias + LeakyReLU,
+    // then the row normalisation in place
+    GemmParams p;
+    p.M = (int)n;
+    p.N = (int)out;
+    p.K = (int)(d + hid);
+    p.a = h;
+    p.lda = ldh;
+    p.a_idx = self_idx;
+    p.K1 = (int)d;
+    p.a2 = agg;
+    p.lda2 = ld_agg;
+    p.b = W;
+    p.ldb = d + hid;
+    p.c = y;
+    p.ldc = out;
+    p.bias = bias;
+    p.act = true;
+    p.stream_k = 0;
+    PS_TRY(launch_gemm(p, (hipStream_t)stream));
+    return launch_l2norm_rows(y, n, (int)out, norms, (hipStream_t)stream);
+  }
   GemmParams p;
   p.M = (int)n;
   p.N = (int)out;

@@ -13,6 +13,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <climits>
 
 namespace ps {
 
@@ -546,6 +547,108 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
   }
 }
 
+// ---------------------------------------------------------------- canonical CSR order
+// The fill claims positions with atomics, so the order of a row's {source row
+// f, weight} pairs -- and with it the fp32 summation order of the transposed
+// aggregation -- would change from run to run.  Both kernels below sort each
+// row's pairs by f (unique within a row: a node's top-T list has distinct
+// entries), so the step is bitwise reproducible.  They run on the frontier's
+// stream right behind the fill, off the step's critical chain.
+//
+// Rows of one chunk (<= kDqChunk pairs): one wave per chunk, a bitonic network
+// over its 16 lanes (shuffles); empty lanes carry INT_MAX keys.
+__global__ __launch_bounds__(256) void csr_sort_chunks_kernel(const int2* __restrict__ chunks,
+                                                              const int* __restrict__ nchunks,
+                                                              int2* __restrict__ occ2) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int nch = *nchunks;
+  for (int64_t ci = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; ci < nch; ci += nw) {
+    const int2 dsc = chunks[ci];
+    const int n = dsc.y & 0xff;
+    if ((dsc.y & kDqSplit) || n < 2) continue;  // (split rows: csr_sort_rows_kernel)
+    int2 v = make_int2(INT_MAX, 0);
+    if (lane < n) v = occ2[ci * kDqChunk + lane];
+#pragma unroll
+    for (int k = 2; k <= kDqChunk; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int ox = __shfl_xor(v.x, j, 64), oy = __shfl_xor(v.y, j, 64);
+        const bool lower = (lane & j) == 0, up = (lane & k) == 0;
+        // ascending block: the lower lane keeps the smaller key
+        const bool take = (lower == up) ? (ox < v.x) : (ox > v.x);
+        if (take) v = make_int2(ox, oy);
+      }
+    if (lane < n) occ2[ci * kDqChunk + lane] = v;
+  }
+}
+
+// Rows split over several chunks (the scan's split list {u, first chunk}):
+// the row's n pairs are contiguous from occ2[cbase * kDqChunk]; one block per
+// row sorts them in LDS up to kSortLds pairs (a bitonic network in its
+// all-ascending form, so the virtual +inf padding past n never moves), in
+// global memory beyond (loads through L2, agent-scope relaxed: correct, slow,
+// only for rows in tens of thousands of neighbour lists).
+constexpr int kSortLds = 20480;  // pairs (160 KiB)
+__device__ __forceinline__ long long pack_pair(int2 v) {
+  return (long long)(((unsigned long long)(unsigned)v.y << 32) | (unsigned)v.x);
+}
+__global__ __launch_bounds__(1024) void csr_sort_rows_kernel(const int2* __restrict__ split,
+                                                             const int* __restrict__ nsplit,
+                                                             const int* __restrict__ off, int2* __restrict__ occ2) {
+  extern __shared__ int2 buf[];
+  const int ns = *nsplit;
+  for (int si = blockIdx.x; si < ns; si += gridDim.x) {
+    const int2 sp = split[si];
+    const int n = off[sp.x + 1] - off[sp.x];
+    int2* row = occ2 + (int64_t)sp.y * kDqChunk;
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    if (n <= kSortLds) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) buf[i] = row[i];
+      __syncthreads();
+      for (int k = 2; k <= p2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = threadIdx.x; i < p2 / 2; i += blockDim.x) {
+            // pair (a, b), a < b: the first stage of a merge compares mirrored
+            // positions, the later ones distance j; min to a
+            const int lo = (i / j) * 2 * j + (i % j);
+            const int a = j == (k >> 1) ? (lo / k) * k + (lo % k) : lo;
+            const int b = j == (k >> 1) ? (a / k) * k + (k - 1 - a % k) : lo + j;
+            if (b < n && buf[b].x < buf[a].x) {
+              const int2 t = buf[a];
+              buf[a] = buf[b];
+              buf[b] = t;
+            }
+          }
+          __syncthreads();
+        }
+      for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = buf[i];
+      __syncthreads();
+    } else {
+      long long* rw = reinterpret_cast<long long*>(row);
+      for (int k = 2; k <= p2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = threadIdx.x; i < p2 / 2; i += blockDim.x) {
+            const int lo = (i / j) * 2 * j + (i % j);
+            const int a = j == (k >> 1) ? (lo / k) * k + (lo % k) : lo;
+            const int b = j == (k >> 1) ? (a / k) * k + (k - 1 - a % k) : lo + j;
+            if (b < n) {
+              const long long va = __hip_atomic_load(rw + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const long long vb = __hip_atomic_load(rw + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if ((int)(unsigned)vb < (int)(unsigned)va) {
+                __hip_atomic_store(rw + a, vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(rw + b, va, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+            }
+          }
+          __threadfence_block();
+          __syncthreads();
+        }
+    }
+  }
+}
+
 // dpq[u] = lrelu'(q[u]) * sum over the occurrences (f, t) of u in the slot
 // table of w[f][t] * dagg[f]   (the transpose of agg, pinsage_model.py:202).
 // One wave per chunk of <= kDqChunk occurrences of ONE row u (chunk list from
@@ -757,6 +860,29 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
   }
 }
 
+// In-place row L2 normalisation of y [n][out] (the W projection's last step,
+// pinsage_model.py:210, for out_dim > 128, where the GEMM's fused L2-norm
+// epilogue does not apply): one wave per row; norms[r] = ||y_r||.
+__global__ __launch_bounds__(256) void l2norm_rows_kernel(float* __restrict__ y, int64_t n, int out,
+                                                          float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wid; r < n; r += nw) {
+    float s2 = 0.f;
+    for (int c = lane; c < out; c += 64) s2 += y[r * out + c] * y[r * out + c];
+    const float nrm = sqrtf(wave_sum(s2));
+    for (int c = lane; c < out; c += 64) y[r * out + c] = y[r * out + c] / nrm;
+    if (lane == 0 && norms) norms[r] = nrm;
+  }
+}
+
+int launch_l2norm_rows(float* y, int64_t n, int out, float* norms, hipStream_t st) {
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(l2norm_rows_kernel, dim3(grid_for(n * 64, 256, 4096)), dim3(256), 0, st, y, n, out, norms);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
 
 // ---------------------------------------------------------------- loss
 // One wave per triple b: rows rq, rp, rn of Z (head outputs of the unique top
@@ -1330,12 +1456,16 @@ int csr_prepare() {
     if (hipFuncSetAttribute((const void*)csr_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kLdsRows * 4) != hipSuccess)
       return (int)kErrHip;
+    if (hipFuncSetAttribute((const void*)csr_sort_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kSortLds * 8) != hipSuccess)
+      return (int)kErrHip;
     return (int)kOk;
   }();
   if (rc != kOk) set_error("csr: cannot raise the dynamic LDS limit");
   return rc;
 }
 
+int64_t dq_chunk_capacity(int64_t S_max, int T, int64_t N_max);
 int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64_t S_max, int T, const int* nN,
                      int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int* cbase, int2* occ2,
                      int2* chunks, int* nchunks, int2* split, int* nsplit, float* dpq, int hid, hipStream_t st) {
@@ -1366,6 +1496,16 @@ int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64
   hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, wloc, nS, T, nN, cursor, off, cbase,
                      occ2, max_ranges);
   PS_CHECK_LAUNCH();
+  // canonical pair order (sorted by source row): bitwise-reproducible sums
+  static const bool canon = !getenv("PINSAGE_CSR_CANON") || atoi(getenv("PINSAGE_CSR_CANON")) != 0;
+  if (canon) {
+    const int64_t max_chunks = dq_chunk_capacity(S_max, T, N_max);
+    hipLaunchKernelGGL(csr_sort_chunks_kernel, dim3(grid_for(max_chunks * 64, 256, 2048)), dim3(256), 0, st,
+                       chunks, nchunks, occ2);
+    PS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(csr_sort_rows_kernel, dim3(256), dim3(1024), kSortLds * 8, st, split, nsplit, off, occ2);
+    PS_CHECK_LAUNCH();
+  }
   return kOk;
 }
 

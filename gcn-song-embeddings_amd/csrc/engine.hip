@@ -18,6 +18,8 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <mutex>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -93,6 +95,7 @@ struct LayerBuf {
   size_t self_src = 0, q_src = 0, loc = 0, wloc = 0;
   size_t q = 0, agg = 0, y = 0, nrm = 0;
   size_t qsplit = 0;  // the Q weight's hi / mid / lo bf16 planes (split-bf16 Q projection)
+  size_t wplanes = 0;  // the W weight's fragment-order bf16 planes (aggw.hip fragment form)
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
          occ2 = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
@@ -211,12 +214,28 @@ struct Engine {
   // the optimizer pass) 0.454-0.467.
   int defer_side = getenv("PINSAGE_DEFER_SIDE") ? atoi(getenv("PINSAGE_DEFER_SIDE")) : 3;
   std::vector<std::function<int()>> pend;  // deferred side launches, in order
-  ~Engine() {
-    for (auto& s : side)
-      if (s) (void)hipStreamDestroy(s);
-    for (auto& e : ev) (void)hipEventDestroy(e);
-  }
+  ~Engine();
 };
+
+// Streams and events of destroyed engines are retired to a process-wide pool
+// and handed to the next engine that needs them, never released: a destroy
+// may run while some stream of the process is being captured into a graph (a
+// Python finaliser inside torch.cuda.graph), and releasing HIP streams /
+// events there invalidates that capture (global capture mode).  An engine
+// destroy therefore makes no HIP call at all.
+static std::mutex g_retired_mu;
+static std::vector<hipStream_t> g_retired_streams;
+static std::vector<hipEvent_t> g_retired_events;
+static std::atomic<int64_t> g_live_engines{0};
+
+Engine::~Engine() {
+  std::lock_guard<std::mutex> lk(g_retired_mu);
+  for (auto& s : side)
+    if (s) g_retired_streams.push_back(s);
+  for (auto& e : ev) g_retired_events.push_back(e);
+  // (timing events are bench-only: pinsage_engine_timing(e, 0) releases them)
+  g_live_engines--;
+}
 
 // An event from the engine's pool (round-robin; a step records well under
 // kEvents, and a wait binds to the record that precedes it on the host).
@@ -224,9 +243,24 @@ constexpr int kEvents = 32;
 static int ensure_streams(Engine& E) {
   if (E.side[0]) return kOk;
   PS_TRY(csr_prepare());
-  for (auto& s : E.side) PS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  std::lock_guard<std::mutex> lk(g_retired_mu);
+  for (auto& s : E.side) {
+    if (!g_retired_streams.empty()) {
+      s = g_retired_streams.back();
+      g_retired_streams.pop_back();
+    } else {
+      PS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+  }
   E.ev.resize(kEvents);
-  for (auto& e : E.ev) PS_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : E.ev) {
+    if (!g_retired_events.empty()) {
+      e = g_retired_events.back();
+      g_retired_events.pop_back();
+    } else {
+      PS_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+  }
   return kOk;
 }
 // `to` waits for everything enqueued so far on `from`
@@ -376,6 +410,7 @@ static void layout(Engine& E) {
     lb.wloc = carve(cur, FS * T * 4);
     lb.q = carve(cur, FN * c.hid * 4);
     lb.qsplit = carve(cur, 3 * c.hid * lb.d * 2);
+    lb.wplanes = carve(cur, agg_wf_planes_bytes(lb.d, c.hid));
     lb.agg = carve(cur, FS * c.hid * 4);
     lb.y = carve(cur, FS * c.out * 4);
     lb.nrm = carve(cur, FS * 4);
@@ -535,6 +570,20 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   const int Lc = (int)c.n_layers, T = (int)c.T;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
+  // W of every layer split once into the aggregation kernel's fragment-order
+  // bf16 planes (the rows form picked by the expected frontier size)
+  std::vector<int> wf_rows((size_t)Lc, 0);
+  if (E.fused_aggw == 1 && !E.fused_next_q) {
+    Timed ts(E, "fwd.wsplit", st);
+    for (int l = 0; l < Lc; ++l) {
+      LayerBuf& lb = E.L[(size_t)l];
+      if (!agg_wf_supported(lb.d, c.hid, c.out, T)) continue;
+      const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
+      wf_rows[(size_t)l] = agg_wf_rows(S_est);
+      PS_TRY(launch_split_wfrag(E.params + lb.pWw, lb.d + c.hid, (int)(lb.d + c.hid), wf_rows[(size_t)l],
+                                at<uint16_t>(ws, lb.wplanes), st));
+    }
+  }
   int q_done = 0;  // this layer's q rows came out of the layer below's kernel (AggNextQ)
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
@@ -579,7 +628,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(dep(E, st, E.fork.stream));
       PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
     }
-    if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {
+    if (E.fused_aggw && (wf_rows[(size_t)l] || agg_w_supported(lb.d, c.hid, c.out, T))) {
       // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
       Timed taw(E, lname("fwd.aggw", l), st);
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
@@ -597,7 +646,8 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(launch_agg_w(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q),
                           (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0,
                           S_est, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
-                          at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st, nx.q ? &nx : nullptr, &q_done));
+                          at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st, nx.q ? &nx : nullptr, &q_done,
+                          wf_rows[(size_t)l] ? at<uint16_t>(ws, lb.wplanes) : nullptr, wf_rows[(size_t)l]));
       continue;
     }
     Timed t_agg(E, lname("fwd.agg", l), st);
@@ -1087,6 +1137,7 @@ int pinsage_engine_create(const pinsage_engine_config* cfg, pinsage_engine** out
     return kErrArg;
   }
   auto* E = new Engine();
+  g_live_engines++;
   E->cfg = EngineConfig{cfg->n_items, cfg->d_in, cfg->hid, cfg->out, cfg->n_layers, cfg->T,
                         cfg->max_pos};
   layout(*E);
@@ -1094,7 +1145,11 @@ int pinsage_engine_create(const pinsage_engine_config* cfg, pinsage_engine** out
   return kOk;
 }
 
+// capture-safe: no HIP call (the engine's streams and events are retired for
+// reuse, see Engine::~Engine)
 void pinsage_engine_destroy(pinsage_engine* e) { delete reinterpret_cast<Engine*>(e); }
+
+int64_t pinsage_engine_live_count(void) { return g_live_engines.load(); }
 
 int64_t pinsage_engine_workspace_bytes(const pinsage_engine* e) {
   return (int64_t) reinterpret_cast<const Engine*>(e)->total;
@@ -1337,6 +1392,21 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
                              at<int>(ws, top.S.count), top.S.cap, at<float>(ws, E->G),
                              at<int>(ws, E->Kc), at<float>(ws, E->dZ), !E->fused_head,
                              (hipStream_t)stream);
+}
+
+int pinsage_engine_reset_backward(pinsage_engine* e, void* ws, void* stream) {
+  if (!e || !ws) {
+    set_error("engine_reset_backward: null argument");
+    return kErrArg;
+  }
+  Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(run_pend(*E));
+  // the dY scatter-add targets of the layers below the top (the forward's
+  // layer_prep zeroed them; a backward accumulates into them)
+  for (size_t l = 0; l + 1 < E->L.size(); ++l)
+    PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E->L[l].dY), 0, (size_t)(E->L[l].S.cap * E->cfg.out) * 4,
+                                (hipStream_t)stream));
+  return kOk;
 }
 
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream) {

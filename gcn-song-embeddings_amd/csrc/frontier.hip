@@ -355,6 +355,34 @@ int launch_mark_table_i64(unsigned long long* bits, const int64_t* ids, int64_t 
   return kOk;
 }
 
+// local_idx[f][t] = rank of nb[nodeset[f]][t] in a finalised set (its
+// position in the sorted members: the word's prefix + popcount below the bit)
+// -- the index tables of relevant_nodes_per_layer_precomp's unique
+// (pinsage_model.py:164-166) as the convolution reads them
+__global__ __launch_bounds__(256) void set_rank_table_kernel(const int64_t* __restrict__ nodeset, int64_t n,
+                                                             const int32_t* __restrict__ nb, int64_t ld, int T,
+                                                             const unsigned long long* __restrict__ bits,
+                                                             const uint32_t* __restrict__ prefix,
+                                                             int32_t* __restrict__ out) {
+  const int64_t total = n * T;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = i / T, t = i - f * T;
+    const int64_t id = nb[nodeset[f] * ld + t];
+    const unsigned long long wd = bits[id >> 6];
+    out[i] = (int32_t)(prefix[id >> 6] + (uint32_t)__popcll(wd & ((1ull << (id & 63)) - 1ull)));
+  }
+}
+
+int launch_set_rank_table(const int64_t* nodeset, int64_t n, const int32_t* nb, int64_t ld, int T,
+                          const unsigned long long* bits, const uint32_t* prefix, int32_t* out, hipStream_t st) {
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(set_rank_table_kernel, dim3(grid_for(n * T, 256)), dim3(256), 0, st, nodeset, n, nb, ld, T,
+                     bits, prefix, out);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 // Finalise a set: dst = a | b, prefix, sorted members, device count.
 int launch_set_finalize(unsigned long long* dst, const unsigned long long* a,
                         const unsigned long long* b, int64_t universe, uint32_t* block_sums,

@@ -167,20 +167,37 @@ std::tuple<at::Tensor, at::Tensor> ppr_topk(const at::Tensor& indptr, const at::
   return {w, nb};
 }
 
-// sorted unique(cat(nb[nodeset, :T].flatten(), nodeset)) as int64
-at::Tensor frontier(const at::Tensor& nodeset, const at::Tensor& nb_table, int64_t T, int64_t n_items) {
+// One step of relevant_nodes_per_layer_precomp (pinsage_model.py:162-166):
+// (uniq, local_idx) with uniq = sorted unique(cat(nb[nodeset, :T].flatten(),
+// nodeset)) int64 and local_idx int32 [n, T], uniq[local_idx[f][t]] ==
+// nb[nodeset[f]][t] (weighted_agg's slot rows).  nb_table int64 (the
+// reference's table, precompute_neighborhoods_topt) or int32 [n_items][>= T];
+// n_items -1 = nb_table's rows.
+std::tuple<at::Tensor, at::Tensor> frontier(const at::Tensor& nodeset, const at::Tensor& nb_table, int64_t T,
+                                            int64_t n_items) {
   need(nodeset, at::kLong, "nodeset");
-  need(nb_table, at::kInt, "nb_table");
+  TORCH_CHECK(nb_table.is_cuda() && nb_table.dim() == 2 &&
+                  (nb_table.scalar_type() == at::kLong || nb_table.scalar_type() == at::kInt),
+              "nb_table: int64 or int32 device [n_items, >= T]");
+  TORCH_CHECK(T >= 1 && T <= nb_table.size(1), "T must be in [1, nb_table columns]");
   c10::hip::HIPGuard guard(nodeset.device().index());
+  if (n_items < 0) n_items = nb_table.size(0);
+  TORCH_CHECK(n_items >= 1 && n_items <= nb_table.size(0), "n_items must be in [1, nb_table rows]");
+  // (the kernels read 32-bit node ids; an int64 table narrows once, on the device)
+  const at::Tensor nb32 = nb_table.scalar_type() == at::kInt ? nb_table.contiguous()
+                                                              : nb_table.narrow(1, 0, T).to(at::kInt).contiguous();
   const int64_t n = nodeset.numel();
   auto ws = at::empty({pinsage_frontier_workspace(n_items)}, nodeset.options().dtype(at::kByte));
   auto out = at::empty({std::max<int64_t>(1, std::min(n_items, n * (T + 1)))}, nodeset.options().dtype(at::kInt));
   auto cnt = at::zeros({1}, nodeset.options().dtype(at::kInt));
-  check(pinsage_frontier_step(nodeset.data_ptr<int64_t>(), n, nb_table.data_ptr<int32_t>(), nb_table.size(1), T,
-                              n_items, ws.data_ptr(), out.data_ptr<int32_t>(), cnt.data_ptr<int32_t>(),
-                              stream_of(nodeset)),
+  auto local_idx = at::empty({n, T}, nodeset.options().dtype(at::kInt));
+  check(pinsage_frontier_step(nodeset.data_ptr<int64_t>(), n, nb32.data_ptr<int32_t>(), nb32.size(1), T, n_items,
+                              ws.data_ptr(), out.data_ptr<int32_t>(), cnt.data_ptr<int32_t>(), stream_of(nodeset)),
         "frontier");
-  return out.narrow(0, 0, cnt.item<int32_t>()).to(at::kLong);
+  check(pinsage_frontier_local_idx(nodeset.data_ptr<int64_t>(), n, nb32.data_ptr<int32_t>(), nb32.size(1), T,
+                                   n_items, ws.data_ptr(), local_idx.data_ptr<int32_t>(), stream_of(nodeset)),
+        "frontier");
+  return {out.narrow(0, 0, cnt.item<int32_t>()).to(at::kLong), local_idx};
 }
 
 // y = x[rows] W^T (+ b) (LeakyReLU 0.01 if lrelu); rows int32 or none
@@ -393,11 +410,13 @@ at::Tensor norm_lrelu_backward(const at::Tensor& dy, const at::Tensor& y, const 
 }  // namespace
 
 TORCH_LIBRARY(pinsage, m) {
+  // rng_mode defaults to the reference's own stream (do_random_walks draws
+  // from torch's global MT19937 generator, pinsage_model.py:32-53)
   m.def("walk(Tensor indptr, Tensor indices, Tensor sources, int n_hops, float alpha, int seed=0, int offset=0, "
-        "str rng_mode='philox', int src_base=0) -> Tensor");
+        "str rng_mode='mt19937', int src_base=0) -> Tensor");
   m.def("ppr_topk(Tensor indptr, Tensor indices, Tensor sources, int n_hops, float alpha, int k, int seed=0, "
-        "int src_base=0, int offset=0, str rng_mode='philox') -> (Tensor, Tensor)");
-  m.def("frontier(Tensor nodeset, Tensor nb_table, int T, int n_items) -> Tensor");
+        "int src_base=0, int offset=0, str rng_mode='mt19937') -> (Tensor, Tensor)");
+  m.def("frontier(Tensor nodeset, Tensor nb_table, int T, int n_items=-1) -> (Tensor, Tensor)");
   m.def("linear(Tensor x, Tensor? rows, Tensor W, Tensor? b, bool lrelu) -> Tensor");
   m.def("gemm(Tensor A, bool a_kmajor, Tensor? a_idx, Tensor B, bool b_kmajor, Tensor? b_idx, int M, int N, "
         "int K) -> Tensor");

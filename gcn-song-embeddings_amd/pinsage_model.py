@@ -21,6 +21,7 @@ from __future__ import annotations
 import ctypes
 import os
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -697,20 +698,10 @@ def _param_order(module_like_n_layers):
     return names + ["G1.weight", "G1.bias", "G2.weight"]
 
 
-_DEFERRED_DESTROY = []
-
-
-def _destroy_deferred():
-    while _DEFERRED_DESTROY:
-        nat.lib().pinsage_engine_destroy(_DEFERRED_DESTROY.pop())
-
-
 class _Engine:
     """Owns a native engine handle for one configuration."""
 
     def __init__(self, n_items, d_in, hid, out, n_layers, T, max_pos):
-        if not torch.cuda.is_current_stream_capturing():
-            _destroy_deferred()
         self.cfg = nat.EngineConfig(n_items, d_in, hid, out, n_layers, T, max_pos)
         h = ctypes.c_void_p()
         nat.check(nat.lib().pinsage_engine_create(ctypes.byref(self.cfg), ctypes.byref(h)),
@@ -722,15 +713,13 @@ class _Engine:
         nat.lib().pinsage_engine_offsets(h, ctypes.byref(self.off))
 
     def __del__(self):
-        # an engine finalised while a stream is capturing is destroyed later
-        # (its streams / events must not be released inside a capture)
+        # capture-safe at the C-ABI (pinsage_engine_destroy makes no HIP call:
+        # the engine's streams / events are retired for reuse), so a finaliser
+        # the garbage collector runs inside a graph capture is harmless
         try:
             if getattr(self, "h", None):
-                if torch.cuda.is_current_stream_capturing():
-                    _DEFERRED_DESTROY.append(self.h)
-                else:
-                    _destroy_deferred()
-                    nat.lib().pinsage_engine_destroy(self.h)
+                nat.lib().pinsage_engine_destroy(self.h)
+                self.h = None
         except Exception:
             pass
 
@@ -742,8 +731,9 @@ class _Engine:
         return pool.pop() if pool else self.new_workspace(dev)
 
     def release_workspace(self, ws):
-        """Back to the pool after its backward was enqueued (stream order keeps
-        the next call's kernels behind it); at most 4 kept."""
+        """Back to the pool once the autograd node that used it is freed
+        (stream order keeps the next call's kernels behind its backward); at
+        most 4 kept."""
         pool = self.__dict__.setdefault("_pool", [])
         if len(pool) < 4:
             pool.append(ws)
@@ -1109,6 +1099,11 @@ class _EngineFn(torch.autograd.Function):
         runner.last_ws = ws  # (bench.py reads frontier sizes from it: the last call to use it)
         ctx.tabs = tabs  # the frontier's tables stay alive with the workspace
         ctx.engine = e
+        ctx.n_bwd = 0
+        # the workspace holds this graph's activations: it goes back to the
+        # pool when the autograd node is freed (after the last backward a
+        # retained graph may still run), never earlier
+        weakref.finalize(ctx, e.release_workspace, ws)
         return out
 
     @staticmethod
@@ -1117,11 +1112,13 @@ class _EngineFn(torch.autograd.Function):
         grads = torch.zeros(e.n_params, dtype=torch.float32, device=runner.dev)
         runner.bind(ctx.feats, ctx.table, grads=grads, tabs=ctx.tabs)
         dout = dout.contiguous().to(torch.float32)
+        if ctx.n_bwd:  # a retained graph's next backward: re-zero what the last one accumulated into
+            nat.check(nat.lib().pinsage_engine_reset_backward(e.h, nat.ptr(ws), nat.stream_ptr()),
+                      "reset_backward")
         nat.check(nat.lib().pinsage_engine_set_output_grad(e.h, nat.ptr(ws), nat.ptr(dout), ctx.n,
                                                            nat.stream_ptr()), "set_output_grad")
         nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(ws), nat.stream_ptr()), "backward")
-        e.release_workspace(ws)
-        ctx.ws = None
+        ctx.n_bwd += 1
         out = []
         off = 0
         for p in runner.params():

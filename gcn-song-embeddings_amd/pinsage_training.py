@@ -501,18 +501,29 @@ class _FusedStep:
 
     # per-site candidates: (cfg, stream_k, splits); a GEMM site takes a block-tile
     # config with or without stream-K, a weight-gradient site a config and a split-K count
-    _GEMM_OPTS = [(c, k, 0) for c in (0, 1, 2, 3) for k in (0, 1) if not (c == 0 and k == 1)]
-    _WGRAD_OPTS = [(c, -1, sp) for c in (0, 1, 2) for sp in (2, 4, 8, 16, 32, 64)]
+    # Candidates keep every site's fp32 summation order (the default tuner is
+    # reproducible run to run): the block tile alone never changes an output
+    # element's k order; stream-K (cut k ranges) and split-K counts do, so
+    # stream-K stays off under the tuner and split counts stay the size model's
+    # (splits 0).  PINSAGE_AUTOTUNE=wide also tries those (timing-picked, so
+    # two runs may then differ at rounding level).
+    _GEMM_OPTS = [(c, 0, 0) for c in (0, 1, 2, 3)]
+    _WGRAD_OPTS = [(c, -1, 0) for c in (0, 1, 2)]
+    _GEMM_OPTS_WIDE = [(c, k, 0) for c in (0, 1, 2, 3) for k in (0, 1) if not (c == 0 and k == 1)]
+    _WGRAD_OPTS_WIDE = [(c, -1, sp) for c in (0, 1, 2) for sp in (2, 4, 8, 16, 32, 64)]
 
     def _gemm_sites(self):
+        wide = os.environ.get("PINSAGE_AUTOTUNE", "1") == "wide"
+        G = self._GEMM_OPTS_WIDE if wide else self._GEMM_OPTS
+        Wg = self._WGRAD_OPTS_WIDE if wide else self._WGRAD_OPTS
         sites = []
         for l in range(self.runner.model.n_layers):
-            sites += [(f"fwd.q_gemm.l{l}", self._GEMM_OPTS), (f"fwd.w_gemm.l{l}", self._GEMM_OPTS),
-                      (f"bwd.dcat.l{l}", self._GEMM_OPTS), (f"bwd.w_wgrad.l{l}", self._WGRAD_OPTS),
-                      (f"bwd.q_wgrad.l{l}", self._WGRAD_OPTS)]
+            sites += [(f"fwd.q_gemm.l{l}", G), (f"fwd.w_gemm.l{l}", G),
+                      (f"bwd.dcat.l{l}", G), (f"bwd.w_wgrad.l{l}", Wg),
+                      (f"bwd.q_wgrad.l{l}", Wg)]
             if l > 0:
-                sites.append((f"bwd.dh.l{l}", self._GEMM_OPTS))
-        return sites + [("bwd.wgrad.g1", self._WGRAD_OPTS), ("bwd.wgrad.g2", self._WGRAD_OPTS)]
+                sites.append((f"bwd.dh.l{l}", G))
+        return sites + [("bwd.wgrad.g1", Wg), ("bwd.wgrad.g2", Wg)]
 
     def _autotune(self, B, p, reps=3):
         """In-context GEMM tuner: the size model picks tile configs from frontier
@@ -527,13 +538,15 @@ class _FusedStep:
         the step's): this step's frontier, layers, loss and backward WITHOUT
         the optimizer -- parameters and Adam state are untouched.
 
-        Reproducibility: every choice computes the same products, but split-K
-        counts and stream-K change the fp32 summation order of a weight
-        gradient, and which candidate wins depends on timing noise -- two runs
-        can therefore differ at fp32 rounding level.  The choices are recorded
-        (``tuned_choices``; bench.py prints them as "gemm_choices"), and
-        PINSAGE_GEMM_CHOICES=<that json> replays them; PINSAGE_AUTOTUNE=0
-        keeps the deterministic size model instead of tuning."""
+        Reproducibility: the candidates (_GEMM_OPTS / _WGRAD_OPTS) differ only
+        in the block tile, which never changes an output element's summation
+        order, so whichever wins, the step computes bitwise the same values
+        (tests/test_gpu_parity.py::test_default_step_is_bitwise_reproducible).
+        PINSAGE_AUTOTUNE=wide also tries stream-K and split-K counts, which
+        change the order (two runs may then differ at rounding level).  The
+        choices are recorded (``tuned_choices``; bench.py prints them as
+        "gemm_choices"), PINSAGE_GEMM_CHOICES=<that json> replays them, and
+        PINSAGE_AUTOTUNE=0 keeps the size model."""
         e = self.runner.engine
         L = nat.lib()
         sites = self._gemm_sites()
@@ -603,9 +616,11 @@ class _FusedStep:
         the step graph (stage coefficients, layers ... Adam, publish), and the
         step graph whose branch stages the predicted next ids into workspace
         1-p and computes their frontier there.  The cyclic garbage collector is
-        off while capturing: an unreachable engine it finalised mid-capture
-        would release HIP streams / events inside the capture (the process
-        aborted in test_engine_variants_train_alike)."""
+        off while capturing (an engine finalised mid-capture once released HIP
+        streams / events inside the capture and aborted the process; the C-ABI
+        destroy is now capture-safe by itself, tests/test_gpu_trainer.py::
+        test_engine_finalised_inside_a_capture, and this keeps unrelated
+        finalisers out of the capture too)."""
         was = gc.isenabled()
         gc.collect()
         gc.disable()

@@ -165,6 +165,12 @@ int64_t pinsage_frontier_workspace(int64_t n_items);
 int pinsage_frontier_step(const int64_t* nodeset, int64_t n, const int32_t* nb_table, int64_t ld,
                           int64_t T, int64_t n_items, void* ws, int32_t* nodes_out,
                           int32_t* count_out, void* stream);
+/* After pinsage_frontier_step on ws (same nodeset, table, T, n_items): the
+ * index table local_idx int32 [n][T] with nodes_out[local_idx[f][t]] ==
+ * nb[nodeset[f]][t] -- the rows of the unique set the convolution's slots
+ * read (weighted_agg's loc), from the set's bitmap ranks. */
+int pinsage_frontier_local_idx(const int64_t* nodeset, int64_t n, const int32_t* nb_table, int64_t ld, int64_t T,
+                               int64_t n_items, const void* ws, int32_t* local_idx, void* stream);
 
 /* ------------------------------------------------------------------ kernels exposed for tests
  * fp32 MFMA GEMM: C[M][N] = A[M][K] * W[N][K]^T (+bias) (leaky_relu if act),
@@ -219,11 +225,13 @@ int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const 
  *   agg[f]  = sum_t w[f][t] * q[loc[f][t]]                     (:202, w normalised)
  *   y[f]    = normalize(lrelu([h[self_src[f]] || agg[f]] W^T + bias))   (:208-210)
  *   norms[f] = ||lrelu(.)||_2 (nullable)
- * in one launch (the engine's kernel): the aggregate staged in LDS and written
- * out once, the projection on split-bf16 MFMA.  h f32 [.][ldh], q f32
- * [q_rows][hid], loc int32 / w f32 [n_rows][T], W f32 [out][d+hid], y f32
- * [n_rows][out], agg f32 [n_rows][hid].  out == 128, d + hid a multiple of 64,
- * d and hid multiples of 4, 1 <= T <= 64.  W_planes is unused (may be null). */
+ * the engine's kernel: the aggregate formed in registers and written out once,
+ * the projection on split-bf16 MFMA.  h f32 [.][ldh], q f32 [q_rows][hid],
+ * loc int32 / w f32 [n_rows][T], W f32 [out][d+hid], y f32 [n_rows][out],
+ * agg f32 [n_rows][hid].  out == 128, 1 <= T <= 64.  W_planes (device
+ * scratch of 3 * out * (d + hid) uint16): W is split into it (fragment-order
+ * bf16 planes) and the fragment form runs -- d and hid multiples of 32; null
+ * runs the LDS-tile form -- d + hid a multiple of 64, d and hid multiples of 4. */
 int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32_t* self_src,
                              const float* q, int64_t hid, int64_t q_rows, const int32_t* loc,
                              const float* w, int64_t n_rows, int64_t T, const float* W,
@@ -241,7 +249,9 @@ int pinsage_gather_rows(const float* h, int64_t ldh, int64_t n_h, int64_t d, con
  *   y[f] = normalize(lrelu([h[self_idx[f]][0..d) || agg[f]] W^T + bias)),
  *   norms[f] = ||lrelu(.)||_2
  * with the concat read in place (no concat buffer).  self_idx int32 nullable
- * (rows 0..n-1), W f32 [out][d+hid], 0 < out <= 128, d and hid multiples of 4. */
+ * (rows 0..n-1), W f32 [out][d+hid], d and hid multiples of 4.  out <= 128:
+ * one launch (the GEMM's L2-norm epilogue); wider: the GEMM with bias +
+ * LeakyReLU, then an in-place row normalisation. */
 int pinsage_concat_linear_l2norm(const float* h, int64_t ldh, const int32_t* self_idx, int64_t n, int64_t d,
                                  const float* agg, int64_t ld_agg, int64_t hid, const float* W,
                                  const float* bias, int64_t out, float* y, float* norms, void* stream);
@@ -323,7 +333,12 @@ typedef struct {
 } pinsage_engine_offsets_t;
 
 int pinsage_engine_create(const pinsage_engine_config* cfg, pinsage_engine** out);
+/* Makes no HIP call (safe inside a stream capture, e.g. a finaliser run by the
+ * garbage collector while torch.cuda.graph captures): the engine's streams and
+ * events are retired to a process-wide pool that later engines reuse. */
 void pinsage_engine_destroy(pinsage_engine* e);
+/* engines created and not yet destroyed (diagnostics / tests) */
+int64_t pinsage_engine_live_count(void);
 int64_t pinsage_engine_workspace_bytes(const pinsage_engine* e);
 int64_t pinsage_engine_num_params(const pinsage_engine* e);
 /* byte offsets of engine outputs inside a workspace (ids int64, pos_rank int32,
@@ -383,6 +398,11 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
                                    void* stream);
 /* all parameter gradients from dZ into the grad buffer (overwritten) */
 int pinsage_engine_backward(pinsage_engine* e, void* ws, void* stream);
+/* Re-arm a workspace whose backward has run for another backward of the same
+ * forward (autograd's retain_graph=True: backward(retain_graph=True) then
+ * backward again): zeroes the scatter-add targets the backward accumulates
+ * into.  The forward's activations and plan are left as they are. */
+int pinsage_engine_reset_backward(pinsage_engine* e, void* ws, void* stream);
 /* the same backward in two calls, for data-parallel steps that all-reduce the
  * first call's gradients while the second runs (pinsage_training.py:188-191
  * under DP): stage 0 = the head and layers L-1 .. 1 (every gradient but layer

@@ -63,14 +63,20 @@ CASES = [  # n_rows, d, ldh, hid, T, U (q rows), n_h (h rows)
     (777, 256, 256, 512, 25, 3000, 4000),       # C3 fanout, d 256
     (300, 256, 256, 512, 50, 2000, 1000),       # C5 fanout
     (250, 64, 64, 128, 64, 500, 600),           # max fanout, small dims (uneven k-steps)
+    (70, 32, 32, 96, 7, 90, 80),                # K = 128: fewer units than waves
 ]
 
 
-@pytest.fixture(params=["0", "1000000000"])
+@pytest.fixture(params=["wf32", "wf16", "lds32", "lds16"])
 def form(request, monkeypatch):
-    """the kernel form behind pinsage_conv_agg_project: the 32-row form (one
-    block per CU) from PINSAGE_AGGW32_MIN_ROWS rows on, else the 16-row form"""
-    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", request.param)
+    """the kernel form behind pinsage_conv_agg_project: the fragment form
+    (agg_wf_kernel, W split into fragment-order planes; the default) or the
+    LDS-tile forms (PINSAGE_AGGW_FORM=0), each with 32- or 16-row tiles"""
+    kind, rows = request.param[:-2], request.param[-2:]
+    monkeypatch.setenv("PINSAGE_AGGW_FORM", "1" if kind == "wf" else "0")
+    big = "0" if rows == "32" else "1000000000"
+    monkeypatch.setenv("PINSAGE_AGGWF32_MIN_ROWS", big)
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", big)
     return request.param
 
 

@@ -549,7 +549,11 @@ def test_fused_ppr_topk_matches_walk_plus_topk(mode, k):
         assert (w[:48].cpu().numpy() == rw).all() and (nb[:48].cpu().numpy() == rn).all()
 
 
-@pytest.mark.parametrize("dims,T,n", [((24, 16, 32), 4, 300), ((128, 128, 512), 10, 700), ((256, 128, 512), 50, 200)])
+@pytest.mark.parametrize("dims,T,n", [((24, 16, 32), 4, 300), ((128, 128, 512), 10, 700), ((256, 128, 512), 50, 200),
+                                      # out_dim wider than the fused L2-norm epilogue: grid_search.py:130 and
+                                      # dashboard.py:137 (out 256, hidden 1024), pinsage_model.py:285 (hidden
+                                      # 1024, out 512)
+                                      ((128, 256, 1024), 10, 300), ((96, 512, 1024), 3, 50)])
 def test_conv_layer_autograd_vs_oracle(dims, T, n):
     """Standalone ConvLayer (pinsage_model.py:171-212) trained through autograd:
     output, every parameter gradient and the gradient of h (a wider h than

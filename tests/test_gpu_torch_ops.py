@@ -28,7 +28,7 @@ def test_ppr_topk_op_matches_sampler():
     seed = 0x1234_5678_9abc
     w_ref, nb_ref, _, _ = pm._ppr_topk_device(g, src, 300, 0.85, 25, philox=(seed, 0))
     ip, ix = (torch.from_numpy(a).cuda() for a in (indptr, indices))
-    w, nb = torch.ops.pinsage.ppr_topk(ip, ix, src, 300, 0.85, 25, seed, 0)
+    w, nb = torch.ops.pinsage.ppr_topk(ip, ix, src, 300, 0.85, 25, seed, 0, rng_mode="philox")
     assert torch.equal(nb, nb_ref) and torch.equal(w, w_ref)
 
 
@@ -42,8 +42,18 @@ def test_frontier_op_matches_precomp_frontier():
     w = torch.from_numpy(rng.random((n, 100)))
     nodes = torch.from_numpy(rng.integers(0, n, 300))
     S = pm.relevant_nodes_per_layer_precomp(nodes, 2, T, (w, nb))
-    out = torch.ops.pinsage.frontier(nodes.cuda(), nb[:, :T].to(torch.int32).contiguous().cuda(), T, n)
-    assert torch.equal(out.cpu(), S[0][0].to(torch.int64))
+    # the reference's int64 table (its frontier step, pinsage_model.py:162-166) and an int32 one
+    for tab in (nb.cuda(), nb[:, :T].to(torch.int32).contiguous().cuda()):
+        for ns, nxt in ((nodes, S[0][0]), (S[0][0].to(torch.int64), None)):
+            uniq, local_idx = torch.ops.pinsage.frontier(ns.cuda(), tab, T)
+            ref = torch.cat([nb[ns, :T].flatten(), ns]).unique()
+            if nxt is not None:
+                assert torch.equal(ref, nxt.to(torch.int64))
+            assert torch.equal(uniq.cpu(), ref)
+            assert local_idx.dtype == torch.int32 and local_idx.shape == (len(ns), T)
+            assert torch.equal(uniq.cpu()[local_idx.cpu().long()], nb[ns, :T])
+    with pytest.raises(RuntimeError, match="T must be"):
+        torch.ops.pinsage.frontier(nodes.cuda(), nb.cuda(), 101)
 
 
 def test_linear_and_agg_ops_with_autograd():
@@ -122,6 +132,15 @@ def test_walk_and_ppr_topk_ops_mt19937_match_reference_fixtures():
             w, nb = ops.ppr_topk(ip, ix, ns, int(d["n_hops"]), 0.85, int(k), rng_mode="mt19937")
             assert (w.cpu().numpy() == d[f"val_{k}"]).all(), (gname, k)
             assert (nb.cpu().numpy() == d[f"idx_{k}"]).all(), (gname, k)
+        # the default rng_mode is the reference's stream
+        torch.manual_seed(int(d["seed"]))
+        w, nb = ops.ppr_topk(ip, ix, ns, int(d["n_hops"]), 0.85, int(d["ks"][0]))
+        assert (nb.cpu().numpy() == d[f"idx_{d['ks'][0]}"]).all()
+    d = golden("walk_small")
+    torch.manual_seed(int(d["seed"]))
+    tr = ops.walk(torch.from_numpy(d["indptr"]).cuda(), torch.from_numpy(d["indices"]).cuda(),
+                  torch.from_numpy(d["nodeset"]).cuda(), 500, 0.85)
+    assert (tr.cpu().numpy() == d["trace"]).all()
     with pytest.raises(RuntimeError, match="rng_mode"):
         ops.walk(ip, ix, ns, 5, 0.85, rng_mode="pcg")
 

@@ -180,3 +180,100 @@ def test_fused_step_is_an_optimizer_step_for_hooks_and_scheduler():
             assert events == ["pre", "post"] * tr.b_per_e
         finally:
             os.chdir(cwd)
+
+
+def test_retained_graph_backward_twice_and_interleaved_forward():
+    """PinSageModel's autograd node keeps its engine
+    workspace until the node is freed, and a retained graph's second backward
+    re-arms it (pinsage_engine_reset_backward), so backward(retain_graph=True)
+    followed by backward -- with another forward + backward in between that
+    must not take the retained workspace -- gives the first gradients again
+    (bitwise: same kernels, same inputs)."""
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            m = tr.model
+            params = list(m.parameters())
+            ids = torch.tensor([3, 77, 3, 1500, 2999, 12, 640, 77])
+            cot = torch.randn(len(ids), 128, generator=torch.Generator().manual_seed(5))
+            out = m(tr.features, ids)
+            loss = (out * cot).sum()
+            g1 = torch.autograd.grad(loss, params, retain_graph=True)
+            # another forward / backward in between (the pool must not hand it this graph's workspace)
+            out2 = m(tr.features, torch.tensor([9, 10, 11, 2000]))
+            out2.sum().backward()
+            for p in params:
+                p.grad = None
+            loss.backward()
+            for a, p in zip(g1, params):
+                assert torch.equal(a, p.grad), "second backward of a retained graph differs"
+            # and the retained graph's node frees its workspace back to the pool
+            eng = m.runner().engine
+            del out, loss, out2
+            import gc
+            gc.collect()
+            assert len(eng.__dict__.get("_pool", [])) >= 1
+        finally:
+            os.chdir(cwd)
+
+
+def test_engine_finalised_inside_a_capture():
+    """an engine the cyclic garbage collector finalises while a
+    stream is being captured (torch.cuda.graph, global capture mode) must
+    neither invalidate the capture nor abort: pinsage_engine_destroy makes no
+    HIP call (its streams / events are retired for reuse).  The engine here has
+    created its side streams (one forward + backward) and sits in a reference
+    cycle; gc.collect() runs inside the capture; the graph then replays and the
+    engine is gone."""
+    import gc
+    import _native as nat
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            out = tr.model(tr.features, torch.tensor([1, 2, 3, 40]))
+            out.sum().backward()  # the engine's side streams and events exist now
+            torch.cuda.synchronize()
+            x = torch.randn(1 << 16, device="cuda")
+            graph = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            gc.disable()  # (no automatic collection before the capture's own)
+            try:
+                runner = tr.model.runner()
+                cyc = [runner.engine]
+                cyc.append(cyc)  # only the cyclic collector can free it
+                runner.engine = None
+                tr.model._runner = None
+                del tr, out, runner, cyc
+                live = nat.lib().pinsage_engine_live_count()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(graph, stream=s):
+                        y = x * 2.0 + 1.0
+                        gc.collect()  # finalises the unreachable engine mid-capture
+                        z = y.sum()
+            finally:
+                gc.enable()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert abs(float(z) - float((x * 2.0 + 1.0).sum())) <= 1e-3 * abs(float(z)) + 1e-3
+            assert nat.lib().pinsage_engine_live_count() < live
+            # a new engine reuses the retired streams and trains normally
+            torch.manual_seed(1)
+            tr2 = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            tr2.batch_size = 32
+            torch.manual_seed(2)
+            batch, _ = tr2.next_batch()
+            loss, _, _ = tr2.train_batch(batch)
+            assert np.isfinite(float(loss))
+        finally:
+            os.chdir(cwd)
