@@ -212,10 +212,11 @@ def host_cores():
     return threads, facts
 
 
-def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
+def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=45.0, steps=20, warmup=3):
     """The oracle's restatement of the reference train step (dense clone
     put_embeddings, f64 aggregation, torch CPU) on the same workload, on all the
-    physical cores this job may use."""
+    physical cores this job may use: `warmup` untimed steps,
+    then the median of `steps` timed ones (fewer only if `seconds` runs out)."""
     from oracle import oracle as orc
     import pinsage_model as pm
     threads, facts = host_cores()
@@ -239,22 +240,31 @@ def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=20.0, max_steps=20):
     tr = orc.RefTrainer(tmp, feats, nbhds[0].numpy(), nbhds[1].numpy(), n_layers=cfg["n_layers"],
                         T=cfg["T"])
     mt = orc.MT(2)
+    for _ in range(warmup):
+        b, _ = orc.sample_batch_easy(mt, pos.numpy(), cfg["n_tracks"], cfg["batch"])
+        tr.step(b)
     times = []
     t_start = time.time()
-    while len(times) < max_steps and (time.time() - t_start) < seconds:
+    while len(times) < steps and (time.time() - t_start) < seconds:
         t0 = time.time()
         b, _ = orc.sample_batch_easy(mt, pos.numpy(), cfg["n_tracks"], cfg["batch"])
         tr.step(b)
         times.append(time.time() - t0)
-    t_step = float(np.median(times[1:] if len(times) > 2 else times))
+    t_step = float(np.median(times))
     torch.set_flush_denormal(False)
     ratio = None
     rp = os.path.join(REPO, "profiles", "r02", "refcpu_ratio.json")
     if os.path.isfile(rp):
         ratio = json.load(open(rp)).get("refcpu_over_reference")
     return dict(value=3 * cfg["batch"] / t_step, unit="target nodes/s", cores=threads, kind="port",
-                sample=f"{len(times)} train steps (median) of the oracle's reference restatement "
-                       f"(torch CPU, {threads} threads) on the same synthetic graph and config",
+                sample=f"median of {len(times)} timed train steps after {warmup} untimed ones, of the "
+                       f"oracle's reference restatement (torch CPU, {threads} threads) on the same synthetic "
+                       f"graph and config",
+                flush_denormal=True,
+                flush_denormal_note="torch.set_flush_denormal(True) while timing: the restatement's backward "
+                                    "at the reference init produces denormals the reference's op order does "
+                                    "not (1.6 -> 8 s per step without the flush); refcpu_over_reference was "
+                                    "measured with the same setting",
                 ms_per_step=t_step * 1e3, host=facts, refcpu_over_reference=ratio,
                 refcpu_over_reference_source="profiles/r02/refcpu_ratio.json (dev container, 8 threads)")
 

@@ -93,6 +93,11 @@ _SIGS = {
     "pinsage_step_stage": (ctypes.c_int, [vp, i64, i64, vp, i64, i64, vp, i64, vp, vp]),
     "pinsage_step_publish": (ctypes.c_int, [vp, i64, vp, i64, vp, vp]),
     "pinsage_stream_hold": (ctypes.c_int, [i64, vp]),
+    "pinsage_stepper_create": (ctypes.c_int, [vp, i64, i64, i64, i64, i64, i64, i64, vp]),
+    "pinsage_stepper_destroy": (None, [vp]),
+    "pinsage_stepper_set_graphs": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp]),
+    "pinsage_stepper_sync_state": (ctypes.c_int, [vp, ctypes.c_int, i64]),
+    "pinsage_stepper_step": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),
     "pinsage_segment_wmean": (ctypes.c_int, [vp, i64, i64, i64, vp, vp, vp, i64, ctypes.c_int, vp, i64,
                                              vp]),
     "pinsage_knn_scratch_bytes": (i64, [i64, i64]),

@@ -884,6 +884,135 @@ int launch_l2norm_rows(float* y, int64_t n, int out, float* norms, hipStream_t s
   return kOk;
 }
 
+// ---------------------------------------------------------------- positions by rank
+// The batch positions grouped by their top-set rank, in position order: after
+// a sort of (rank, position) keys, pos_sorted[rank_off[r] .. rank_off[r + 1])
+// are the positions p with pos_rank[p] == r, increasing.  The loss (and the
+// autograd path's output gradient) sum a repeated node's per-position
+// gradients in that order (deterministic; see det_accum below).  One block,
+// keys in LDS (a bitonic network in its all-ascending form: the virtual +inf
+// padding past n never moves); more than kPosCsrMax positions marks the CSR
+// absent (rank_off[0] = -1) and the writers fall back to float atomics.
+constexpr int kPosCsrMax = 20480;  // (160 KiB of 8-byte keys)
+__global__ __launch_bounds__(1024) void pos_csr_kernel(const int32_t* __restrict__ pos_rank, int n,
+                                                       int* __restrict__ rank_off, int32_t* __restrict__ pos_sorted) {
+  extern __shared__ unsigned long long key[];
+  if (n > kPosCsrMax) {
+    if (threadIdx.x == 0) rank_off[0] = -1;
+    return;
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    key[i] = ((unsigned long long)(unsigned)pos_rank[i] << 32) | (unsigned)i;
+  __syncthreads();
+  int p2 = 1;
+  while (p2 < n) p2 <<= 1;
+  for (int k = 2; k <= p2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < p2 / 2; i += blockDim.x) {
+        const int lo = (i / j) * 2 * j + (i % j);
+        const int a = lo;
+        const int b = j == (k >> 1) ? (a / k) * k + (k - 1 - a % k) : lo + j;
+        if (b < n && key[b] < key[a]) {
+          const unsigned long long t = key[a];
+          key[a] = key[b];
+          key[b] = t;
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const unsigned long long v = key[i];
+    const int r = (int)(v >> 32);
+    pos_sorted[i] = (int32_t)(unsigned)v;
+    if (i == 0 || (int)(key[i - 1] >> 32) != r) rank_off[r] = i;
+    if (i == n - 1) rank_off[r + 1] = n;
+  }
+}
+
+int launch_pos_csr(const int32_t* pos_rank, int64_t n, int* rank_off, int32_t* pos_sorted, hipStream_t st) {
+  static bool prepared = false;
+  if (!prepared) {
+    PS_CHECK_HIP(hipFuncSetAttribute((const void*)pos_csr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kPosCsrMax * 8));
+    prepared = true;
+  }
+  if (n <= 0) return kOk;
+  hipLaunchKernelGGL(pos_csr_kernel, dim3(1), dim3(1024), n <= kPosCsrMax ? (unsigned)(n * 8) : 0u, st, pos_rank,
+                     (int)std::min<int64_t>(n, INT32_MAX), rank_off, pos_sorted);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+// Deterministic accumulation of one position's gradient row x (held by a wave,
+// XPL values per lane, column lane + 64 i) into G[grp][r] (row stride d),
+// positions of group grp = p % ng:
+//   * the node's only position in the batch (the common case): G row = x;
+//   * repeated: x goes to Gp[p]; every contributor of (grp, r) counts itself
+//     on arrive[grp][r] (release / acquire, MI355X_MICROARCH.md inter-workgroup
+//     visibility) and the last to arrive sums the group's rows in position
+//     order into G and re-arms the counter -- no float atomics, so the sum is
+//     bitwise the same on every run.
+//   rank_off[0] == -1 (no CSR): float atomics (order-dependent) as before.
+template <int XPL>
+__device__ __forceinline__ void det_accum(const float (&x)[XPL], int d, int p, int r, int grp, int ng,
+                                          const int* __restrict__ rank_off, const int32_t* __restrict__ pos_sorted,
+                                          float* __restrict__ G, int64_t S_max, float* __restrict__ Gp,
+                                          int* __restrict__ arrive, int lane) {
+  float* g = G + ((int64_t)grp * S_max + r) * d;
+  if (rank_off[0] < 0) {
+#pragma unroll
+    for (int i = 0; i < XPL; ++i)
+      if (lane + 64 * i < d) atomicAdd(g + lane + 64 * i, x[i]);
+    return;
+  }
+  const int o0 = rank_off[r], o1 = rank_off[r + 1];
+  if (o1 - o0 == 1) {
+#pragma unroll
+    for (int i = 0; i < XPL; ++i)
+      if (lane + 64 * i < d) g[lane + 64 * i] = x[i];
+    return;
+  }
+  // this group's contributors of r
+  int K = 0;
+  for (int o = o0; o < o1; o += 64) {
+    const int q = o + lane < o1 ? pos_sorted[o + lane] : -1;
+    K += __popcll(__ballot(q >= 0 && q % ng == grp));
+  }
+  if (K == 1) {
+#pragma unroll
+    for (int i = 0; i < XPL; ++i)
+      if (lane + 64 * i < d) g[lane + 64 * i] = x[i];
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < XPL; ++i)
+    if (lane + 64 * i < d) Gp[(int64_t)p * d + lane + 64 * i] = x[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0)
+    old = __hip_atomic_fetch_add(arrive + (int64_t)grp * S_max + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != K - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float acc[XPL];
+#pragma unroll
+  for (int i = 0; i < XPL; ++i) acc[i] = 0.f;
+  for (int o = o0; o < o1; ++o) {
+    const int q = pos_sorted[o];
+    if (q % ng != grp) continue;
+#pragma unroll
+    for (int i = 0; i < XPL; ++i)
+      if (lane + 64 * i < d) acc[i] += __builtin_nontemporal_load(Gp + (int64_t)q * d + lane + 64 * i);
+  }
+#pragma unroll
+  for (int i = 0; i < XPL; ++i)
+    if (lane + 64 * i < d) g[lane + 64 * i] = acc[i];
+  if (lane == 0) __hip_atomic_store(arrive + (int64_t)grp * S_max + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- loss
 // One wave per triple b: rows rq, rp, rn of Z (head outputs of the unique top
 // nodes).  Per call c in {q, pos, neg} and position b, the reference's
@@ -903,7 +1032,8 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
     const float* __restrict__ Z, int d, const int32_t* __restrict__ pos_rank, int B, float margin,
     const float* __restrict__ feats, int64_t ld_f, int d_in, const int64_t* __restrict__ batch,
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ part,
-    float* __restrict__ colpart, float* __restrict__ hinge) {
+    float* __restrict__ colpart, float* __restrict__ hinge, const int* __restrict__ rank_off,
+    const int32_t* __restrict__ pos_sorted, float* __restrict__ Gp, int* __restrict__ arrive) {
   __shared__ float red[4][4];  // per wave: loss, nfl, sum||h_q||^2, unused
   __shared__ float qrow[4][64 * ZPL];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -980,16 +1110,28 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
       pq = wave_sum(pq);
       pp = wave_sum(pp);
       pn = wave_sum(pn);
+      float xq[ZPL], xp[ZPL], xn[ZPL];
 #pragma unroll
       for (int i = 0; i < ZPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < d) {
-          const float a = zq[i] / nq, p = zp[i] / np, n = zn[i] / nn;
-          atomicAdd(G + ((int64_t)0 * S_max + rq) * d + c, (g * (n - p) - a * pq) / nq);
-          atomicAdd(G + ((int64_t)1 * S_max + rp) * d + c, (-g * a - p * pp) / np);
-          atomicAdd(G + ((int64_t)2 * S_max + rn) * d + c, (g * a - n * pn) / nn);
-        }
+        const float a = zq[i] / nq, p = zp[i] / np, n = zn[i] / nn;
+        xq[i] = (g * (n - p) - a * pq) / nq;
+        xp[i] = (-g * a - p * pp) / np;
+        xn[i] = (g * a - n * pn) / nn;
       }
+      det_accum<ZPL>(xq, d, 3 * b, rq, 0, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+      det_accum<ZPL>(xp, d, 3 * b + 1, rp, 1, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+      det_accum<ZPL>(xn, d, 3 * b + 2, rn, 2, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+    } else if (valid && rank_off[0] >= 0) {
+      // an inactive triple adds zeros: a repeated node's last contributor still
+      // needs every contributor's arrival (and zero rows) to form its sum
+      float z0[ZPL];
+#pragma unroll
+      for (int i = 0; i < ZPL; ++i) z0[i] = 0.f;
+      const int rr[3] = {rq, rp, rn};
+#pragma unroll
+      for (int c3 = 0; c3 < 3; ++c3)
+        if (rank_off[rr[c3] + 1] - rank_off[rr[c3]] > 1)
+          det_accum<ZPL>(z0, d, 3 * b + c3, rr[c3], c3, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
     }
     if (valid && lane == 0) {
       atomicAdd(Kc + 0 * S_max + rq, 1);
@@ -1230,15 +1372,23 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   }
 }
 
-// one call: G[r] = sum of dout rows at positions of node r, K[r] = multiplicity
-__global__ void dout_accum_kernel(const float* __restrict__ dout, int d,
-                                  const int32_t* __restrict__ pr, int64_t n, float* __restrict__ G,
-                                  int* __restrict__ Kc) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * d;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = e / d, c = e - i * d;
-    atomicAdd(G + (int64_t)pr[i] * d + c, dout[e]);
-    if (c == 0) atomicAdd(Kc + pr[i], 1);
+// one call: G[r] = sum of dout rows at positions of node r (in position order,
+// det_accum), K[r] = multiplicity; one wave per position
+__global__ __launch_bounds__(256) void dout_accum_kernel(const float* __restrict__ dout, int d,
+                                                         const int32_t* __restrict__ pr, int64_t n,
+                                                         float* __restrict__ G, int* __restrict__ Kc, int64_t S_max,
+                                                         const int* __restrict__ rank_off,
+                                                         const int32_t* __restrict__ pos_sorted,
+                                                         float* __restrict__ Gp, int* __restrict__ arrive) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
+    const int r = pr[i];
+    float x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = lane + 64 * k < d ? dout[i * d + lane + 64 * k] : 0.f;
+    det_accum<4>(x, d, (int)i, r, 0, 1, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+    if (lane == 0) atomicAdd(Kc + r, 1);
   }
 }
 __global__ void dz_scale_kernel(const float* __restrict__ G, const int* __restrict__ Kc, int d,
@@ -1358,9 +1508,11 @@ int launch_gather_rows(const float* h, int64_t ldh, int64_t n_h, int d, const in
 // 0, K slab 0); dZ = K * G is formed by the fused head backward (or here, for
 // the unfused head: scale = true)
 int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, const int* nS,
-                        int64_t S_max, float* G, int* Kc, float* dZ, bool scale, hipStream_t st) {
-  hipLaunchKernelGGL(dout_accum_kernel, dim3(grid_for(n * d, 256)), dim3(256), 0, st, dout, d, pr, n,
-                     G, Kc);
+                        int64_t S_max, float* G, int* Kc, float* dZ, bool scale, const int* rank_off,
+                        const int32_t* pos_sorted, float* Gp, int* arrive, hipStream_t st) {
+  PS_REQUIRE(d <= 256, kErrArg, "dz_from_dout: out_dim must be <= 256");
+  hipLaunchKernelGGL(dout_accum_kernel, dim3(grid_for(n * 64, 256)), dim3(256), 0, st, dout, d, pr, n, G, Kc, S_max,
+                     rank_off, pos_sorted, Gp, arrive);
   PS_CHECK_LAUNCH();
   if (scale) {
     hipLaunchKernelGGL(dz_scale_kernel, dim3(grid_for(S_max * d, 256)), dim3(256), 0, st, G, Kc, d, nS,
@@ -1561,7 +1713,8 @@ int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int
 int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float margin,
                 const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
                 int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
-                float* hinge, bool combine_dz, hipStream_t st) {
+                float* hinge, bool combine_dz, const int* rank_off, const int32_t* pos_sorted, float* Gp,
+                int* arrive, hipStream_t st) {
   // G and Kc are zero on entry (init_workspace; then the head backward (or
   // dz_combine) and the first backward kernel leave them zero)
   PS_REQUIRE(d <= 256, kErrArg, "loss: out_dim must be <= 256");
@@ -1570,7 +1723,8 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   const int fpl = d_in <= 128 ? 2 : d_in <= 256 ? 4 : 8;
 #define PS_LOSS(ZP, FP)                                                                           \
   hipLaunchKernelGGL((loss_triple_kernel<ZP, FP>), dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, \
-                     margin, feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge)
+                     margin, feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge, rank_off, pos_sorted, \
+                     Gp, arrive)
   if (d <= 128) {
     if (fpl == 2) PS_LOSS(2, 2);
     else if (fpl == 4) PS_LOSS(2, 4);

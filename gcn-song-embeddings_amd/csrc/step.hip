@@ -10,6 +10,9 @@
 #include "../../include/pinsage_hip.h"
 #include "common.h"
 
+#include <cstring>
+#include <vector>
+
 namespace ps {
 
 __global__ void step_stage_kernel(const uint64_t* __restrict__ ring, int64_t slot_words, int64_t R,
@@ -83,6 +86,147 @@ int pinsage_stream_hold(int64_t us, void* stream) {
   }
   hipLaunchKernelGGL(stream_hold_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint64_t)us * 100u);
   PS_CHECK_LAUNCH();
+  return kOk;
+}
+
+// ------------------------------------------------------------------ the host side of one step
+// The per-step host work of _FusedStep in one call: wait for the ring slot's
+// previous user, write the Adam coefficients, reuse or stage the step's ids
+// (its frontier was computed ahead when the batch equals the predicted one),
+// write the next step's predicted ids and launch the captured graphs.  The
+// graphs are hipGraphExec_t handles of torch.cuda.CUDAGraph captures
+// (raw_cuda_graph_exec), so a step costs one C call besides the launches.
+struct Stepper {
+  int64_t R = 0, slot_bytes = 0, off_ids = 0, off_next = 0, off_coef = 0, max_ids = 0, n_items = 0;
+  uint8_t* ring = nullptr;  // pinned host ring [R][slot_bytes]
+  hipGraphExec_t gf[2] = {nullptr, nullptr}, gm[2] = {nullptr, nullptr}, ga[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev;
+  std::vector<char> ev_live;
+  std::vector<int64_t> pending[2];  // ids whose frontier sits in workspace p (empty: none)
+  int parity = 0;
+  int64_t nstep = 0, hits = 0;
+};
+
+}  // extern "C"
+namespace {
+bool ids_in_range(const int64_t* ids, int64_t n, int64_t n_items) {
+  for (int64_t i = 0; i < n; ++i)
+    if (ids[i] < 0 || ids[i] >= n_items) return false;
+  return true;
+}
+}  // namespace
+extern "C" {
+
+int pinsage_stepper_create(void* ring, int64_t R, int64_t slot_bytes, int64_t off_ids, int64_t off_next,
+                           int64_t off_coef, int64_t max_ids, int64_t n_items, pinsage_stepper** out) {
+  if (!ring || !out || R <= 0 || max_ids <= 0 || off_ids < 0 || off_next < 0 || off_coef < 0 ||
+      off_ids + max_ids * 8 > slot_bytes || off_next + max_ids * 8 > slot_bytes || off_coef + 8 > slot_bytes) {
+    set_error("stepper_create: bad argument");
+    return kErrArg;
+  }
+  auto* s = new Stepper();
+  s->ring = static_cast<uint8_t*>(ring);
+  s->R = R;
+  s->slot_bytes = slot_bytes;
+  s->off_ids = off_ids;
+  s->off_next = off_next;
+  s->off_coef = off_coef;
+  s->max_ids = max_ids;
+  s->n_items = n_items;
+  s->ev.assign((size_t)R, nullptr);
+  s->ev_live.assign((size_t)R, 0);
+  for (auto& e : s->ev) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      set_error("stepper_create: hipEventCreate failed");
+      for (auto& x : s->ev)
+        if (x) (void)hipEventDestroy(x);
+      delete s;
+      return kErrHip;
+    }
+  }
+  *out = reinterpret_cast<pinsage_stepper*>(s);
+  return kOk;
+}
+
+void pinsage_stepper_destroy(pinsage_stepper* h) {
+  auto* s = reinterpret_cast<Stepper*>(h);
+  if (!s) return;
+  for (auto& e : s->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete s;
+}
+
+int pinsage_stepper_set_graphs(pinsage_stepper* h, int p, void* gf, void* gm, void* ga) {
+  auto* s = reinterpret_cast<Stepper*>(h);
+  if (!s || (p != 0 && p != 1) || !gf || !gm) {
+    set_error("stepper_set_graphs: bad argument");
+    return kErrArg;
+  }
+  s->gf[p] = (hipGraphExec_t)gf;
+  s->gm[p] = (hipGraphExec_t)gm;
+  s->ga[p] = (hipGraphExec_t)ga;
+  return kOk;
+}
+
+int pinsage_stepper_sync_state(pinsage_stepper* h, int parity, int64_t nstep) {
+  auto* s = reinterpret_cast<Stepper*>(h);
+  if (!s || (parity != 0 && parity != 1) || nstep < 0) {
+    set_error("stepper_sync_state: bad argument");
+    return kErrArg;
+  }
+  s->parity = parity;
+  s->nstep = nstep;
+  s->pending[0].clear();
+  s->pending[1].clear();
+  return kOk;
+}
+
+int pinsage_stepper_step(pinsage_stepper* h, const int64_t* batch, int64_t n_ids, const float* coef,
+                         const int64_t* next, void* stream, int64_t* info) {
+  auto* s = reinterpret_cast<Stepper*>(h);
+  if (!s || !batch || !coef || n_ids <= 0 || n_ids > s->max_ids) {
+    set_error("stepper_step: bad argument");
+    return kErrArg;
+  }
+  const int p = s->parity;
+  if (!s->gf[p] || !s->gm[p] || (next && !s->ga[p])) {
+    set_error("stepper_step: graphs not set");
+    return kErrArg;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t k = s->nstep % s->R;
+  if (s->ev_live[(size_t)k]) PS_CHECK_HIP(hipEventSynchronize(s->ev[(size_t)k]));  // the slot's last user is done
+  uint8_t* slot = s->ring + k * s->slot_bytes;
+  std::memcpy(slot + s->off_coef, coef, 8);
+  const bool hit = (int64_t)s->pending[p].size() == n_ids &&
+                   std::memcmp(s->pending[p].data(), batch, (size_t)n_ids * 8) == 0;
+  if (!hit) {
+    if (!ids_in_range(batch, n_ids, s->n_items)) {
+      set_error("stepper_step: batch ids out of range");
+      return kErrIndex;
+    }
+    std::memcpy(slot + s->off_ids, batch, (size_t)n_ids * 8);
+    PS_CHECK_HIP(hipGraphLaunch(s->gf[p], st));
+  } else {
+    s->hits++;
+  }
+  s->pending[p].clear();
+  if (next && ids_in_range(next, n_ids, s->n_items)) {
+    std::memcpy(slot + s->off_next, next, (size_t)n_ids * 8);
+    PS_CHECK_HIP(hipGraphLaunch(s->ga[p], st));
+    s->pending[1 - p].assign(next, next + n_ids);
+  } else {
+    PS_CHECK_HIP(hipGraphLaunch(s->gm[p], st));
+    s->pending[1 - p].clear();
+  }
+  PS_CHECK_HIP(hipEventRecord(s->ev[(size_t)k], st));
+  s->ev_live[(size_t)k] = 1;
+  if (info) {
+    info[0] = hit ? 1 : 0;
+    info[1] = s->nstep;
+  }
+  s->parity ^= 1;
+  s->nstep++;
   return kOk;
 }
 

@@ -990,7 +990,7 @@ class _EngineRunner:
             tabs.append((nbt, wnt))
         # feature rows: call c's copy of the table at c * n_items (made once per
         # feature tensor), the virtual rows written per call group
-        fx = self._fly_feats(feats, C, n_items, n_valid)
+        fx = self._fly_feats(feats, C, n_items, n_valid, n_x=sum(n_x))
         parts, xo = [], base_x
         for c, d in enumerate(draws):
             parts.append(d.uniq + c * n_items)
@@ -1012,16 +1012,21 @@ class _EngineRunner:
             outs.append(out_u[d.inv].to(initial_h.device))
         return outs
 
-    def _fly_feats(self, feats, C, n_items, n_valid):
+    def _fly_feats(self, feats, C, n_items, n_valid, n_x=0):
         """Feature rows of fly_calls' node ids: call c's copy of the table at
         c * n_items (made once per feature tensor); rows from C * n_items are
-        the virtual nodes', written per call group."""
+        the virtual nodes', written per call group.  A call that writes virtual
+        rows while an earlier call's backward is still pending on the cached
+        buffer (its backward reads those rows) gets its own copy."""
         key = (id(feats), feats.data_ptr(), getattr(feats, "_version", 0), C, int(self.engine.cfg.n_items))
         if getattr(self, "_fly_feat_key", None) != key:
             fx = torch.empty((int(self.engine.cfg.n_items), feats.shape[1]), dtype=feats.dtype, device=self.dev)
             for c in range(C):
                 fx[c * n_items:c * n_items + n_valid] = feats[:n_valid]
             self._fly_feat, self._fly_feat_key = fx, key
+            self._fly_pending = set()
+        if n_x and self._fly_pending:
+            return self._fly_feat.clone()
         return self._fly_feat
 
     def _fly_calls_merged(self, initial_h, feats, ids_c, n_items, n_valid):
@@ -1034,7 +1039,7 @@ class _EngineRunner:
         base_x = C * n_items
         if base_x + n_x > int(self.engine.cfg.n_items):
             raise RuntimeError("on-the-fly calls exceed the engine's node rows")
-        fx = self._fly_feats(feats, C, n_items, n_valid)
+        fx = self._fly_feats(feats, C, n_items, n_valid, n_x=n_x)
         ids = uniq
         if n_x:
             fx[base_x:base_x + n_x] = feats[ids_x]
@@ -1104,6 +1109,13 @@ class _EngineFn(torch.autograd.Function):
         # pool when the autograd node is freed (after the last backward a
         # retained graph may still run), never earlier
         weakref.finalize(ctx, e.release_workspace, ws)
+        pend = getattr(runner, "_fly_pending", None)
+        if pend is not None and feats is getattr(runner, "_fly_feat", None):
+            # this call's backward reads the shared on-the-fly feature buffer
+            tok = object()
+            pend.add(tok)
+            ctx.fly_tok = tok
+            weakref.finalize(ctx, pend.discard, tok)
         return out
 
     @staticmethod
@@ -1119,6 +1131,9 @@ class _EngineFn(torch.autograd.Function):
                                                            nat.stream_ptr()), "set_output_grad")
         nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(ws), nat.stream_ptr()), "backward")
         ctx.n_bwd += 1
+        tok = getattr(ctx, "fly_tok", None)
+        if tok is not None:
+            runner.__dict__.get("_fly_pending", set()).discard(tok)
         out = []
         off = 0
         for p in runner.params():

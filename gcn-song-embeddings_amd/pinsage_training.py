@@ -203,21 +203,24 @@ def batch_variance(h):
 # ----------------------------------------------------------------------------- data parallel
 def _allreduce_start(flat):
     """Begin the mean of a flat gradient bucket over the process group, ordered
-    after the current stream's work; returns a handle for _allreduce_finish
-    (RCCL: asynchronous on its own stream, averaged in the collective; gloo:
-    synchronous, then scaled)."""
+    after the current stream's work; returns a handle for _allreduce_finish.
+    Both backends run it asynchronously (async_op=True), so the overlap and its
+    stream ordering are the same code on RCCL (the 8-GPU run) and on gloo (the
+    tests): RCCL averages in the collective; gloo sums (it has no AVG) and the
+    finish scales."""
     d = torch.distributed
     if d.get_backend() == "nccl":
-        return d.all_reduce(flat, op=d.ReduceOp.AVG, async_op=True)
-    d.all_reduce(flat)
-    flat.mul_(1.0 / d.get_world_size())
-    return None
+        return d.all_reduce(flat, op=d.ReduceOp.AVG, async_op=True), None
+    return d.all_reduce(flat, async_op=True), flat
 
 
-def _allreduce_finish(work):
-    """The current stream waits for a bucket started by _allreduce_start."""
-    if work is not None:
-        work.wait()
+def _allreduce_finish(handle):
+    """The current stream waits for a bucket started by _allreduce_start (and
+    the gloo sum becomes the mean, on that stream)."""
+    work, flat = handle
+    work.wait()
+    if flat is not None:
+        flat.mul_(1.0 / torch.distributed.get_world_size())
 
 
 def average_gradients(flat):
@@ -351,6 +354,7 @@ class _FusedStep:
             self._tuned = False
             self.tuned_choices = None
             self.graphs = None
+            self._drop_stepper()
 
     def adopt_optimizer_state(self):
         """Use the optimizer's Adam state (if any, e.g. after load_state_dict) as
@@ -712,6 +716,68 @@ class _FusedStep:
         self.graphs = graphs
         self.graph_B = B
         self.graph_sig = sig
+        self._make_stepper(B)
+
+    # ---- the native per-step host path (pinsage_stepper_*)
+    def _make_stepper(self, B):
+        """After a capture: the host side of each step as one native call
+        (ring slot wait, coefficients, ids / ahead check, graph launches) when
+        the step is one stream's graphs (not data-parallel, not "split")."""
+        self._drop_stepper(sync=False)
+        if (self.dist or self.ahead_mode == "split" or os.environ.get("PINSAGE_NATIVE_STEP", "1") == "0"
+                or not hasattr(torch.cuda.CUDAGraph, "raw_cuda_graph_exec")):
+            return
+        L = nat.lib()
+        h = ctypes.c_void_p()
+        nat.check(L.pinsage_stepper_create(nat.ptr(self.ring), self.HOST_RING, self.slot_bytes, self.slot_ids,
+                                           self.slot_next, self.slot_coef, 3 * B,
+                                           int(self.runner.engine.cfg.n_items), ctypes.byref(h)), "stepper_create")
+        self.stepper = h
+        for p, (gf, gm, ga, _) in enumerate(self.graphs):
+            nat.check(L.pinsage_stepper_set_graphs(h, p, ctypes.c_void_p(gf.raw_cuda_graph_exec()),
+                                                   ctypes.c_void_p(gm.raw_cuda_graph_exec()),
+                                                   ctypes.c_void_p(ga.raw_cuda_graph_exec())), "stepper_set_graphs")
+        # (called at the end of a capture, inside the eager step self.nstep: the
+        # native path takes over from the next step, with every ring slot free)
+        torch.cuda.current_stream().synchronize()
+        nat.check(L.pinsage_stepper_sync_state(h, self.parity, self.nstep + 1), "stepper_sync_state")
+        self._coef_np = np.zeros(2, np.float32)
+        self._info = (ctypes.c_int64 * 2)()
+
+    def _drop_stepper(self, sync=True):
+        st = getattr(self, "stepper", None)
+        if st is None:
+            return
+        if sync:  # its ring slots may still be read by launched steps
+            torch.cuda.current_stream().synchronize()
+        nat.lib().pinsage_stepper_destroy(st)
+        self.stepper = None
+
+    def _call_native(self, batch, B):
+        """One captured step through pinsage_stepper_step (the graph path of
+        _call below, in C)."""
+        b = batch.numpy() if batch.device.type == "cpu" else batch.cpu().numpy()
+        if b.dtype != np.int64 or not b.flags.c_contiguous:
+            b = np.ascontiguousarray(b, dtype=np.int64)
+        self._coef_np[:] = self._adam_coef(self.host_step + 1)
+        nxt = self._predicted(B)
+        if nxt is not None and (nxt.dtype != np.int64 or not nxt.flags.c_contiguous):
+            nxt = np.ascontiguousarray(nxt, dtype=np.int64)
+        _tick("peek")
+        rc = nat.lib().pinsage_stepper_step(self.stepper, b.ctypes.data_as(nat.vp), 3 * B,
+                                            self._coef_np.ctypes.data_as(nat.vp),
+                                            nxt.ctypes.data_as(nat.vp) if nxt is not None else None,
+                                            nat.stream_ptr(), self._info)
+        if rc == -5:
+            raise IndexError(f"batch ids out of range for {int(self.runner.engine.cfg.n_items)} items")
+        nat.check(rc, "stepper_step")
+        self.ahead_hits += int(self._info[0])
+        self.parity ^= 1
+        out = self.out_ring[self.nstep % self.OUT_RING]
+        self.nstep += 1
+        self.host_step += 1
+        _tick("replay")
+        return out[0], out[1], out[3]
 
     def _predicted(self, B):
         """This rank's slice of the batch the sampler drew ahead, or None."""
@@ -755,14 +821,19 @@ class _FusedStep:
         r = self.runner
         feats = r.features(tr.features)
         table = r.table(tr.nbhds)
-        r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)
         self.B_cur = B
-        p = self.parity
-        self.parity ^= 1
-        self.ws = self.wss[p]
         sig = self._signature(feats, table)
         if self.graphs is not None and (self.graph_B != B or self.graph_sig != sig or not self.use_graph):
             self.graphs = None  # buffers moved: the captured pointers are stale
+            self._drop_stepper()
+        if self.graphs is not None and getattr(self, "stepper", None) is not None:
+            self.ws = self.wss[self.parity]
+            _tick("pre")
+            return self._call_native(batch, B)  # (the captured graphs hold every pointer: no bind)
+        r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)
+        p = self.parity
+        self.parity ^= 1
+        self.ws = self.wss[p]
         _tick("pre")
         k = self.nstep % self.HOST_RING
         if self.ring_ev[k] is not None:  # the step that used this slot is done
@@ -972,7 +1043,13 @@ class PinSage:
         backward per call (autograd), torch's Adam."""
         batch = torch.as_tensor(batch)
         model = self.model
-        if model._forward_pre_hooks or model._forward_hooks_with_kwargs:
+        from torch.nn.modules import module as _nnm
+        if (model._forward_pre_hooks or model._forward_hooks_with_kwargs or model._forward_hooks_always_called
+                or model._backward_hooks or model._backward_pre_hooks or _nnm._global_forward_hooks
+                or _nnm._global_forward_pre_hooks or _nnm._global_backward_hooks
+                or _nnm._global_backward_pre_hooks):
+            # hooks the merged call cannot replay per call (pre-hooks, global
+            # and backward hooks): the reference's three model calls
             h_q = model(self.features, batch[:, 0])
             h_pos = model(self.features, batch[:, 1])
             h_neg = model(self.features, batch[:, 2])

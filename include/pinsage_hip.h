@@ -279,6 +279,29 @@ int pinsage_step_publish(const float* scal, int64_t n, float* ring_out, int64_t 
  * time the kernels rather than the host's enqueue gaps. */
 int pinsage_stream_hold(int64_t us, void* stream);
 
+/* The host side of one captured train step (pinsage_training._FusedStep) in
+ * one call -- the per-step work of pinsage_training.py:181-191's loop body
+ * before the device runs it.  ring: the pinned hand-off ring [R][slot_bytes]
+ * whose slot holds the step's ids (off_ids), the predicted next ids
+ * (off_next) and the Adam coefficients (off_coef, 2 f32).  Per parity p
+ * (workspace), three hipGraphExec_t of torch captures: gf (stage + frontier),
+ * gm (the step), ga (the step + the next batch's frontier in the other
+ * workspace).  pinsage_stepper_step: waits for the slot's previous step,
+ * writes coef, launches gf unless the batch equals the ids whose frontier the
+ * previous step computed ahead, then ga with `next` (the sampler's predicted
+ * next batch, nullable) or gm, and records the slot's event.  batch / next:
+ * n_ids int64 host ids (ids outside [0, n_items): kErrIndex, nothing
+ * launched).  info (nullable) int64[2] = {ahead hit, step index}. */
+typedef struct pinsage_stepper pinsage_stepper;
+int pinsage_stepper_create(void* ring, int64_t R, int64_t slot_bytes, int64_t off_ids, int64_t off_next,
+                           int64_t off_coef, int64_t max_ids, int64_t n_items, pinsage_stepper** out);
+void pinsage_stepper_destroy(pinsage_stepper* s);
+int pinsage_stepper_set_graphs(pinsage_stepper* s, int p, void* gf, void* gm, void* ga);
+/* resume from the trainer's eager path: next parity, step counter, no pending frontier */
+int pinsage_stepper_sync_state(pinsage_stepper* s, int parity, int64_t nstep);
+int pinsage_stepper_step(pinsage_stepper* s, const int64_t* batch, int64_t n_ids, const float* coef,
+                         const int64_t* next, void* stream, int64_t* info);
+
 /* ------------------------------------------------------------------ lib/gnns MEAN aggregator
  * GNN_model.aggregate, agg_func 'MEAN' (lib/gnns/GNNs_unsupervised.py:537-588):
  * mask.mm(embed_matrix) with the dense [F, U] mask kept as a CSR.  For each

@@ -47,6 +47,17 @@ def _worker(rank, world, port, tmp, out_q):
         state = torch.get_rng_state()
         flat = torch.full((10,), float(rank + 1))
         pt.average_gradients(flat)
+        # the staged step's bucket protocol (_dp_tail): two asynchronous starts,
+        # work between them, then the finishes in start order -- the code the
+        # RCCL path runs (gloo: async sum, the finish scales to the mean)
+        ba, bb = torch.full((7,), 2.0 * (rank + 1)), torch.full((5,), -3.0 * (rank + 1))
+        wa = pt._allreduce_start(ba)
+        busy = torch.arange(1000.0).sum()
+        wb = pt._allreduce_start(bb)
+        pt._allreduce_finish(wa)
+        pt._allreduce_finish(wb)
+        buckets_ok = bool(torch.allclose(ba, torch.full((7,), 3.0)) and torch.allclose(bb, torch.full((5,), -4.5))
+                          and float(busy) == 499500.0)
         # precompute exchange: equal contiguous shards (n not divisible by the
         # world size), one all-gather per table
         import pinsage_model as pm
@@ -59,7 +70,7 @@ def _worker(rank, world, port, tmp, out_q):
         sw[:hi - lo], snb[:hi - lo] = full_w[lo:hi], full_nb[lo:hi]
         gw, gnb = pm._gather_shards(sw, snb, n, per, None)
         gathered_ok = torch.equal(gw, full_w) and torch.equal(gnb, full_nb)
-        out_q.put((rank, [s.numpy() for s in slices], state.numpy(), flat.numpy(), gathered_ok))
+        out_q.put((rank, [s.numpy() for s in slices], state.numpy(), flat.numpy(), gathered_ok and buckets_ok))
     finally:
         os.chdir(cwd)
         dist.destroy_process_group()
@@ -105,4 +116,4 @@ def test_dp_batch_slices_and_grad_average():
         assert (got == ref[s]).all()
     assert (res[0][1] == res[1][1]).all()  # RNG stays in lock-step across ranks
     assert np.allclose(res[0][2], 1.5) and np.allclose(res[1][2], 1.5)
-    assert res[0][3] and res[1][3]  # all-gathered precompute shards == the full table
+    assert res[0][3] and res[1][3]  # all-gathered precompute shards == the full table; async buckets averaged

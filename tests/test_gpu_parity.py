@@ -709,3 +709,55 @@ def test_presplit_q_weights_train_like_in_register_split():
                 else:
                     os.environ[k] = v
             os.chdir(cwd)
+
+
+def test_default_step_is_bitwise_reproducible():
+    """two fresh trainers with the default in-context GEMM
+    tuner ON and the same seeds end 3 fused steps with bitwise-equal
+    parameters and losses.  What makes it hold: the tuner's candidates keep
+    every site's summation order (tile configs only; split-K counts and
+    stream-K stay the size model's), the backward's CSR pairs are sorted by
+    source row (canonical transposed-aggregation order), and a node repeated
+    inside a call has its per-position loss gradients summed in position order
+    by the last contributor (no float atomics).  The batch (512 triples over
+    3000 tracks) repeats nodes three and more times per call, and popular
+    tracks split over several CSR chunks."""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(3000, 600, 20000, seed=61)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(3000, 256, seed=62))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 15000, seed=63))
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        old = os.environ.pop("PINSAGE_AUTOTUNE", None)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
+            pt.PinSage(g, 3000, feats, pos, log=False, load_save=False)  # (precompute the table once)
+
+            def run():
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, 3000, feats, pos, log=False, load_save=False)
+                tr.batch_size = 512
+                torch.manual_seed(6)
+                losses, reps = [], 0
+                for _ in range(3):
+                    batch, _ = tr.next_batch()
+                    for c in range(3):
+                        reps = max(reps, int(torch.bincount(batch[:, c].reshape(-1)).max()))
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                assert tr._fused.tuned_choices is not None  # the tuner ran
+                return losses, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).cpu(), reps
+
+            l0, p0, reps = run()
+            l1, p1, _ = run()
+            assert reps >= 3, reps
+            assert l0 == l1, (l0, l1)
+            assert torch.equal(p0, p1), (p0 - p1).abs().max().item()
+        finally:
+            os.chdir(cwd)
+            if old is not None:
+                os.environ["PINSAGE_AUTOTUNE"] = old

@@ -1,14 +1,17 @@
-# Round 4: GPU tests touched this session, then the aggregation + W A/B
+# Round 4: the GPU suite, then A/B lines (aggregation + W form; native step host path)
 set -o pipefail
 out=gpurun_out/r4ab
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_aggw.py tests/test_gpu_trainer.py tests/test_gpu_torch_ops.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
 tail -1 $out/tests.log
 for f in 1 0; do
   PINSAGE_AGGW_FORM=$f timeout -k 10 120 python tools/aggw_bench.py --shapes c2l0,c2l1,c4l0,c4sl0 > $out/aggw_bench_f$f.json 2>&1 || { tail $out/aggw_bench_f$f.json; exit 1; }
 done
-for f in 1 0 1 0; do
+for f in 1 0; do
   PINSAGE_AGGW_FORM=$f timeout -k 10 150 python bench.py --no-cpu-baseline > $out/c2_f$f.json 2>$out/c2_f$f.err || { tail $out/c2_f$f.err; exit 1; }
   PINSAGE_AGGW_FORM=$f timeout -k 10 200 python bench.py --no-cpu-baseline --config c4 --scaling strong > $out/c4s_f$f.json 2>$out/c4s_f$f.err || { tail $out/c4s_f$f.err; exit 1; }
+done
+for n in 0 1; do
+  PINSAGE_NATIVE_STEP=$n PINSAGE_HOST_TIMING=1 timeout -k 10 150 python bench.py --no-cpu-baseline > $out/c2_native$n.json 2>$out/c2_native$n.err || { tail $out/c2_native$n.err; exit 1; }
 done
 echo ok
