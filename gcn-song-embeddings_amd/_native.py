@@ -93,6 +93,7 @@ _SIGS = {
     "pinsage_step_stage": (ctypes.c_int, [vp, i64, i64, vp, i64, i64, vp, i64, vp, vp]),
     "pinsage_step_publish": (ctypes.c_int, [vp, i64, vp, i64, vp, vp]),
     "pinsage_stream_hold": (ctypes.c_int, [i64, vp]),
+    "pinsage_engine_site_stream_k": (ctypes.c_int, [vp, ctypes.c_char_p]),
     "pinsage_stepper_create": (ctypes.c_int, [vp, i64, i64, i64, i64, i64, i64, i64, vp]),
     "pinsage_stepper_destroy": (None, [vp]),
     "pinsage_stepper_set_graphs": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp]),

@@ -584,68 +584,108 @@ __global__ __launch_bounds__(256) void csr_sort_chunks_kernel(const int2* __rest
 }
 
 // Rows split over several chunks (the scan's split list {u, first chunk}):
-// the row's n pairs are contiguous from occ2[cbase * kDqChunk]; one block per
-// row sorts them in LDS up to kSortLds pairs (a bitonic network in its
-// all-ascending form, so the virtual +inf padding past n never moves), in
-// global memory beyond (loads through L2, agent-scope relaxed: correct, slow,
-// only for rows in tens of thousands of neighbour lists).
-constexpr int kSortLds = 20480;  // pairs (160 KiB)
-__device__ __forceinline__ long long pack_pair(int2 v) {
-  return (long long)(((unsigned long long)(unsigned)v.y << 32) | (unsigned)v.x);
-}
+// the row's n pairs are contiguous from occ2[cbase * kDqChunk], and their
+// source rows f are distinct.  One block per row ranks every pair by a bitmap
+// of the f range (windows of kRankBits): a pair's sorted position is the
+// count of set bits below its own, read from per-word popcount prefixes, so it
+// writes itself to its place in `tmp` (no comparison sort: O(range / 32 + n)
+// per row), then the sorted row is copied back.
+constexpr int kRankWords = 16384;                   // bitmap words per window (64 KiB)
+constexpr int64_t kRankBits = (int64_t)kRankWords * 32;
+constexpr int kRankLds = kRankWords * 4 * 2 + 64;   // bitmap + word prefixes + scan scratch
 __global__ __launch_bounds__(1024) void csr_sort_rows_kernel(const int2* __restrict__ split,
                                                              const int* __restrict__ nsplit,
-                                                             const int* __restrict__ off, int2* __restrict__ occ2) {
-  extern __shared__ int2 buf[];
+                                                             const int* __restrict__ off, int2* __restrict__ occ2,
+                                                             int2* __restrict__ tmp) {
+  extern __shared__ unsigned rk[];
+  unsigned* bits = rk;                            // [kRankWords]
+  unsigned* pref = rk + kRankWords;               // [kRankWords] exclusive popcount prefix
+  int* red = reinterpret_cast<int*>(pref + kRankWords);  // [16] wave partials
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ns = *nsplit;
   for (int si = blockIdx.x; si < ns; si += gridDim.x) {
     const int2 sp = split[si];
     const int n = off[sp.x + 1] - off[sp.x];
     int2* row = occ2 + (int64_t)sp.y * kDqChunk;
-    int p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    if (n <= kSortLds) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) buf[i] = row[i];
-      __syncthreads();
-      for (int k = 2; k <= p2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = threadIdx.x; i < p2 / 2; i += blockDim.x) {
-            // pair (a, b), a < b: the first stage of a merge compares mirrored
-            // positions, the later ones distance j; min to a
-            const int lo = (i / j) * 2 * j + (i % j);
-            const int a = j == (k >> 1) ? (lo / k) * k + (lo % k) : lo;
-            const int b = j == (k >> 1) ? (a / k) * k + (k - 1 - a % k) : lo + j;
-            if (b < n && buf[b].x < buf[a].x) {
-              const int2 t = buf[a];
-              buf[a] = buf[b];
-              buf[b] = t;
-            }
-          }
-          __syncthreads();
-        }
-      for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = buf[i];
-      __syncthreads();
-    } else {
-      long long* rw = reinterpret_cast<long long*>(row);
-      for (int k = 2; k <= p2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = threadIdx.x; i < p2 / 2; i += blockDim.x) {
-            const int lo = (i / j) * 2 * j + (i % j);
-            const int a = j == (k >> 1) ? (lo / k) * k + (lo % k) : lo;
-            const int b = j == (k >> 1) ? (a / k) * k + (k - 1 - a % k) : lo + j;
-            if (b < n) {
-              const long long va = __hip_atomic_load(rw + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              const long long vb = __hip_atomic_load(rw + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if ((int)(unsigned)vb < (int)(unsigned)va) {
-                __hip_atomic_store(rw + a, vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(rw + b, va, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              }
-            }
-          }
-          __threadfence_block();
-          __syncthreads();
-        }
+    int2* out = tmp + (int64_t)sp.y * kDqChunk;
+    // f range of the row
+    int lo = INT_MAX, hi = -1;
+    for (int i = tid; i < n; i += blockDim.x) {
+      const int f = row[i].x;
+      lo = min(lo, f);
+      hi = max(hi, f);
     }
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o, 64));
+      hi = max(hi, __shfl_xor(hi, o, 64));
+    }
+    if (lane == 0) red[wv] = lo;
+    __syncthreads();
+    if (tid == 0) {
+      int a = red[0];
+      for (int w = 1; w < 16; ++w) a = min(a, red[w]);
+      red[0] = a;
+    }
+    __syncthreads();
+    lo = red[0];
+    __syncthreads();
+    if (lane == 0) red[wv] = hi;
+    __syncthreads();
+    if (tid == 0) {
+      int a = red[0];
+      for (int w = 1; w < 16; ++w) a = max(a, red[w]);
+      red[0] = a;
+    }
+    __syncthreads();
+    hi = red[0];
+    __syncthreads();
+    int base = 0;  // pairs placed by earlier windows
+    for (int64_t w0 = lo; w0 <= hi; w0 += kRankBits) {
+      const int nwords = (int)min((int64_t)kRankWords, (hi - w0) / 32 + 1);
+      for (int i = tid; i < nwords; i += blockDim.x) bits[i] = 0u;
+      __syncthreads();
+      for (int i = tid; i < n; i += blockDim.x) {
+        const int64_t b = (int64_t)row[i].x - w0;
+        if (b >= 0 && b < (int64_t)nwords * 32) atomicOr(bits + (b >> 5), 1u << (b & 31));
+      }
+      __syncthreads();
+      // exclusive prefix of the words' popcounts: each thread a contiguous run
+      const int per = (nwords + (int)blockDim.x - 1) / (int)blockDim.x;
+      const int i0 = tid * per;
+      int s = 0;
+      for (int i = i0; i < min(nwords, i0 + per); ++i) s += __popc(bits[i]);
+      int inc = s;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) red[wv] = inc;
+      __syncthreads();
+      int pre = inc - s;
+      for (int w = 0; w < wv; ++w) pre += red[w];
+      int total = 0;
+      for (int w = 0; w < 16; ++w) total += red[w];
+      for (int i = i0; i < min(nwords, i0 + per); ++i) {
+        pref[i] = (unsigned)pre;
+        pre += __popc(bits[i]);
+      }
+      __syncthreads();
+      for (int i = tid; i < n; i += blockDim.x) {
+        const int2 v = row[i];
+        const int64_t b = (int64_t)v.x - w0;
+        if (b >= 0 && b < (int64_t)nwords * 32) {
+          const int wd = (int)(b >> 5);
+          const int r = base + (int)pref[wd] + __popc(bits[wd] & ((1u << (b & 31)) - 1u));
+          out[r] = v;
+        }
+      }
+      base += total;
+      __syncthreads();  // (the next window rewrites bits / pref / red)
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) row[i] = out[i];
+    __syncthreads();
   }
 }
 
@@ -1609,7 +1649,7 @@ int csr_prepare() {
                             kLdsRows * 4) != hipSuccess)
       return (int)kErrHip;
     if (hipFuncSetAttribute((const void*)csr_sort_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kSortLds * 8) != hipSuccess)
+                            kRankLds) != hipSuccess)
       return (int)kErrHip;
     return (int)kOk;
   }();
@@ -1620,7 +1660,8 @@ int csr_prepare() {
 int64_t dq_chunk_capacity(int64_t S_max, int T, int64_t N_max);
 int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64_t S_max, int T, const int* nN,
                      int64_t N_max, int* cnt, int* bsum, int* off, int* cursor, int* cbase, int2* occ2,
-                     int2* chunks, int* nchunks, int2* split, int* nsplit, float* dpq, int hid, hipStream_t st) {
+                     int2* chunks, int* nchunks, int2* split, int* nsplit, float* dpq, int hid, hipStream_t st,
+                     int2* occ2_tmp) {
   const int lds = (int)std::min<int64_t>(N_max, kLdsRows) * 4;
   // more rows than one histogram: (range, slice) items over a CU-wide grid
   const int gb = N_max > kLdsRows ? kCsrRangeGrid : std::max(1, std::min(128, ceil_div(S_max * T, 2048)));
@@ -1650,12 +1691,13 @@ int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64
   PS_CHECK_LAUNCH();
   // canonical pair order (sorted by source row): bitwise-reproducible sums
   static const bool canon = !getenv("PINSAGE_CSR_CANON") || atoi(getenv("PINSAGE_CSR_CANON")) != 0;
-  if (canon) {
+  if (canon && occ2_tmp) {
     const int64_t max_chunks = dq_chunk_capacity(S_max, T, N_max);
     hipLaunchKernelGGL(csr_sort_chunks_kernel, dim3(grid_for(max_chunks * 64, 256, 2048)), dim3(256), 0, st,
                        chunks, nchunks, occ2);
     PS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(csr_sort_rows_kernel, dim3(256), dim3(1024), kSortLds * 8, st, split, nsplit, off, occ2);
+    hipLaunchKernelGGL(csr_sort_rows_kernel, dim3(256), dim3(1024), kRankLds, st, split, nsplit, off, occ2,
+                       occ2_tmp);
     PS_CHECK_LAUNCH();
   }
   return kOk;

@@ -47,7 +47,7 @@ int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_csr_build(const int32_t*, const float*, const int*, int64_t, int, const int*, int64_t, int*, int*,
-                     int*, int*, int*, int2*, int2*, int*, int2*, int*, float*, int, hipStream_t);
+                     int*, int*, int*, int2*, int2*, int*, int2*, int*, float*, int, hipStream_t, int2*);
 int64_t dq_chunk_capacity(int64_t, int, int64_t);
 int64_t dq_split_capacity(int64_t, int);
 int launch_dq_chunks(const int2*, const int*, int64_t, const int2*, const int*, int64_t, const int*,
@@ -99,7 +99,7 @@ struct LayerBuf {
   size_t wplanes = 0;  // the W weight's fragment-order bf16 planes (aggw.hip fragment form)
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
-         occ2 = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
+         occ2 = 0, occ2b = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
   size_t csrc = 0;  // chunk rows' source indices (bottom layer, Engine::dq_chunk_rows)
   int64_t max_chunks = 0, max_split = 0;
   // parameter offsets (floats) into the flat param / grad buffers
@@ -164,6 +164,9 @@ struct Engine {
     int cfg = -1, stream_k = -1, splits = 0;
   };
   std::map<std::string, GemmChoice> choice;
+  // per GEMM site: whether its last launch ran stream-K (the tuner keeps a
+  // site's summation order: pinsage_engine_site_stream_k)
+  std::map<std::string, int> sk_used;
   // pinsage_engine_set_fork: the next forward_layers call forks another
   // workspace's frontier onto `stream` right after the layer-0 Q projection
   struct Fork {
@@ -429,6 +432,7 @@ static void layout(Engine& E) {
     lb.max_chunks = dq_chunk_capacity(FS, (int)T, FN);
     lb.cbase = carve(cur, (FN + 1) * 4);
     lb.occ2 = carve(cur, lb.max_chunks * 16 * 8);  // {row, weight} pairs, 16 per chunk
+    lb.occ2b = carve(cur, lb.max_chunks * 16 * 8);  // (split rows' canonical reorder)
     lb.chunks = carve(cur, lb.max_chunks * 8);
     lb.nchunks = carve(cur, 16);
     lb.dqpart = carve(cur, lb.max_chunks * c.hid * 4);  // partials of split dq rows
@@ -569,7 +573,8 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
                             lb.N.cap, at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
                             at<int>(ws, lb.cursor), at<int>(ws, lb.cbase), at<int2>(ws, lb.occ2),
                             at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), at<int2>(ws, lb.split),
-                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, st));
+                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, st,
+                            at<int2>(ws, lb.occ2b)));
   }
   return kOk;
 }
@@ -630,6 +635,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       if (!q.b_split) with_sk(E, ws, q);
       apply_choice(E, lname("fwd.q_gemm", l), q);
       PS_TRY(launch_gemm(q, st));
+      E.sk_used[lname("fwd.q_gemm", l)] = gemm_last_stream_k();
     }
     }
     q_done = 0;
@@ -688,6 +694,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     with_sk(E, ws, w);
     apply_choice(E, lname("fwd.w_gemm", l), w);
     PS_TRY(launch_gemm(w, st));
+    E.sk_used[lname("fwd.w_gemm", l)] = gemm_last_stream_k();
   }
   // head: G2(lrelu(G1 y))
   Timed t_head(E, "fwd.head", st);
@@ -1014,6 +1021,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
       }));
       Timed td(E, lname("bwd.dcat", l), st);
       PS_TRY(launch_gemm(p, st));
+      E.sk_used[lname("bwd.dcat", l)] = gemm_last_stream_k();
     }
     PS_TRY(run_pend(E));
     if (adam && l == 0) {  // every gradient but Q0's exists on s_w; W0 was read last
@@ -1080,6 +1088,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
       apply_choice(E, lname("bwd.dh", l), p);
       Timed tdh(E, lname("bwd.dh", l), st);
       PS_TRY(launch_gemm(p, st));
+      E.sk_used[lname("bwd.dh", l)] = gemm_last_stream_k();
     }
     PS_TRY(run_pend(E));
     if (l == 0) {  // dQ0 ends the chain, on the main stream
@@ -1282,6 +1291,13 @@ int pinsage_engine_set_gemm_choice(pinsage_engine* e, const char* site, int cfg,
   if (cfg < 0 && stream_k < 0 && splits == 0) E->choice.erase(site);
   else E->choice[site] = Engine::GemmChoice{cfg, stream_k, splits};
   return kOk;
+}
+
+int pinsage_engine_site_stream_k(const pinsage_engine* e, const char* site) {
+  const Engine* E = reinterpret_cast<const Engine*>(e);
+  if (!E || !site) return -1;
+  auto it = E->sk_used.find(site);
+  return it == E->sk_used.end() ? -1 : it->second;
 }
 
 int pinsage_engine_set_layer_table(pinsage_engine* e, int64_t layer, const int32_t* nb,

@@ -111,5 +111,7 @@ int gemm_slots();
 int gemm_pick_config(int M, int N, int K, int splits);
 
 int launch_gemm(const GemmParams& p, hipStream_t st);
+// 1 if the calling thread's last launch_gemm ran stream-K, else 0
+int gemm_last_stream_k();
 
 }  // namespace ps

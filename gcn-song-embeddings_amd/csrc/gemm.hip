@@ -773,8 +773,14 @@ static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3>), g, dim3(256), 0, st, p);
 }
 
+// whether the calling thread's last launch_gemm ran stream-K (its k ranges cut
+// over blocks: a different fp32 summation order than a whole-K tile)
+static thread_local int g_last_sk = 0;
+int gemm_last_stream_k() { return g_last_sk; }
+
 int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   GemmParams p = p_in;
+  g_last_sk = 0;
   const int Mmax = p.M_dev ? p.M_max : p.M;
   const int Kmax = p.K_dev ? p.K_max : p.K;
   PS_REQUIRE(p.N > 0 && Mmax >= 0 && Kmax >= 0, kErrArg, "gemm: bad sizes");
@@ -836,6 +842,7 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
     p.sk_cnt = nullptr;
     p.sk_slab = nullptr;
   }
+  g_last_sk = sk ? 1 : 0;
   const int BMc = kCfgBM[cfg];
   const int tiles_m = (Mmax + BMc - 1) / BMc;
   int grid;

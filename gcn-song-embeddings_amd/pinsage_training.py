@@ -544,7 +544,8 @@ class _FusedStep:
 
         Reproducibility: the candidates (_GEMM_OPTS / _WGRAD_OPTS) differ only
         in the block tile, which never changes an output element's summation
-        order, so whichever wins, the step computes bitwise the same values
+        order (a site the size model runs stream-K keeps the size model's
+        schedule), so whichever wins, the step computes bitwise the same values
         (tests/test_gpu_parity.py::test_default_step_is_bitwise_reproducible).
         PINSAGE_AUTOTUNE=wide also tries stream-K and split-K counts, which
         change the order (two runs may then differ at rounding level).  The
@@ -554,6 +555,20 @@ class _FusedStep:
         e = self.runner.engine
         L = nat.lib()
         sites = self._gemm_sites()
+        if os.environ.get("PINSAGE_AUTOTUNE", "1") != "wide":
+            # a site the size model runs stream-K keeps that schedule (its cut
+            # points fix the summation order): probe the size model once, then
+            # tune tile configs only where it runs whole-K tiles
+            for site, _ in sites:
+                nat.check(L.pinsage_engine_set_gemm_choice(e.h, site.encode(), -1, -1, 0), "set_gemm_choice")
+            self._frontier(B, p)
+            st = nat.stream_ptr()
+            nat.check(L.pinsage_engine_forward_layers(e.h, nat.ptr(self.wss[p]), st), "forward_layers")
+            nat.check(L.pinsage_engine_loss(e.h, nat.ptr(self.wss[p]), B, float(self.tr.margin), 1, st), "loss")
+            nat.check(L.pinsage_engine_backward(e.h, nat.ptr(self.wss[p]), st), "backward")
+            torch.cuda.synchronize()
+            sites = [(site, [(-1, -1, 0)] if L.pinsage_engine_site_stream_k(e.h, site.encode()) == 1 else o)
+                     for site, o in sites]
         n_probe = max(len(o) for _, o in sites)
         best = {name: (float("inf"), None) for name, _ in sites}
         hold = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -458,6 +458,9 @@ int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t*
  * (relevant_nodes_per_layer, pinsage_model.py:142-154) draws every layer's
  * neighbourhoods separately.  nb = wn = null restores the engine-wide table.
  * Read when a frontier is enqueued (pinsage_engine_forward / _frontier). */
+/* Whether a GEMM site's last launch ran stream-K (1), a whole-K tile (0), or
+ * is unknown (-1): the in-context tuner keeps a site's summation order. */
+int pinsage_engine_site_stream_k(const pinsage_engine* e, const char* site);
 int pinsage_engine_set_layer_table(pinsage_engine* e, int64_t layer, const int32_t* nb,
                                    const float* wn, int64_t ld);
 /* Per-site GEMM choice (a tuner measures the sites in context and fixes them):

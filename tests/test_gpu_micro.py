@@ -128,7 +128,11 @@ def test_micro_batched_step_equals_fused_step(tmpdir_cwd, L, T, m):
     outs = [tr.train_batch(b) for tr in trs]
     torch.cuda.synchronize()
     l0, l1 = float(outs[0][0]), float(outs[1][0])
-    assert abs(l0 - l1) <= 1e-5 * abs(l1) + 1e-8, (l0, l1)
+    # the hinge terms are differences of cosines near 1: their fp32 rounding is
+    # ~1e-7 absolute (an ulp at 1) whatever the loss's size, so the floor is
+    # 1e-7 (the kernels' different row tilings of a 16-triple slice and of the
+    # whole batch round differently: 2.3e-8 apart on a 8.2e-4 loss, round 4)
+    assert abs(l0 - l1) <= 1e-5 * abs(l1) + 1e-7, (l0, l1)
     p0, p1 = dict(trs[0].model.named_parameters()), dict(trs[1].model.named_parameters())
     for k in p0:
         a, c = p0[k].grad.double().cpu().numpy(), p1[k].grad.double().cpu().numpy()

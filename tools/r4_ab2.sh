@@ -1,9 +1,9 @@
-# Round 4: the GPU suite, then A/B lines (aggregation + W form; native step host path)
+# Round 4: A/B lines (aggregation + W form; native step host path)
 set -o pipefail
 out=gpurun_out/r4ab
 mkdir -p $out
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
-tail -1 $out/tests.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_micro.py tests/test_gpu_fly.py -m gpu -q --timeout 200 --timeout-method thread > $out/tests2.log 2>&1 || { tail -40 $out/tests2.log; exit 1; }
+tail -1 $out/tests2.log
 for f in 1 0; do
   PINSAGE_AGGW_FORM=$f timeout -k 10 120 python tools/aggw_bench.py --shapes c2l0,c2l1,c4l0,c4sl0 > $out/aggw_bench_f$f.json 2>&1 || { tail $out/aggw_bench_f$f.json; exit 1; }
 done
