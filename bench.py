@@ -355,6 +355,8 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t_sample = t_enqueue = 0.0
+        fz = tr._fused
+        w0 = fz.ring_wait_s() if fz is not None else 0.0
         t0 = time.perf_counter()
         for _ in range(args.steps):
             ta = time.perf_counter()
@@ -363,6 +365,7 @@ def main():
             loss = tr.train_batch(batch)[0]
             t_sample += tb - ta
             t_enqueue += time.perf_counter() - tb
+        t_wait = (fz.ring_wait_s() - w0) if fz is not None else 0.0
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -500,7 +503,11 @@ def main():
                                     "Infinity Cache"},
         "frontier": {"U0_mean": U0, "F0_mean": F0},
         "host_ms_per_step": {"sample_batch": t_sample / args.steps * 1e3,
-                             "train_batch_enqueue": t_enqueue / args.steps * 1e3},
+                             "train_batch_enqueue": t_enqueue / args.steps * 1e3,
+                             # the enqueue's own host work: without the time blocked on
+                             # ring slots while the device is behind
+                             "train_batch_enqueue_excl_ring_wait": (t_enqueue - t_wait) / args.steps * 1e3,
+                             "native_step": bool(fz is not None and fz.stepper is not None)},
         "precompute": {"seconds": t_pre, "seconds_warm": t_pre_warm, "rng": args.precompute_rng,
                        "hops_per_s": hops / t_pre,
                        "hops_per_s_warm": hops / t_pre_warm if t_pre_warm else None,

@@ -503,7 +503,7 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
                     int epi, int splits, int cfg, int stream_k, void* stream) {
   if (M < 0 || N <= 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX ||
       (epi != kEpiStore && epi != kEpiAccum && epi != kEpiPartial) || splits < 1 || cfg < -1 ||
-      cfg > 4) {
+      cfg > 5) {
     set_error("gemm_ex: bad argument");
     return kErrArg;
   }
@@ -527,6 +527,11 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
   p.splits = splits;
   p.cfg = cfg;
   p.stream_k = stream_k;
+  if (cfg == 5 && (!gemm_ws_supported(p) || stream_k == 1 || gemm_default_prec() != 1)) {
+    set_error("gemm_ex: cfg 5 needs split-bf16 products, K-major A and B, a store epilogue, K % 32 == 0, "
+              "N % 128 == 0 and no stream-K");
+    return kErrArg;
+  }
   if (stream_k != 0) {  // library-owned stream-K scratch (tests and microbenchmarks)
     static float* slab = nullptr;
     static int* cnt = nullptr;
@@ -568,7 +573,7 @@ int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, in
                            const float* bias, int64_t N, int act, float* C, int64_t ldc, int cfg,
                            void* stream) {
   if (M < 0 || N <= 0 || K < 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX || cfg < -1 ||
-      cfg > 4) {
+      cfg > 5) {
     set_error("linear_split_b: bad argument");
     return kErrArg;
   }

@@ -1284,8 +1284,8 @@ int pinsage_engine_set_gemm_choice(pinsage_engine* e, const char* site, int cfg,
     set_error("engine_set_gemm_choice: null argument");
     return kErrArg;
   }
-  if (cfg < -1 || cfg > 3 || stream_k < -1 || stream_k > 1 || splits < 0 || splits > kMaxSplits) {
-    set_error("engine_set_gemm_choice: cfg in [-1, 3], stream_k in [-1, 1], splits in [0, 64]");
+  if (cfg < -1 || cfg > 5 || stream_k < -1 || stream_k > 1 || splits < 0 || splits > kMaxSplits) {
+    set_error("engine_set_gemm_choice: cfg in [-1, 5], stream_k in [-1, 1], splits in [0, 64]");
     return kErrArg;
   }
   if (cfg < 0 && stream_k < 0 && splits == 0) E->choice.erase(site);

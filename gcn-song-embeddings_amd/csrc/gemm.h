@@ -108,10 +108,14 @@ int gemm_slots();
 //   1:  64 x 128 x 32  (2x2 waves of 32x64)      medium M
 //   2:  32 x 128 x 32  (1x4 waves of 32x32)      small M, N = 128 (W projection)
 //   3:  64 x 128 x 16  (2x2 waves of 32x64), three workgroups per CU
+//   5:  64 x 128 x 32 warp-specialised split bf16 (K-major A and B, store
+//       epilogue; other launches run cfg 3), one 512-thread workgroup per CU
 int gemm_pick_config(int M, int N, int K, int splits);
 
 int launch_gemm(const GemmParams& p, hipStream_t st);
 // 1 if the calling thread's last launch_gemm ran stream-K, else 0
 int gemm_last_stream_k();
+// whether cfg 5 (gemm_ws_kernel) can run this launch
+bool gemm_ws_supported(const GemmParams& p);
 
 }  // namespace ps

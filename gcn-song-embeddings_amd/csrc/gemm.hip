@@ -644,6 +644,201 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   }
 }
 
+// ---------------------------------------------------------------- warp-specialised split-bf16 GEMM
+// C = act(A B^T + bias) with A [M][K] (rows gathered by a_idx) and B [N][K]
+// both K-major -- the Q projections (pinsage_model.py:196-201).  One
+// 512-thread workgroup per CU, persistent over 64 x 128 tiles.  Waves 4-7
+// (producers) load fp32 k-blocks of A and B from global memory (coalesced
+// rows, two k-blocks ahead in registers), split every element ONCE into its
+// bf16 hi / mid / lo pieces (split3's arithmetic: bitwise the in-register
+// split of gemm_f32_kernel) and write them to a 3-slot LDS ring of bf16
+// planes.  Waves 0-3 (consumers, one per SIMD beside one producer) read
+// fragments of the three planes and run only the six products per 16-k step
+// (v_mfma_f32_32x32x16_bf16, two 32x32 accumulators per wave): the
+// conversions leave the MFMA waves, each element is converted once per tile
+// instead of once per wave that reads it, and the VALU work of the producers
+// runs beside the MFMAs of the consumers on every SIMD.  Same k order and
+// product order as gemm_f32_kernel's split-bf16 path: bitwise its results.
+constexpr int kWsBM = 64, kWsBN = 128, kWsBK = 32;
+constexpr int kWsRowB = 80;                     // bytes per plane row of a slot: 64 + 16 pad (b128 reads spread banks)
+constexpr int kWsPlaneA = kWsBM * kWsRowB;      // bytes of one A plane of a slot
+constexpr int kWsPlaneB = kWsBN * kWsRowB;
+constexpr int kWsSlot = 3 * (kWsPlaneA + kWsPlaneB);  // 46080 bytes
+constexpr int kWsSlots = 3;
+constexpr int kWsRows = kWsBM + kWsBN;           // 192 rows of 32 k per k-block
+constexpr int kWsPer = kWsRows * (kWsBK / 4) / 256;  // float4 per producer lane per k-block (6)
+
+__device__ __forceinline__ void ws_split4(const float4& v, uint2& H, uint2& M, uint2& L) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split_pair(f32x2{v.x, v.y}, h0, m0, l0);
+  split_pair(f32x2{v.z, v.w}, h1, m1, l1);
+  H = make_uint2(h0, h1);
+  M = make_uint2(m0, m1);
+  L = make_uint2(l0, l1);
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_ws_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = p.M_dev ? *p.M_dev : p.M;
+  const int N = p.N, K = p.K;
+  const int tiles_m = (M + kWsBM - 1) / kWsBM, tiles_n = N / kWsBN;
+  const int nkb = K / kWsBK;
+  const bool producer = wave >= 4;
+  // tiles of one row panel go to blocks b, b + 8, ... (one XCD: they share
+  // the panel's A rows in its L2; speed only)
+  const int G = tiles_m, W = tiles_n;
+  const int iters = 8 * ((G + 7) / 8) * W;
+  for (int t = blockIdx.x; t < iters; t += gridDim.x) {
+    const int xcd = t & 7, s = t >> 3;
+    const int tm = (s / W) * 8 + xcd, tn = s % W;
+    if (tm >= G) continue;
+    const int m0 = tm * kWsBM, n0 = tn * kWsBN;
+    if (producer) {
+      // lane pl (0..255) owns float4 q = pl + 256 j of the 192 x 8 k-block grid
+      const int pl = tid - 256;
+      const float* src[kWsPer];
+      int dst[kWsPer];  // byte offset inside a slot, plane 0
+#pragma unroll
+      for (int j = 0; j < kWsPer; ++j) {
+        const int q = pl + 256 * j, r = q >> 3, c4 = q & 7;
+        if (r < kWsBM) {
+          const int g = min(m0 + r, M - 1);
+          src[j] = p.a + (int64_t)(p.a_idx ? p.a_idx[g] : g) * p.lda + 4 * c4;
+          dst[j] = r * kWsRowB + c4 * 8;
+        } else {
+          const int rb = r - kWsBM;
+          src[j] = p.b + (int64_t)(n0 + rb) * p.ldb + 4 * c4;
+          dst[j] = 3 * kWsPlaneA + rb * kWsRowB + c4 * 8;
+        }
+      }
+      float4 cur[kWsPer], nxt[kWsPer];
+#pragma unroll
+      for (int j = 0; j < kWsPer; ++j) cur[j] = *reinterpret_cast<const float4*>(src[j]);
+      if (nkb > 1) {
+#pragma unroll
+        for (int j = 0; j < kWsPer; ++j) nxt[j] = *reinterpret_cast<const float4*>(src[j] + kWsBK);
+      }
+      auto put = [&](int kb, const float4 (&v)[kWsPer]) __attribute__((always_inline)) {
+        unsigned char* slot = ws_lds + (kb % kWsSlots) * kWsSlot;
+#pragma unroll
+        for (int j = 0; j < kWsPer; ++j) {
+          uint2 H, Mi, L;
+          ws_split4(v[j], H, Mi, L);
+          const int plane = dst[j] < 3 * kWsPlaneA ? kWsPlaneA : kWsPlaneB;
+          *reinterpret_cast<uint2*>(slot + dst[j]) = H;
+          *reinterpret_cast<uint2*>(slot + dst[j] + plane) = Mi;
+          *reinterpret_cast<uint2*>(slot + dst[j] + 2 * plane) = L;
+        }
+      };
+      // prologue: k-blocks 0 and 1 into slots 0 and 1
+      put(0, cur);
+      if (nkb > 1) {
+        put(1, nxt);
+        if (nkb > 2) {
+#pragma unroll
+          for (int j = 0; j < kWsPer; ++j) cur[j] = *reinterpret_cast<const float4*>(src[j] + 2 * kWsBK);
+        }
+      }
+      __syncthreads();
+      for (int kb = 0; kb < nkb; ++kb) {
+        // consumers read slot kb % 3; k-block kb + 2 goes to slot (kb + 2) % 3
+        // (read at iteration kb - 1, released by the barrier below it)
+        if (kb + 2 < nkb) {
+          if (kb + 3 < nkb) {
+#pragma unroll
+            for (int j = 0; j < kWsPer; ++j) nxt[j] = *reinterpret_cast<const float4*>(src[j] + (kb + 3) * kWsBK);
+          }
+          put(kb + 2, cur);
+#pragma unroll
+          for (int j = 0; j < kWsPer; ++j) cur[j] = nxt[j];
+        }
+        __syncthreads();
+      }
+      __syncthreads();  // the consumers' epilogue (no LDS) -- keep the barrier count equal
+    } else {
+      const int wm = wave >> 1, wn = wave & 1;
+      const int l32 = lane & 31, kh = lane >> 5;
+      f32x16 acc[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      const int arow = (wm * 32 + l32) * kWsRowB + 16 * kh;
+      const int brow0 = 3 * kWsPlaneA + (wn * 64 + l32) * kWsRowB + 16 * kh;
+      const int brow1 = brow0 + 32 * kWsRowB;
+      __syncthreads();  // the prologue's slots
+      for (int kb = 0; kb < nkb; ++kb) {
+        const unsigned char* slot = ws_lds + (kb % kWsSlots) * kWsSlot;
+#pragma unroll
+        for (int st = 0; st < kWsBK / 16; ++st) {
+          const int ko = 32 * st;  // bytes: 16 k of bf16
+          const bf16x8 aH = *reinterpret_cast<const bf16x8*>(slot + arow + ko);
+          const bf16x8 aM = *reinterpret_cast<const bf16x8*>(slot + arow + ko + kWsPlaneA);
+          const bf16x8 aL = *reinterpret_cast<const bf16x8*>(slot + arow + ko + 2 * kWsPlaneA);
+          bf16x8 bH[2], bM[2], bL[2];
+          bH[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko);
+          bM[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko + kWsPlaneB);
+          bL[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko + 2 * kWsPlaneB);
+          bH[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko);
+          bM[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko + kWsPlaneB);
+          bL[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko + 2 * kWsPlaneB);
+#define PS_WS2(X, Y)                                                                   \
+  acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, Y[0], acc[0], 0, 0, 0);          \
+  acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, Y[1], acc[1], 0, 0, 0);
+          PS_WS2(aL, bH)
+          PS_WS2(aH, bL)
+          PS_WS2(aM, bM)
+          PS_WS2(aM, bH)
+          PS_WS2(aH, bM)
+          PS_WS2(aH, bH)
+#undef PS_WS2
+        }
+        __syncthreads();  // slot kb % 3 is free for k-block kb + 3
+      }
+      // epilogue: bias (+ LeakyReLU) and the stores, straight from registers
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + 32 * j + l32;
+        const float bj = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+          if (row < M) {
+            float v = acc[j][r] + bj;
+            if (p.act) v = lrelu(v);
+            p.c[(int64_t)row * p.ldc + col] = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+bool gemm_ws_supported(const GemmParams& p) {
+  return p.a_kmajor && p.b_kmajor && p.K1 < 0 && !p.a2 && !p.c_idx && !p.c2 && !p.mask && !p.b_split &&
+         p.epi == kEpiStore && !p.K_dev && p.K > 0 && p.K % kWsBK == 0 && p.N % kWsBN == 0 && p.lda % 4 == 0 &&
+         p.ldb % 4 == 0;
+}
+
+static int launch_gemm_ws(const GemmParams& p, int Mmax, hipStream_t st) {
+  static bool prepared = false;
+  if (!prepared) {
+    PS_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kWsSlots * kWsSlot));
+    prepared = true;
+  }
+  const int tiles = ((Mmax + kWsBM - 1) / kWsBM) * (p.N / kWsBN);
+  const int slots = gemm_slots() / 2;  // one workgroup per CU
+  const int iters = 8 * ((((Mmax + kWsBM - 1) / kWsBM) + 7) / 8) * (p.N / kWsBN);
+  int grid = std::min(std::max(tiles, 1), slots);
+  grid = std::min(grid, iters);
+  hipLaunchKernelGGL(gemm_ws_kernel, dim3(grid), dim3(512), kWsSlots * kWsSlot, st, p);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 constexpr int kCfgBM[5] = {128, 64, 32, 64, 64};
 
 // the product arithmetic of GEMMs that do not choose (GemmParams::prec < 0):
@@ -805,6 +1000,14 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
   PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
              "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
+  if (p.cfg == 5) {  // the warp-specialised split-bf16 kernel (K-major A and B, store epilogue)
+    if (gemm_ws_supported(p) && (p.prec == 1 || (p.prec < 0 && gemm_default_prec() == 1))) {
+      g_last_sk = 0;
+      return launch_gemm_ws(p, Mmax, st);
+    }
+    p.cfg = 3;  // a launch it cannot run: the same products and k order on cfg 3's tiles
+    p.stream_k = 0;
+  }
   PS_REQUIRE(!p.b_split || (p.b_kmajor && p.ldb_split % 8 == 0 && p.ldb_split >= Kmax &&
                             (p.K_dev || p.K % 8 == 0) && (uintptr_t)p.b_split % 16 == 0),
              kErrArg, "gemm: pre-split B needs K-major B, K and ldb_split multiples of 8, 16-B aligned planes");

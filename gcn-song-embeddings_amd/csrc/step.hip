@@ -10,6 +10,7 @@
 #include "../../include/pinsage_hip.h"
 #include "common.h"
 
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -105,6 +106,7 @@ struct Stepper {
   std::vector<int64_t> pending[2];  // ids whose frontier sits in workspace p (empty: none)
   int parity = 0;
   int64_t nstep = 0, hits = 0;
+  int64_t wait_ns = 0;  // host time blocked on ring slots (the GPU is behind)
 };
 
 }  // extern "C"
@@ -156,6 +158,11 @@ void pinsage_stepper_destroy(pinsage_stepper* h) {
   delete s;
 }
 
+int64_t pinsage_stepper_wait_ns(const pinsage_stepper* h) {
+  const auto* s = reinterpret_cast<const Stepper*>(h);
+  return s ? s->wait_ns : -1;
+}
+
 int pinsage_stepper_set_graphs(pinsage_stepper* h, int p, void* gf, void* gm, void* ga) {
   auto* s = reinterpret_cast<Stepper*>(h);
   if (!s || (p != 0 && p != 1) || !gf || !gm) {
@@ -195,7 +202,11 @@ int pinsage_stepper_step(pinsage_stepper* h, const int64_t* batch, int64_t n_ids
   }
   hipStream_t st = (hipStream_t)stream;
   const int64_t k = s->nstep % s->R;
-  if (s->ev_live[(size_t)k]) PS_CHECK_HIP(hipEventSynchronize(s->ev[(size_t)k]));  // the slot's last user is done
+  if (s->ev_live[(size_t)k]) {  // the slot's last user is done
+    const auto t0 = std::chrono::steady_clock::now();
+    PS_CHECK_HIP(hipEventSynchronize(s->ev[(size_t)k]));
+    s->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  }
   uint8_t* slot = s->ring + k * s->slot_bytes;
   std::memcpy(slot + s->off_coef, coef, 8);
   const bool hit = (int64_t)s->pending[p].size() == n_ids &&

@@ -314,6 +314,16 @@ class _FusedStep:
         # (deterministic: the same choices, so the same summation orders, on every run)
         self.autotune = os.environ.get("PINSAGE_AUTOTUNE", "1") != "0"
         self.tuned_choices = None
+        self.wait_s = 0.0  # host seconds blocked on ring slots (Python path)
+        self.stepper = None
+
+    def ring_wait_s(self):
+        """Host seconds the steps spent blocked on ring slots, i.e. waiting for
+        the device (both host paths)."""
+        w = self.wait_s
+        if self.stepper is not None:
+            w += nat.lib().pinsage_stepper_wait_ns(self.stepper) * 1e-9
+        return w
 
     def ensure(self, B):
         r = self.runner
@@ -511,7 +521,7 @@ class _FusedStep:
     # stream-K stays off under the tuner and split counts stay the size model's
     # (splits 0).  PINSAGE_AUTOTUNE=wide also tries those (timing-picked, so
     # two runs may then differ at rounding level).
-    _GEMM_OPTS = [(c, 0, 0) for c in (0, 1, 2, 3)]
+    _GEMM_OPTS = [(c, 0, 0) for c in (0, 1, 2, 3, 5)]
     _WGRAD_OPTS = [(c, -1, 0) for c in (0, 1, 2)]
     _GEMM_OPTS_WIDE = [(c, k, 0) for c in (0, 1, 2, 3) for k in (0, 1) if not (c == 0 and k == 1)]
     _WGRAD_OPTS_WIDE = [(c, -1, sp) for c in (0, 1, 2) for sp in (2, 4, 8, 16, 32, 64)]
@@ -765,6 +775,7 @@ class _FusedStep:
             return
         if sync:  # its ring slots may still be read by launched steps
             torch.cuda.current_stream().synchronize()
+        self.wait_s += nat.lib().pinsage_stepper_wait_ns(st) * 1e-9
         nat.lib().pinsage_stepper_destroy(st)
         self.stepper = None
 
@@ -852,7 +863,9 @@ class _FusedStep:
         _tick("pre")
         k = self.nstep % self.HOST_RING
         if self.ring_ev[k] is not None:  # the step that used this slot is done
+            tw = time.perf_counter()
             self.ring_ev[k].synchronize()
+            self.wait_s += time.perf_counter() - tw
         self._slot_write_coef(k)
         _tick("slot_wait")
         staged = self.dist and self.dp_buckets

@@ -297,6 +297,8 @@ int pinsage_stepper_create(void* ring, int64_t R, int64_t slot_bytes, int64_t of
                            int64_t off_coef, int64_t max_ids, int64_t n_items, pinsage_stepper** out);
 void pinsage_stepper_destroy(pinsage_stepper* s);
 int pinsage_stepper_set_graphs(pinsage_stepper* s, int p, void* gf, void* gm, void* ga);
+/* host nanoseconds spent blocked on ring slots so far (the device behind the host) */
+int64_t pinsage_stepper_wait_ns(const pinsage_stepper* s);
 /* resume from the trainer's eager path: next parity, step counter, no pending frontier */
 int pinsage_stepper_sync_state(pinsage_stepper* s, int parity, int64_t nstep);
 int pinsage_stepper_step(pinsage_stepper* s, const int64_t* batch, int64_t n_ids, const float* coef,

@@ -294,3 +294,39 @@ def test_presplit_b_argument_checks():
     C = torch.empty(16, 128, device="cuda")
     assert lib.pinsage_linear_split_b(_vp(A), 12, None, 16, 12, _vp(W), _vp(planes), 12, None, 128, 0,
                                       _vp(C), 128, 3, stream) != 0  # K % 8
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 32), (63, 128, 128), (1000, 256, 512), (10541, 512, 512),
+                                   (3000, 512, 128), (700, 128, 1024)])
+def test_warp_specialised_gemm_is_bitwise_cfg3(M, N, K):
+    """cfg 5 (gemm_ws_kernel: producer waves split each element once into LDS
+    bf16 planes, consumer waves run the products) computes the same products
+    in the same k order as the split-bf16 tiles: bitwise cfg 3's output, for
+    gathered rows with the Q projection's bias + LeakyReLU epilogue, within
+    1e-4 of float64."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    pool = M + 37
+    A = torch.randn(pool, K, device="cuda", generator=g)
+    a_idx = torch.randperm(pool, device="cuda", generator=g)[:M].to(torch.int32)
+    B = torch.randn(N, K, device="cuda", generator=g) * 0.05
+    bias = torch.randn(N, device="cuda", generator=g)
+    out = []
+    for cfg in (5, 3):
+        C = torch.full((M, N), float("nan"), device="cuda")
+        _gemm(M, N, K, 1, 1, A, a_idx, B, C, bias=bias, act=1, cfg=cfg)
+        torch.cuda.synchronize()
+        out.append(C)
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1])
+    assert _rel(out[0], _ref(M, N, K, 1, 1, A, a_idx, B, bias, 1)) < REL_TOL
+
+
+def test_warp_specialised_gemm_argument_checks():
+    A = torch.randn(64, 96, device="cuda")
+    C = torch.empty(64, 128, device="cuda")
+    B = torch.randn(128, 96, device="cuda")
+    for args in [dict(K=80), dict(ak=0), dict(N=64)]:  # K % 32, M-major A, N % 128
+        K = args.get("K", 64)
+        N = args.get("N", 128)
+        with pytest.raises(RuntimeError, match="cfg 5"):
+            _gemm(64, N, K, args.get("ak", 1), 1, A, None, B, C, cfg=5)
