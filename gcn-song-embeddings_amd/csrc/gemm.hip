@@ -659,14 +659,17 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
 // instead of once per wave that reads it, and the VALU work of the producers
 // runs beside the MFMAs of the consumers on every SIMD.  Same k order and
 // product order as gemm_f32_kernel's split-bf16 path: bitwise its results.
-constexpr int kWsBM = 64, kWsBN = 128, kWsBK = 32;
-constexpr int kWsRowB = 80;                     // bytes per plane row of a slot: 64 + 16 pad (b128 reads spread banks)
-constexpr int kWsPlaneA = kWsBM * kWsRowB;      // bytes of one A plane of a slot
-constexpr int kWsPlaneB = kWsBN * kWsRowB;
-constexpr int kWsSlot = 3 * (kWsPlaneA + kWsPlaneB);  // 46080 bytes
+constexpr int kWsBM = 64, kWsBN = 128;
+constexpr int kWsRows = kWsBM + kWsBN;  // 192 rows of a k-block
+
+template <int BK>
+struct WsGeom {
+  static constexpr int RowB = BK * 2 + 16;            // bytes per plane row of a slot (+16: b128 reads spread banks)
+  static constexpr int PlaneA = kWsBM * RowB, PlaneB = kWsBN * RowB;
+  static constexpr int Slot = 3 * (PlaneA + PlaneB);
+  static constexpr int Per = kWsRows * (BK / 4) / 256;  // float4 per producer lane per k-block
+};
 constexpr int kWsSlots = 3;
-constexpr int kWsRows = kWsBM + kWsBN;           // 192 rows of 32 k per k-block
-constexpr int kWsPer = kWsRows * (kWsBK / 4) / 256;  // float4 per producer lane per k-block (6)
 
 __device__ __forceinline__ void ws_split4(const float4& v, uint2& H, uint2& M, uint2& L) {
   unsigned h0, m0, l0, h1, m1, l1;
@@ -677,13 +680,18 @@ __device__ __forceinline__ void ws_split4(const float4& v, uint2& H, uint2& M, u
   L = make_uint2(l0, l1);
 }
 
-__global__ __launch_bounds__(512, 1) void gemm_ws_kernel(GemmParams p) {
+// BK: k per slot; AHEAD: k-blocks a producer lane holds loaded ahead of the
+// one it writes (global latency cover); WPC: workgroups per CU
+template <int BK, int AHEAD, int WPC>
+__global__ __launch_bounds__(512, 2 * WPC) void gemm_ws_kernel(GemmParams p) {
+  using Gm = WsGeom<BK>;
+  constexpr int PER = Gm::Per;
   extern __shared__ __attribute__((aligned(16))) unsigned char ws_lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = p.M_dev ? *p.M_dev : p.M;
   const int N = p.N, K = p.K;
   const int tiles_m = (M + kWsBM - 1) / kWsBM, tiles_n = N / kWsBN;
-  const int nkb = K / kWsBK;
+  const int nkb = K / BK;
   const bool producer = wave >= 4;
   // tiles of one row panel go to blocks b, b + 8, ... (one XCD: they share
   // the panel's A rows in its L2; speed only)
@@ -695,67 +703,69 @@ __global__ __launch_bounds__(512, 1) void gemm_ws_kernel(GemmParams p) {
     if (tm >= G) continue;
     const int m0 = tm * kWsBM, n0 = tn * kWsBN;
     if (producer) {
-      // lane pl (0..255) owns float4 q = pl + 256 j of the 192 x 8 k-block grid
+      // lane pl (0..255) owns float4 q = pl + 256 j of the 192 x (BK / 4) grid
       const int pl = tid - 256;
-      const float* src[kWsPer];
-      int dst[kWsPer];  // byte offset inside a slot, plane 0
+      const float* src[PER];
+      int dst[PER];  // byte offset inside a slot, plane 0
 #pragma unroll
-      for (int j = 0; j < kWsPer; ++j) {
-        const int q = pl + 256 * j, r = q >> 3, c4 = q & 7;
+      for (int j = 0; j < PER; ++j) {
+        const int q = pl + 256 * j, r = q / (BK / 4), c4 = q % (BK / 4);
         if (r < kWsBM) {
           const int g = min(m0 + r, M - 1);
           src[j] = p.a + (int64_t)(p.a_idx ? p.a_idx[g] : g) * p.lda + 4 * c4;
-          dst[j] = r * kWsRowB + c4 * 8;
+          dst[j] = r * Gm::RowB + c4 * 8;
         } else {
           const int rb = r - kWsBM;
           src[j] = p.b + (int64_t)(n0 + rb) * p.ldb + 4 * c4;
-          dst[j] = 3 * kWsPlaneA + rb * kWsRowB + c4 * 8;
+          dst[j] = 3 * Gm::PlaneA + rb * Gm::RowB + c4 * 8;
         }
       }
-      float4 cur[kWsPer], nxt[kWsPer];
+      auto load = [&](int kb, float4 (&v)[PER]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int j = 0; j < kWsPer; ++j) cur[j] = *reinterpret_cast<const float4*>(src[j]);
-      if (nkb > 1) {
+        for (int j = 0; j < PER; ++j) v[j] = *reinterpret_cast<const float4*>(src[j] + kb * BK);
+      };
+      auto put = [&](int kb, const float4 (&v)[PER]) __attribute__((always_inline)) {
+        unsigned char* slot = ws_lds + (kb % kWsSlots) * Gm::Slot;
 #pragma unroll
-        for (int j = 0; j < kWsPer; ++j) nxt[j] = *reinterpret_cast<const float4*>(src[j] + kWsBK);
-      }
-      auto put = [&](int kb, const float4 (&v)[kWsPer]) __attribute__((always_inline)) {
-        unsigned char* slot = ws_lds + (kb % kWsSlots) * kWsSlot;
-#pragma unroll
-        for (int j = 0; j < kWsPer; ++j) {
+        for (int j = 0; j < PER; ++j) {
           uint2 H, Mi, L;
           ws_split4(v[j], H, Mi, L);
-          const int plane = dst[j] < 3 * kWsPlaneA ? kWsPlaneA : kWsPlaneB;
+          const int plane = dst[j] < 3 * Gm::PlaneA ? Gm::PlaneA : Gm::PlaneB;
           *reinterpret_cast<uint2*>(slot + dst[j]) = H;
           *reinterpret_cast<uint2*>(slot + dst[j] + plane) = Mi;
           *reinterpret_cast<uint2*>(slot + dst[j] + 2 * plane) = L;
         }
       };
-      // prologue: k-blocks 0 and 1 into slots 0 and 1
-      put(0, cur);
-      if (nkb > 1) {
-        put(1, nxt);
-        if (nkb > 2) {
+      // prologue: k-blocks 0 and 1 into slots 0 and 1; v[r] <- k-block 2 + r
+      float4 v[AHEAD][PER];
+      {
+        float4 a0[PER], a1[PER];
+        load(0, a0);
+        if (nkb > 1) load(1, a1);
 #pragma unroll
-          for (int j = 0; j < kWsPer; ++j) cur[j] = *reinterpret_cast<const float4*>(src[j] + 2 * kWsBK);
-        }
+        for (int r = 0; r < AHEAD; ++r)
+          if (2 + r < nkb) load(2 + r, v[r]);
+        put(0, a0);
+        if (nkb > 1) put(1, a1);
       }
       __syncthreads();
-      for (int kb = 0; kb < nkb; ++kb) {
-        // consumers read slot kb % 3; k-block kb + 2 goes to slot (kb + 2) % 3
-        // (read at iteration kb - 1, released by the barrier below it)
-        if (kb + 2 < nkb) {
-          if (kb + 3 < nkb) {
+      // iteration kb (consumers on slot kb % 3): k-block kb + 2 (in v[kb %
+      // AHEAD]) goes to slot (kb + 2) % 3, which iteration kb - 1 read; then
+      // that register set loads k-block kb + 2 + AHEAD
+      for (int kb0 = 0; kb0 < nkb; kb0 += AHEAD) {
 #pragma unroll
-            for (int j = 0; j < kWsPer; ++j) nxt[j] = *reinterpret_cast<const float4*>(src[j] + (kb + 3) * kWsBK);
+        for (int r = 0; r < AHEAD; ++r) {
+          const int kb = kb0 + r;
+          if (kb < nkb) {
+            if (kb + 2 < nkb) {
+              put(kb + 2, v[r]);
+              if (kb + 2 + AHEAD < nkb) load(kb + 2 + AHEAD, v[r]);
+            }
+            __syncthreads();
           }
-          put(kb + 2, cur);
-#pragma unroll
-          for (int j = 0; j < kWsPer; ++j) cur[j] = nxt[j];
         }
-        __syncthreads();
       }
-      __syncthreads();  // the consumers' epilogue (no LDS) -- keep the barrier count equal
+      __syncthreads();  // (the consumers' epilogue barrier)
     } else {
       const int wm = wave >> 1, wn = wave & 1;
       const int l32 = lane & 31, kh = lane >> 5;
@@ -764,25 +774,25 @@ __global__ __launch_bounds__(512, 1) void gemm_ws_kernel(GemmParams p) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-      const int arow = (wm * 32 + l32) * kWsRowB + 16 * kh;
-      const int brow0 = 3 * kWsPlaneA + (wn * 64 + l32) * kWsRowB + 16 * kh;
-      const int brow1 = brow0 + 32 * kWsRowB;
+      const int arow = (wm * 32 + l32) * Gm::RowB + 16 * kh;
+      const int brow0 = 3 * Gm::PlaneA + (wn * 64 + l32) * Gm::RowB + 16 * kh;
+      const int brow1 = brow0 + 32 * Gm::RowB;
       __syncthreads();  // the prologue's slots
       for (int kb = 0; kb < nkb; ++kb) {
-        const unsigned char* slot = ws_lds + (kb % kWsSlots) * kWsSlot;
+        const unsigned char* slot = ws_lds + (kb % kWsSlots) * Gm::Slot;
 #pragma unroll
-        for (int st = 0; st < kWsBK / 16; ++st) {
+        for (int st = 0; st < BK / 16; ++st) {
           const int ko = 32 * st;  // bytes: 16 k of bf16
           const bf16x8 aH = *reinterpret_cast<const bf16x8*>(slot + arow + ko);
-          const bf16x8 aM = *reinterpret_cast<const bf16x8*>(slot + arow + ko + kWsPlaneA);
-          const bf16x8 aL = *reinterpret_cast<const bf16x8*>(slot + arow + ko + 2 * kWsPlaneA);
+          const bf16x8 aM = *reinterpret_cast<const bf16x8*>(slot + arow + ko + Gm::PlaneA);
+          const bf16x8 aL = *reinterpret_cast<const bf16x8*>(slot + arow + ko + 2 * Gm::PlaneA);
           bf16x8 bH[2], bM[2], bL[2];
           bH[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko);
-          bM[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko + kWsPlaneB);
-          bL[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko + 2 * kWsPlaneB);
+          bM[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko + Gm::PlaneB);
+          bL[0] = *reinterpret_cast<const bf16x8*>(slot + brow0 + ko + 2 * Gm::PlaneB);
           bH[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko);
-          bM[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko + kWsPlaneB);
-          bL[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko + 2 * kWsPlaneB);
+          bM[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko + Gm::PlaneB);
+          bL[1] = *reinterpret_cast<const bf16x8*>(slot + brow1 + ko + 2 * Gm::PlaneB);
 #define PS_WS2(X, Y)                                                                   \
   acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, Y[0], acc[0], 0, 0, 0);          \
   acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, Y[1], acc[1], 0, 0, 0);
@@ -818,25 +828,36 @@ __global__ __launch_bounds__(512, 1) void gemm_ws_kernel(GemmParams p) {
 
 bool gemm_ws_supported(const GemmParams& p) {
   return p.a_kmajor && p.b_kmajor && p.K1 < 0 && !p.a2 && !p.c_idx && !p.c2 && !p.mask && !p.b_split &&
-         p.epi == kEpiStore && !p.K_dev && p.K > 0 && p.K % kWsBK == 0 && p.N % kWsBN == 0 && p.lda % 4 == 0 &&
+         p.epi == kEpiStore && !p.K_dev && p.K > 0 && p.K % 32 == 0 && p.N % kWsBN == 0 && p.lda % 4 == 0 &&
          p.ldb % 4 == 0;
 }
 
-static int launch_gemm_ws(const GemmParams& p, int Mmax, hipStream_t st) {
+// PINSAGE_WS_VARIANT (A/B): 0 = 32-k slots, 3 k-blocks ahead, one workgroup
+// per CU (default); 1 = 16-k slots, 2 ahead, two per CU; 2 = 32-k slots, 1 ahead
+template <int BK, int AHEAD, int WPC>
+static int launch_ws_variant(const GemmParams& p, int Mmax, hipStream_t st) {
   static bool prepared = false;
+  const int lds = kWsSlots * WsGeom<BK>::Slot;
   if (!prepared) {
-    PS_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kWsSlots * kWsSlot));
+    PS_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<BK, AHEAD, WPC>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     prepared = true;
   }
-  const int tiles = ((Mmax + kWsBM - 1) / kWsBM) * (p.N / kWsBN);
-  const int slots = gemm_slots() / 2;  // one workgroup per CU
-  const int iters = 8 * ((((Mmax + kWsBM - 1) / kWsBM) + 7) / 8) * (p.N / kWsBN);
-  int grid = std::min(std::max(tiles, 1), slots);
+  const int tm = (Mmax + kWsBM - 1) / kWsBM;
+  const int tiles = tm * (p.N / kWsBN);
+  const int iters = 8 * ((tm + 7) / 8) * (p.N / kWsBN);
+  int grid = std::min(std::max(tiles, 1), WPC * gemm_slots() / 2);
   grid = std::min(grid, iters);
-  hipLaunchKernelGGL(gemm_ws_kernel, dim3(grid), dim3(512), kWsSlots * kWsSlot, st, p);
+  hipLaunchKernelGGL((gemm_ws_kernel<BK, AHEAD, WPC>), dim3(grid), dim3(512), lds, st, p);
   PS_CHECK_LAUNCH();
   return kOk;
+}
+
+static int launch_gemm_ws(const GemmParams& p, int Mmax, hipStream_t st) {
+  static const int variant = getenv("PINSAGE_WS_VARIANT") ? atoi(getenv("PINSAGE_WS_VARIANT")) : 0;
+  if (variant == 1) return launch_ws_variant<16, 2, 2>(p, Mmax, st);
+  if (variant == 2) return launch_ws_variant<32, 1, 1>(p, Mmax, st);
+  return launch_ws_variant<32, 3, 1>(p, Mmax, st);
 }
 
 constexpr int kCfgBM[5] = {128, 64, 32, 64, 64};
