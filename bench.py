@@ -357,6 +357,7 @@ def main():
         t_sample = t_enqueue = 0.0
         fz = tr._fused
         w0 = fz.ring_wait_s() if fz is not None else 0.0
+        st0 = fz.stepper_stats() if fz is not None and fz.stepper is not None else None
         t0 = time.perf_counter()
         for _ in range(args.steps):
             ta = time.perf_counter()
@@ -366,6 +367,8 @@ def main():
             t_sample += tb - ta
             t_enqueue += time.perf_counter() - tb
         t_wait = (fz.ring_wait_s() - w0) if fz is not None else 0.0
+        native_step = bool(fz is not None and fz.stepper is not None)
+        st_stats = fz.stepper_stats() if native_step else None
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -507,7 +510,12 @@ def main():
                              # the enqueue's own host work: without the time blocked on
                              # ring slots while the device is behind
                              "train_batch_enqueue_excl_ring_wait": (t_enqueue - t_wait) / args.steps * 1e3,
-                             "native_step": bool(fz is not None and fz.stepper is not None)},
+                             "native_step": native_step,
+                             # inside the native step call (pinsage_stepper_stats): all of
+                             # it, and the graph launches alone
+                             **({"native_call": (st_stats["call_ns"] - st0["call_ns"]) / args.steps * 1e-6,
+                                 "graph_launch": (st_stats["launch_ns"] - st0["launch_ns"]) / args.steps * 1e-6}
+                                if st_stats is not None and st0 is not None else {})},
         "precompute": {"seconds": t_pre, "seconds_warm": t_pre_warm, "rng": args.precompute_rng,
                        "hops_per_s": hops / t_pre,
                        "hops_per_s_warm": hops / t_pre_warm if t_pre_warm else None,

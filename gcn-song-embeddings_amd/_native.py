@@ -97,6 +97,7 @@ _SIGS = {
     "pinsage_stepper_create": (ctypes.c_int, [vp, i64, i64, i64, i64, i64, i64, i64, vp]),
     "pinsage_stepper_destroy": (None, [vp]),
     "pinsage_stepper_wait_ns": (i64, [vp]),
+    "pinsage_stepper_stats": (ctypes.c_int, [vp, vp, ctypes.c_int]),
     "pinsage_stepper_set_graphs": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp]),
     "pinsage_stepper_sync_state": (ctypes.c_int, [vp, ctypes.c_int, i64]),
     "pinsage_stepper_step": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, vp]),

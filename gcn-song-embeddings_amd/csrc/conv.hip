@@ -323,9 +323,11 @@ __device__ __forceinline__ void scan_emit(int* __restrict__ cnt, int64_t i0, int
       cbase[i] = pc;
       cnt[i] = 0;
       const int nc = n_chunks(v);
-      // chunk = {row, occurrences (<= kDqChunk) | kDqSplit if the row spans several chunks}
-      for (int j = 0; j < nc; ++j)
-        chunks[pc + j] = make_int2((int)i, min(kDqChunk, v - j * kDqChunk) | (nc > 1 ? kDqSplit : 0));
+      // chunk = {row, occurrences (<= kDqChunk) | kDqSplit if the row spans
+      // several chunks}; a split row's chunks are written by csr_fill_kernel's
+      // blocks in parallel (one thread here would write thousands for a
+      // popular row)
+      if (nc == 1) chunks[pc] = make_int2((int)i, v);
       if (nc > 1) split[atomicAdd(nsplit, 1)] = make_int2((int)i, pc);  // order is irrelevant
       p += v;
       pc += nc;
@@ -473,10 +475,21 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
                                                         int* __restrict__ cursor,
                                                         const int* __restrict__ off,
                                                         const int* __restrict__ cbase,
-                                                        int2* __restrict__ occ2, int max_ranges) {
+                                                        int2* __restrict__ occ2, int max_ranges,
+                                                        const int2* __restrict__ split,
+                                                        const int* __restrict__ nsplit,
+                                                        int2* __restrict__ chunks) {
   extern __shared__ int hist[];
   const int64_t n = (int64_t)(*nS) * T;
   const int U = *nN;
+  // the chunk descriptors of the rows split over several chunks (the scan's split list)
+  const int ns = *nsplit;
+  for (int si = blockIdx.x; si < ns; si += gridDim.x) {
+    const int2 sp = split[si];
+    const int v = off[sp.x + 1] - off[sp.x], nc = n_chunks(v);
+    for (int j = threadIdx.x; j < nc; j += blockDim.x)
+      chunks[sp.y + j] = make_int2(sp.x, min(kDqChunk, v - j * kDqChunk) | kDqSplit);
+  }
   if (U <= kLdsRows) {
     for (int u = threadIdx.x; u < U; u += blockDim.x) hist[u] = 0;
     __syncthreads();
@@ -556,9 +569,14 @@ __global__ __launch_bounds__(1024) void csr_fill_kernel(const int32_t* __restric
 // stream right behind the fill, off the step's critical chain.
 //
 // Rows of one chunk (<= kDqChunk pairs): one wave per chunk, a bitonic network
-// over its 16 lanes (shuffles); empty lanes carry INT_MAX keys.
+// over its 16 lanes (shuffles); empty lanes carry INT_MAX keys.  A row split
+// over 2..4 chunks (<= 64 pairs, contiguous from its first chunk) is sorted by
+// the wave of its first chunk: every lane holds one pair and its place is the
+// number of the row's pairs with a smaller source row.
+constexpr int kSortWaveRow = 64;
 __global__ __launch_bounds__(256) void csr_sort_chunks_kernel(const int2* __restrict__ chunks,
                                                               const int* __restrict__ nchunks,
+                                                              const int* __restrict__ off,
                                                               int2* __restrict__ occ2) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -566,7 +584,18 @@ __global__ __launch_bounds__(256) void csr_sort_chunks_kernel(const int2* __rest
   for (int64_t ci = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; ci < nch; ci += nw) {
     const int2 dsc = chunks[ci];
     const int n = dsc.y & 0xff;
-    if ((dsc.y & kDqSplit) || n < 2) continue;  // (split rows: csr_sort_rows_kernel)
+    if (dsc.y & kDqSplit) {
+      if (ci > 0 && chunks[ci - 1].x == dsc.x) continue;  // (not the row's first chunk)
+      const int nr = off[dsc.x + 1] - off[dsc.x];
+      if (nr > kSortWaveRow) continue;  // (csr_sort_rows_kernel)
+      const int2 v = lane < nr ? occ2[ci * kDqChunk + lane] : make_int2(INT_MAX, 0);
+      int r = 0;
+      for (int j = 0; j < nr; ++j) r += __shfl(v.x, j, 64) < v.x;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < nr) occ2[ci * kDqChunk + r] = v;
+      continue;
+    }
+    if (n < 2) continue;
     int2 v = make_int2(INT_MAX, 0);
     if (lane < n) v = occ2[ci * kDqChunk + lane];
 #pragma unroll
@@ -606,6 +635,7 @@ __global__ __launch_bounds__(1024) void csr_sort_rows_kernel(const int2* __restr
   for (int si = blockIdx.x; si < ns; si += gridDim.x) {
     const int2 sp = split[si];
     const int n = off[sp.x + 1] - off[sp.x];
+    if (n <= kSortWaveRow) continue;  // (sorted by csr_sort_chunks_kernel)
     int2* row = occ2 + (int64_t)sp.y * kDqChunk;
     int2* out = tmp + (int64_t)sp.y * kDqChunk;
     // f range of the row
@@ -925,46 +955,95 @@ int launch_l2norm_rows(float* y, int64_t n, int out, float* norms, hipStream_t s
 }
 
 // ---------------------------------------------------------------- positions by rank
-// The batch positions grouped by their top-set rank, in position order: after
-// a sort of (rank, position) keys, pos_sorted[rank_off[r] .. rank_off[r + 1])
-// are the positions p with pos_rank[p] == r, increasing.  The loss (and the
-// autograd path's output gradient) sum a repeated node's per-position
-// gradients in that order (deterministic; see det_accum below).  One block,
-// keys in LDS (a bitonic network in its all-ascending form: the virtual +inf
-// padding past n never moves); more than kPosCsrMax positions marks the CSR
-// absent (rank_off[0] = -1) and the writers fall back to float atomics.
-constexpr int kPosCsrMax = 20480;  // (160 KiB of 8-byte keys)
+// The batch positions grouped by their top-set rank, in position order:
+// pos_sorted[rank_off[r] .. rank_off[r + 1]) are the positions p with
+// pos_rank[p] == r, increasing.  The loss (and the autograd path's output
+// gradient) sum a repeated node's per-position gradients in that order
+// (deterministic; see det_put below).  One block: a stable LSD radix sort of
+// (rank << 16 | position) keys in LDS by the rank's two 7-bit digits.  Each of
+// the 16 waves owns a contiguous run of keys and walks it 64 at a time; lanes
+// holding the same digit find each other with seven ballots, so a key's place
+// is its (digit, wave) base plus the count of same-digit lanes below it --
+// stable without atomics.  More than kPosCsrMax positions marks the CSR absent
+// (rank_off[0] = -1) and the writers fall back to float atomics.
+constexpr int kPosCsrMax = 16384;  // ranks < 2^14: two 7-bit digits
+constexpr int kPosDig = 7, kPosBuckets = 1 << kPosDig, kPosWaves = 16;
+constexpr int kPosCsrLds = 2 * kPosCsrMax * 4 + kPosBuckets * kPosWaves * 4 + 64;
+__device__ __forceinline__ unsigned long long match_digit(int dig, bool valid) {
+  unsigned long long m = __ballot(valid);
+#pragma unroll
+  for (int bit = 0; bit < kPosDig; ++bit) {
+    const unsigned long long bb = __ballot((dig >> bit) & 1);
+    m &= ((dig >> bit) & 1) ? bb : ~bb;
+  }
+  return m;
+}
 __global__ __launch_bounds__(1024) void pos_csr_kernel(const int32_t* __restrict__ pos_rank, int n,
                                                        int* __restrict__ rank_off, int32_t* __restrict__ pos_sorted) {
-  extern __shared__ unsigned long long key[];
+  extern __shared__ unsigned pk[];
   if (n > kPosCsrMax) {
     if (threadIdx.x == 0) rank_off[0] = -1;
     return;
   }
-  for (int i = threadIdx.x; i < n; i += blockDim.x)
-    key[i] = ((unsigned long long)(unsigned)pos_rank[i] << 32) | (unsigned)i;
-  __syncthreads();
-  int p2 = 1;
-  while (p2 < n) p2 <<= 1;
-  for (int k = 2; k <= p2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < p2 / 2; i += blockDim.x) {
-        const int lo = (i / j) * 2 * j + (i % j);
-        const int a = lo;
-        const int b = j == (k >> 1) ? (a / k) * k + (k - 1 - a % k) : lo + j;
-        if (b < n && key[b] < key[a]) {
-          const unsigned long long t = key[a];
-          key[a] = key[b];
-          key[b] = t;
-        }
-      }
-      __syncthreads();
+  unsigned* src = pk;
+  unsigned* dst = pk + kPosCsrMax;
+  int* base = reinterpret_cast<int*>(pk + 2 * kPosCsrMax);  // [bucket][wave]
+  int* wsum = base + kPosBuckets * kPosWaves;                // [16] scan scratch
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < n; i += blockDim.x) src[i] = ((unsigned)pos_rank[i] << 16) | (unsigned)i;
+  const int seg = ((n + kPosWaves - 1) / kPosWaves + 63) & ~63;
+  const int w0 = min(n, wv * seg), w1 = min(n, w0 + seg);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int sh = 16 + kPosDig * pass;
+    for (int i = tid; i < kPosBuckets * kPosWaves; i += blockDim.x) base[i] = 0;
+    __syncthreads();
+    for (int i0 = w0; i0 < w1; i0 += 64) {  // this wave's digit counts (column wv only)
+      const int i = i0 + lane;
+      const bool valid = i < w1;
+      const int dig = valid ? (int)(src[i] >> sh) & (kPosBuckets - 1) : 0;
+      const unsigned long long m = match_digit(dig, valid);
+      if (valid && (m & below) == 0) base[dig * kPosWaves + wv] += __popcll(m);
     }
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const unsigned long long v = key[i];
-    const int r = (int)(v >> 32);
-    pos_sorted[i] = (int32_t)(unsigned)v;
-    if (i == 0 || (int)(key[i - 1] >> 32) != r) rank_off[r] = i;
+    __syncthreads();
+    // exclusive scan of the (bucket, wave) counts, two per thread
+    const int c0 = base[2 * tid], c1 = base[2 * tid + 1];
+    int inc = c0 + c1;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int pre = inc - c0 - c1;
+    for (int w = 0; w < wv; ++w) pre += wsum[w];
+    base[2 * tid] = pre;
+    base[2 * tid + 1] = pre + c0;
+    __syncthreads();
+    for (int i0 = w0; i0 < w1; i0 += 64) {  // stable placement
+      const int i = i0 + lane;
+      const bool valid = i < w1;
+      const unsigned key = valid ? src[i] : 0u;
+      const int dig = (int)(key >> sh) & (kPosBuckets - 1);
+      const unsigned long long m = match_digit(dig, valid);
+      const int b = valid ? base[dig * kPosWaves + wv] : 0;
+      __builtin_amdgcn_wave_barrier();
+      if (valid) {
+        dst[b + __popcll(m & below)] = key;
+        if ((m & below) == 0) base[dig * kPosWaves + wv] = b + __popcll(m);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    unsigned* t = src;
+    src = dst;
+    dst = t;
+  }
+  for (int i = tid; i < n; i += blockDim.x) {
+    const unsigned v = src[i];
+    const int r = (int)(v >> 16);
+    pos_sorted[i] = (int32_t)(v & 0xffffu);
+    if (i == 0 || (int)(src[i - 1] >> 16) != r) rank_off[r] = i;
     if (i == n - 1) rank_off[r + 1] = n;
   }
 }
@@ -973,31 +1052,28 @@ int launch_pos_csr(const int32_t* pos_rank, int64_t n, int* rank_off, int32_t* p
   static bool prepared = false;
   if (!prepared) {
     PS_CHECK_HIP(hipFuncSetAttribute((const void*)pos_csr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kPosCsrMax * 8));
+                                     kPosCsrLds));
     prepared = true;
   }
   if (n <= 0) return kOk;
-  hipLaunchKernelGGL(pos_csr_kernel, dim3(1), dim3(1024), n <= kPosCsrMax ? (unsigned)(n * 8) : 0u, st, pos_rank,
+  hipLaunchKernelGGL(pos_csr_kernel, dim3(1), dim3(1024), n <= kPosCsrMax ? (unsigned)kPosCsrLds : 0u, st, pos_rank,
                      (int)std::min<int64_t>(n, INT32_MAX), rank_off, pos_sorted);
   PS_CHECK_LAUNCH();
   return kOk;
 }
 
 // Deterministic accumulation of one position's gradient row x (held by a wave,
-// XPL values per lane, column lane + 64 i) into G[grp][r] (row stride d),
-// positions of group grp = p % ng:
+// XPL values per lane, column lane + 64 i) into G[grp][r] (row stride d), in
+// two passes with no float atomics and no cross-workgroup fences:
 //   * the node's only position in the batch (the common case): G row = x;
-//   * repeated: x goes to Gp[p]; every contributor of (grp, r) counts itself
-//     on arrive[grp][r] (release / acquire, MI355X_MICROARCH.md inter-workgroup
-//     visibility) and the last to arrive sums the group's rows in position
-//     order into G and re-arms the counter -- no float atomics, so the sum is
-//     bitwise the same on every run.
-//   rank_off[0] == -1 (no CSR): float atomics (order-dependent) as before.
+//   * a repeated node: x goes to Gp[p] (zeros from an inactive triple too), and
+//     rep_sum_kernel, launched behind the writer, sums each group's rows in
+//     position order (pos_sorted) into G -- bitwise the same on every run.
+//   rank_off[0] == -1 (no position CSR): float atomics (order-dependent).
 template <int XPL>
-__device__ __forceinline__ void det_accum(const float (&x)[XPL], int d, int p, int r, int grp, int ng,
-                                          const int* __restrict__ rank_off, const int32_t* __restrict__ pos_sorted,
-                                          float* __restrict__ G, int64_t S_max, float* __restrict__ Gp,
-                                          int* __restrict__ arrive, int lane) {
+__device__ __forceinline__ void det_put(const float (&x)[XPL], int d, int p, int r, int grp,
+                                        const int* __restrict__ rank_off, float* __restrict__ G, int64_t S_max,
+                                        float* __restrict__ Gp, int lane) {
   float* g = G + ((int64_t)grp * S_max + r) * d;
   if (rank_off[0] < 0) {
 #pragma unroll
@@ -1005,52 +1081,71 @@ __device__ __forceinline__ void det_accum(const float (&x)[XPL], int d, int p, i
       if (lane + 64 * i < d) atomicAdd(g + lane + 64 * i, x[i]);
     return;
   }
-  const int o0 = rank_off[r], o1 = rank_off[r + 1];
-  if (o1 - o0 == 1) {
-#pragma unroll
-    for (int i = 0; i < XPL; ++i)
-      if (lane + 64 * i < d) g[lane + 64 * i] = x[i];
-    return;
-  }
-  // this group's contributors of r
-  int K = 0;
-  for (int o = o0; o < o1; o += 64) {
-    const int q = o + lane < o1 ? pos_sorted[o + lane] : -1;
-    K += __popcll(__ballot(q >= 0 && q % ng == grp));
-  }
-  if (K == 1) {
-#pragma unroll
-    for (int i = 0; i < XPL; ++i)
-      if (lane + 64 * i < d) g[lane + 64 * i] = x[i];
-    return;
-  }
+  float* dst = rank_off[r + 1] - rank_off[r] == 1 ? g : Gp + (int64_t)p * d;
 #pragma unroll
   for (int i = 0; i < XPL; ++i)
-    if (lane + 64 * i < d) Gp[(int64_t)p * d + lane + 64 * i] = x[i];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int old = 0;
-  if (lane == 0)
-    old = __hip_atomic_fetch_add(arrive + (int64_t)grp * S_max + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __shfl(old, 0, 64);
-  if (old != K - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float acc[XPL];
+    if (lane + 64 * i < d) dst[lane + 64 * i] = x[i];
+}
+
+// Second pass: one wave per repeated rank r; G[grp][r] = the sum, in position
+// order, of the rows Gp[p] of r's positions p with p % ng == grp (groups with
+// no position keep their zero row).  Sixteen rows are in flight at a time
+// (their positions one load by lanes 0..15), added in order.
+constexpr int kRepBatch = 16;
+template <int XPL, int NG>
+__global__ __launch_bounds__(256) void rep_sum_kernel(const int* __restrict__ rank_off,
+                                                      const int32_t* __restrict__ pos_sorted,
+                                                      const int* __restrict__ nS, int d,
+                                                      const float* __restrict__ Gp, float* __restrict__ G,
+                                                      int64_t S_max) {
+  if (rank_off[0] < 0) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t R = *nS;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += nw) {
+    const int o0 = rank_off[r], o1 = rank_off[r + 1];
+    if (o1 - o0 < 2) continue;
+    float acc[NG][XPL];
+    bool any[NG];
 #pragma unroll
-  for (int i = 0; i < XPL; ++i) acc[i] = 0.f;
-  for (int o = o0; o < o1; ++o) {
-    const int q = pos_sorted[o];
-    if (q % ng != grp) continue;
+    for (int c = 0; c < NG; ++c) {
+      any[c] = false;
 #pragma unroll
-    for (int i = 0; i < XPL; ++i)
-      if (lane + 64 * i < d) acc[i] += __builtin_nontemporal_load(Gp + (int64_t)q * d + lane + 64 * i);
+      for (int i = 0; i < XPL; ++i) acc[c][i] = 0.f;
+    }
+    for (int o = o0; o < o1; o += kRepBatch) {
+      const int my_q = lane < kRepBatch && o + lane < o1 ? pos_sorted[o + lane] : -1;
+      int q[kRepBatch];
+      float v[kRepBatch][XPL];
+#pragma unroll
+      for (int u = 0; u < kRepBatch; ++u) q[u] = __shfl(my_q, u, 64);
+#pragma unroll
+      for (int u = 0; u < kRepBatch; ++u)
+#pragma unroll
+        for (int i = 0; i < XPL; ++i)
+          v[u][i] = q[u] >= 0 && lane + 64 * i < d ? Gp[(int64_t)q[u] * d + lane + 64 * i] : 0.f;
+#pragma unroll
+      for (int u = 0; u < kRepBatch; ++u) {
+        if (q[u] < 0) continue;
+        const int c = NG == 1 ? 0 : q[u] % NG;
+#pragma unroll
+        for (int cc = 0; cc < NG; ++cc)
+          if (cc == c) {
+            any[cc] = true;
+#pragma unroll
+            for (int i = 0; i < XPL; ++i) acc[cc][i] += v[u][i];
+          }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NG; ++c)
+      if (any[c]) {
+        float* g = G + ((int64_t)c * S_max + r) * d;
+#pragma unroll
+        for (int i = 0; i < XPL; ++i)
+          if (lane + 64 * i < d) g[lane + 64 * i] = acc[c][i];
+      }
   }
-#pragma unroll
-  for (int i = 0; i < XPL; ++i)
-    if (lane + 64 * i < d) g[lane + 64 * i] = acc[i];
-  if (lane == 0) __hip_atomic_store(arrive + (int64_t)grp * S_max + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- loss
@@ -1073,7 +1168,7 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
     const float* __restrict__ feats, int64_t ld_f, int d_in, const int64_t* __restrict__ batch,
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ part,
     float* __restrict__ colpart, float* __restrict__ hinge, const int* __restrict__ rank_off,
-    const int32_t* __restrict__ pos_sorted, float* __restrict__ Gp, int* __restrict__ arrive) {
+    float* __restrict__ Gp) {
   __shared__ float red[4][4];  // per wave: loss, nfl, sum||h_q||^2, unused
   __shared__ float qrow[4][64 * ZPL];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1158,20 +1253,19 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
         xp[i] = (-g * a - p * pp) / np;
         xn[i] = (g * a - n * pn) / nn;
       }
-      det_accum<ZPL>(xq, d, 3 * b, rq, 0, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
-      det_accum<ZPL>(xp, d, 3 * b + 1, rp, 1, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
-      det_accum<ZPL>(xn, d, 3 * b + 2, rn, 2, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+      det_put<ZPL>(xq, d, 3 * b, rq, 0, rank_off, G, S_max, Gp, lane);
+      det_put<ZPL>(xp, d, 3 * b + 1, rp, 1, rank_off, G, S_max, Gp, lane);
+      det_put<ZPL>(xn, d, 3 * b + 2, rn, 2, rank_off, G, S_max, Gp, lane);
     } else if (valid && rank_off[0] >= 0) {
-      // an inactive triple adds zeros: a repeated node's last contributor still
-      // needs every contributor's arrival (and zero rows) to form its sum
-      float z0[ZPL];
-#pragma unroll
-      for (int i = 0; i < ZPL; ++i) z0[i] = 0.f;
+      // an inactive triple's positions of a repeated node hold zero rows (the
+      // ordered sum reads every position of the node)
       const int rr[3] = {rq, rp, rn};
 #pragma unroll
       for (int c3 = 0; c3 < 3; ++c3)
         if (rank_off[rr[c3] + 1] - rank_off[rr[c3]] > 1)
-          det_accum<ZPL>(z0, d, 3 * b + c3, rr[c3], c3, 3, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+#pragma unroll
+          for (int i = 0; i < ZPL; ++i)
+            if (lane + 64 * i < d) Gp[(int64_t)(3 * b + c3) * d + lane + 64 * i] = 0.f;
     }
     if (valid && lane == 0) {
       atomicAdd(Kc + 0 * S_max + rq, 1);
@@ -1413,13 +1507,12 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
 }
 
 // one call: G[r] = sum of dout rows at positions of node r (in position order,
-// det_accum), K[r] = multiplicity; one wave per position
+// det_put + rep_sum_kernel), K[r] = multiplicity; one wave per position
 __global__ __launch_bounds__(256) void dout_accum_kernel(const float* __restrict__ dout, int d,
                                                          const int32_t* __restrict__ pr, int64_t n,
                                                          float* __restrict__ G, int* __restrict__ Kc, int64_t S_max,
                                                          const int* __restrict__ rank_off,
-                                                         const int32_t* __restrict__ pos_sorted,
-                                                         float* __restrict__ Gp, int* __restrict__ arrive) {
+                                                         float* __restrict__ Gp) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
@@ -1427,7 +1520,7 @@ __global__ __launch_bounds__(256) void dout_accum_kernel(const float* __restrict
     float x[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) x[k] = lane + 64 * k < d ? dout[i * d + lane + 64 * k] : 0.f;
-    det_accum<4>(x, d, (int)i, r, 0, 1, rank_off, pos_sorted, G, S_max, Gp, arrive, lane);
+    det_put<4>(x, d, (int)i, r, 0, rank_off, G, S_max, Gp, lane);
     if (lane == 0) atomicAdd(Kc + r, 1);
   }
 }
@@ -1549,10 +1642,13 @@ int launch_gather_rows(const float* h, int64_t ldh, int64_t n_h, int d, const in
 // the unfused head: scale = true)
 int launch_dz_from_dout(const float* dout, int d, const int32_t* pr, int64_t n, const int* nS,
                         int64_t S_max, float* G, int* Kc, float* dZ, bool scale, const int* rank_off,
-                        const int32_t* pos_sorted, float* Gp, int* arrive, hipStream_t st) {
+                        const int32_t* pos_sorted, float* Gp, hipStream_t st) {
   PS_REQUIRE(d <= 256, kErrArg, "dz_from_dout: out_dim must be <= 256");
   hipLaunchKernelGGL(dout_accum_kernel, dim3(grid_for(n * 64, 256)), dim3(256), 0, st, dout, d, pr, n, G, Kc, S_max,
-                     rank_off, pos_sorted, Gp, arrive);
+                     rank_off, Gp);
+  PS_CHECK_LAUNCH();
+  hipLaunchKernelGGL((rep_sum_kernel<4, 1>), dim3(grid_for(S_max * 64, 256)), dim3(256), 0, st, rank_off,
+                     pos_sorted, nS, d, Gp, G, S_max);
   PS_CHECK_LAUNCH();
   if (scale) {
     hipLaunchKernelGGL(dz_scale_kernel, dim3(grid_for(S_max * d, 256)), dim3(256), 0, st, G, Kc, d, nS,
@@ -1687,14 +1783,14 @@ int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64
     PS_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(csr_fill_kernel, dim3(gb), dim3(1024), lds, st, loc, wloc, nS, T, nN, cursor, off, cbase,
-                     occ2, max_ranges);
+                     occ2, max_ranges, split, nsplit, chunks);
   PS_CHECK_LAUNCH();
   // canonical pair order (sorted by source row): bitwise-reproducible sums
   static const bool canon = !getenv("PINSAGE_CSR_CANON") || atoi(getenv("PINSAGE_CSR_CANON")) != 0;
   if (canon && occ2_tmp) {
     const int64_t max_chunks = dq_chunk_capacity(S_max, T, N_max);
     hipLaunchKernelGGL(csr_sort_chunks_kernel, dim3(grid_for(max_chunks * 64, 256, 2048)), dim3(256), 0, st,
-                       chunks, nchunks, occ2);
+                       chunks, nchunks, off, occ2);
     PS_CHECK_LAUNCH();
     hipLaunchKernelGGL(csr_sort_rows_kernel, dim3(256), dim3(1024), kRankLds, st, split, nsplit, off, occ2,
                        occ2_tmp);
@@ -1756,7 +1852,7 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
                 const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
                 int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
                 float* hinge, bool combine_dz, const int* rank_off, const int32_t* pos_sorted, float* Gp,
-                int* arrive, hipStream_t st) {
+                hipStream_t st) {
   // G and Kc are zero on entry (init_workspace; then the head backward (or
   // dz_combine) and the first backward kernel leave them zero)
   PS_REQUIRE(d <= 256, kErrArg, "loss: out_dim must be <= 256");
@@ -1765,8 +1861,7 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   const int fpl = d_in <= 128 ? 2 : d_in <= 256 ? 4 : 8;
 #define PS_LOSS(ZP, FP)                                                                           \
   hipLaunchKernelGGL((loss_triple_kernel<ZP, FP>), dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, \
-                     margin, feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge, rank_off, pos_sorted, \
-                     Gp, arrive)
+                     margin, feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge, rank_off, Gp)
   if (d <= 128) {
     if (fpl == 2) PS_LOSS(2, 2);
     else if (fpl == 4) PS_LOSS(2, 4);
@@ -1777,6 +1872,13 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
     else PS_LOSS(4, 8);
   }
 #undef PS_LOSS
+  PS_CHECK_LAUNCH();
+  if (d <= 128)
+    hipLaunchKernelGGL((rep_sum_kernel<2, 3>), dim3(grid_for(S_max * 64, 256)), dim3(256), 0, st, rank_off,
+                       pos_sorted, nS, d, Gp, G, S_max);
+  else
+    hipLaunchKernelGGL((rep_sum_kernel<4, 3>), dim3(grid_for(S_max * 64, 256)), dim3(256), 0, st, rank_off,
+                       pos_sorted, nS, d, Gp, G, S_max);
   PS_CHECK_LAUNCH();
   if (combine_dz) {
     hipLaunchKernelGGL(dz_combine_kernel, dim3(grid_for(S_max * d, 1024, 256)), dim3(1024), 0, st, G,

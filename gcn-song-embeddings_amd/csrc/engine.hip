@@ -57,7 +57,7 @@ int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const i
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
-                float*, bool, const int*, const int32_t*, float*, int*, hipStream_t);
+                float*, bool, const int*, const int32_t*, float*, hipStream_t);
 int launch_pos_csr(const int32_t*, int64_t, int*, int32_t*, hipStream_t);
 int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
@@ -72,7 +72,7 @@ int launch_head_bwd(float*, int*, int64_t, float*, int, const int*, int64_t, con
                     const float*, const float*, const float*, const float*, float*, float*,
                     hipStream_t);
 int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
-                        int*, float*, bool, const int*, const int32_t*, float*, int*, hipStream_t);
+                        int*, float*, bool, const int*, const int32_t*, float*, hipStream_t);
 
 struct EngineConfig {
   int64_t n_items;   // rows of the feature table (track universe)
@@ -182,8 +182,8 @@ struct Engine {
   size_t block_sums = 0, ids = 0, pos_rank = 0, H1 = 0, Z = 0, dZ = 0, dP1 = 0;
   size_t G = 0, Kc = 0, part = 0, scal = 0, slab = 0, bslab = 0, varpart = 0, hinge = 0;
   // the batch positions by top-set rank (pos_csr) and the deterministic
-  // accumulation of repeated nodes' gradients (conv.hip det_accum)
-  size_t rank_off = 0, pos_sorted = 0, Gp = 0, arrive = 0;
+  // accumulation of repeated nodes' gradients (conv.hip det_put / rep_sum_kernel)
+  size_t rank_off = 0, pos_sorted = 0, Gp = 0;
   size_t slab_main = 0, bslab_main = 0;  // split-K slabs of the main stream's weight gradient
   int64_t slab_floats = 0;
   // stream-K scratch of the main stream's GEMMs (gemm.h)
@@ -453,7 +453,6 @@ static void layout(Engine& E) {
   E.rank_off = carve(cur, (c.max_pos + 2) * 4);
   E.pos_sorted = carve(cur, c.max_pos * 4);
   E.Gp = carve(cur, c.max_pos * c.out * 4);
-  E.arrive = carve(cur, 3 * top * 4);
   E.part = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * 4 * 4);
   E.varpart = carve(cur, (int64_t)(ceil_div(c.max_pos, 4) + 1) * 2 * c.out * 4);  // (sum, M2)
   E.hinge = carve(cur, (c.max_pos / 3 + 1) * 4);  // per-triple hinge argument of the last loss
@@ -1117,7 +1116,6 @@ int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
   const int64_t top = E.L.back().S.cap;
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.G), 0, (size_t)(3 * top * c.out) * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.Kc), 0, (size_t)(3 * top) * 4, st));
-  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.arrive), 0, (size_t)(3 * top) * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.rank_off), 0xff, 4, st));  // (no positions yet)
   for (auto& lb : E.L)
     PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, lb.cnt), 0, (size_t)(lb.N.cap + 1) * 4, st));
@@ -1392,7 +1390,7 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
                        at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
                        at<float>(ws, E->varpart), at<float>(ws, E->scal), at<float>(ws, E->hinge),
                        !E->fused_head, at<int>(ws, E->rank_off), at<int32_t>(ws, E->pos_sorted),
-                       at<float>(ws, E->Gp), at<int>(ws, E->arrive), st));
+                       at<float>(ws, E->Gp), st));
   }
   // the monitors (loss, node-feature loss, variance scalars) beside the
   // backward, on side stream 0, joined at the backward's end (with
@@ -1421,7 +1419,7 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
                              at<int>(ws, top.S.count), top.S.cap, at<float>(ws, E->G),
                              at<int>(ws, E->Kc), at<float>(ws, E->dZ), !E->fused_head,
                              at<int>(ws, E->rank_off), at<int32_t>(ws, E->pos_sorted), at<float>(ws, E->Gp),
-                             at<int>(ws, E->arrive), (hipStream_t)stream);
+                             (hipStream_t)stream);
 }
 
 int pinsage_engine_reset_backward(pinsage_engine* e, void* ws, void* stream) {

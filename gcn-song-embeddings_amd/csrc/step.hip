@@ -106,7 +106,9 @@ struct Stepper {
   std::vector<int64_t> pending[2];  // ids whose frontier sits in workspace p (empty: none)
   int parity = 0;
   int64_t nstep = 0, hits = 0;
-  int64_t wait_ns = 0;  // host time blocked on ring slots (the GPU is behind)
+  int64_t wait_ns = 0;    // host time blocked on ring slots (the GPU is behind)
+  int64_t launch_ns = 0;  // host time inside hipGraphLaunch
+  int64_t call_ns = 0;    // host time inside pinsage_stepper_step
 };
 
 }  // extern "C"
@@ -163,6 +165,17 @@ int64_t pinsage_stepper_wait_ns(const pinsage_stepper* h) {
   return s ? s->wait_ns : -1;
 }
 
+int pinsage_stepper_stats(const pinsage_stepper* h, int64_t* out, int n) {
+  const auto* s = reinterpret_cast<const Stepper*>(h);
+  if (!s || !out || n < 0) {
+    set_error("stepper_stats: bad argument");
+    return kErrArg;
+  }
+  const int64_t v[5] = {s->wait_ns, s->launch_ns, s->call_ns, s->nstep, s->hits};
+  for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+  return kOk;
+}
+
 int pinsage_stepper_set_graphs(pinsage_stepper* h, int p, void* gf, void* gm, void* ga) {
   auto* s = reinterpret_cast<Stepper*>(h);
   if (!s || (p != 0 && p != 1) || !gf || !gm) {
@@ -201,11 +214,16 @@ int pinsage_stepper_step(pinsage_stepper* h, const int64_t* batch, int64_t n_ids
     return kErrArg;
   }
   hipStream_t st = (hipStream_t)stream;
+  using clk = std::chrono::steady_clock;
+  auto ns_since = [](clk::time_point t) {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t).count();
+  };
+  const auto t_call = clk::now();
   const int64_t k = s->nstep % s->R;
   if (s->ev_live[(size_t)k]) {  // the slot's last user is done
-    const auto t0 = std::chrono::steady_clock::now();
+    const auto t0 = clk::now();
     PS_CHECK_HIP(hipEventSynchronize(s->ev[(size_t)k]));
-    s->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    s->wait_ns += ns_since(t0);
   }
   uint8_t* slot = s->ring + k * s->slot_bytes;
   std::memcpy(slot + s->off_coef, coef, 8);
@@ -217,17 +235,23 @@ int pinsage_stepper_step(pinsage_stepper* h, const int64_t* batch, int64_t n_ids
       return kErrIndex;
     }
     std::memcpy(slot + s->off_ids, batch, (size_t)n_ids * 8);
+    const auto t0 = clk::now();
     PS_CHECK_HIP(hipGraphLaunch(s->gf[p], st));
+    s->launch_ns += ns_since(t0);
   } else {
     s->hits++;
   }
   s->pending[p].clear();
   if (next && ids_in_range(next, n_ids, s->n_items)) {
     std::memcpy(slot + s->off_next, next, (size_t)n_ids * 8);
+    const auto t0 = clk::now();
     PS_CHECK_HIP(hipGraphLaunch(s->ga[p], st));
+    s->launch_ns += ns_since(t0);
     s->pending[1 - p].assign(next, next + n_ids);
   } else {
+    const auto t0 = clk::now();
     PS_CHECK_HIP(hipGraphLaunch(s->gm[p], st));
+    s->launch_ns += ns_since(t0);
     s->pending[1 - p].clear();
   }
   PS_CHECK_HIP(hipEventRecord(s->ev[(size_t)k], st));
@@ -238,6 +262,7 @@ int pinsage_stepper_step(pinsage_stepper* h, const int64_t* batch, int64_t n_ids
   }
   s->parity ^= 1;
   s->nstep++;
+  s->call_ns += ns_since(t_call);
   return kOk;
 }
 

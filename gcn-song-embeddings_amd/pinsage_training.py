@@ -325,6 +325,15 @@ class _FusedStep:
             w += nat.lib().pinsage_stepper_wait_ns(self.stepper) * 1e-9
         return w
 
+    def stepper_stats(self):
+        """Host nanoseconds of the native step path so far (pinsage_stepper_stats):
+        {wait_ns, launch_ns, call_ns, steps, hits}, or None without a stepper."""
+        if self.stepper is None:
+            return None
+        v = (ctypes.c_int64 * 5)()
+        nat.check(nat.lib().pinsage_stepper_stats(self.stepper, v, 5), "stepper_stats")
+        return dict(zip(("wait_ns", "launch_ns", "call_ns", "steps", "hits"), (int(x) for x in v)))
+
     def ensure(self, B):
         r = self.runner
         r.pack()

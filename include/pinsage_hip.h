@@ -299,6 +299,9 @@ void pinsage_stepper_destroy(pinsage_stepper* s);
 int pinsage_stepper_set_graphs(pinsage_stepper* s, int p, void* gf, void* gm, void* ga);
 /* host nanoseconds spent blocked on ring slots so far (the device behind the host) */
 int64_t pinsage_stepper_wait_ns(const pinsage_stepper* s);
+/* out[0 .. n) of {ns blocked on ring slots, ns inside hipGraphLaunch, ns inside
+ * pinsage_stepper_step, steps, ahead hits} (host accounting of the native path) */
+int pinsage_stepper_stats(const pinsage_stepper* s, int64_t* out, int n);
 /* resume from the trainer's eager path: next parity, step counter, no pending frontier */
 int pinsage_stepper_sync_state(pinsage_stepper* s, int parity, int64_t nstep);
 int pinsage_stepper_step(pinsage_stepper* s, const int64_t* batch, int64_t n_ids, const float* coef,
