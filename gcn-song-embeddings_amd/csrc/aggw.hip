@@ -438,11 +438,20 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
         }
         const int col = cg * 32 + l32;
         const float bq = nx.Qb[col];
+        // values and destinations first, pinned in registers, then the stores
+        // alone: a use of the loaded bias among the guarded stores made the
+        // compiler wait for every earlier store before each one
+        float qv[16];
+        int us[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int u = sLoc[(r & 3) + 8 * (r >> 2) + 4 * hh];
-          if (u >= 0) nx.q[(int64_t)u * nx.hid + col] = lrelu(acc[r] + bq);
+          us[r] = sLoc[(r & 3) + 8 * (r >> 2) + 4 * hh];
+          qv[r] = lrelu(acc[r] + bq);
+          asm volatile("" : "+v"(qv[r]), "+v"(us[r]));
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (us[r] >= 0) nx.q[(int64_t)us[r] * nx.hid + col] = qv[r];
       }
     }
     __syncthreads();  // LDS is reused by the next tile

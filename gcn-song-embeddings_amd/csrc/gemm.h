@@ -61,7 +61,7 @@ struct GemmParams {
   float* norms = nullptr;         // kEpiL2Norm: per-row L2 norms
   int splits = 1;                 // kEpiPartial: split-K count
   int M_hint = 0;                 // expected M (device-side M): picks the block tile
-  int cfg = -1;                   // force a tile config (tests); -1 = choose by size
+  int cfg = -1;                   // force a tile config 0..5 (tests, tuner); -1 = choose by size
   // stream-K (kEpiStore / kEpiAccum / kEpiL2Norm, static K > 0, K-major or
   // ungathered MN-major operands): the launch's k-steps are cut into equal runs
   // over a full grid, and tiles cut between blocks are combined in-launch.

@@ -182,10 +182,42 @@ struct SkPlan {
   }
 };
 
+// 4 x 4 transposes inside lane quads, by two DPP butterflies: v[4g + k] of
+// lane (quad q, i = lane & 3) holds row k of column 4q + i of row group g
+// (the 32x32 f32 accumulator layout: register r is row (r & 3) + 8 (r >> 2) of
+// column l32); afterwards it holds row i, column 4q + k -- four consecutive
+// columns of one row, one 16-B store instead of four 4-B ones.
+__device__ __forceinline__ float dpp_xor1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float dpp_xor2(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+}
+__device__ __forceinline__ void quad_transpose16(float (&v)[16], int lane) {
+  const int i = lane & 3;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = dpp_xor1(v[4 * g + (k ^ 1)]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((i & 1) != (k & 1)) v[4 * g + k] = t[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = dpp_xor2(v[4 * g + (k ^ 2)]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((i & 2) != (k & 2)) v[4 * g + k] = t[k];
+  }
+}
+
 // WM x WN waves, each TM x TN MFMA tiles of 32x32; stage depth BK; at most
-// NSMAX stage buffers in the ring.
+// NSMAX stage buffers in the ring.  SK: the kernel carries the stream-K
+// schedule (cfg 1 and 2, the tiles launch_gemm runs it on); without it the
+// tile loop is inlined once and the code is ~40 % smaller, which a launch
+// pays for in instruction fetch before its first MFMA.
 template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2,
-          bool BF = false, bool PB = false>
+          bool BF = false, bool PB = false, bool SK = true>
 __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   static_assert(!BF || BK % 16 == 0, "split-bf16 products: 16-k steps");
   static_assert(!PB || (BF && BKM), "pre-split B: split-bf16 products, K-major B");
@@ -208,6 +240,13 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+#ifdef PS_GEMM_PROBE  // (diagnostic build only) wall-clock phases of block 0's first tile
+  uint64_t pt[6] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0};
+  int pti = 1;
+#define PS_PROBE() do { if (pti < 6) pt[pti++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PS_PROBE() do { } while (0)
+#endif
   const int M = p.M_dev ? *p.M_dev : p.M;
   const int K = p.K_dev ? *p.K_dev : p.K;
   const int N = p.N;
@@ -274,6 +313,14 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
     };
     const bool do_bias = !AK && p.bias_part && tn == 0 && tid < BM;
     float bsum = 0.f;
+    // the store / accumulate epilogue's bias, fetched under the k loop (a load
+    // issued in the epilogue put one more memory round trip on every tile)
+    float bj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + (wn * TN + j) * 32 + l32;
+      bj[j] = (p.bias && col < N && p.epi != kEpiL2Norm && p.epi != kEpiPartial) ? p.bias[col] : 0.f;
+    }
     // MFMA k-assignment: in the r-th MFMA of octet s, lane half h supplies
     // k = 8s + 4h + r for both operands (any bijection onto the 8 k works).
     // Fragments of octet s+1 are read from LDS while octet s's MFMAs run.
@@ -362,11 +409,13 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
     // ring: stage t is computed from slot t % NS while stages t+1 .. t+NS-2 are
     // in flight; stage t+NS-1 is issued into the slot stage t-1 used
     auto slot = [&](int st) __attribute__((always_inline)) { return smem + (st % NS) * SZS; };
+    PS_PROBE();
     for (int st = 0; st < NS - 1 && st < nk; ++st) issue(st);
     for (int it = 0; it < nk; ++it) {
       // retire this wave's DMAs of stage it; the younger stages stay in flight
       const int younger = min(NS - 2, nk - 1 - it);
       wait_stage<NG, NS - 2>(younger);
+      if (it == 0) PS_PROBE();
       float* cur = slot(it);
       if (tail && it == nk - 1) {  // zero the k-tail this thread's DMAs brought in
         const int k0 = kb + it * BK;
@@ -390,13 +439,14 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
       compute(cur, cur + SZA);
     }
     __syncthreads();  // stage buffers are reused by the epilogue / next tile
+    PS_PROBE();
 
     // ------------------------------------------------------------ stream-K
     // Publish (write-through sc1 slab stores, every wave drains, one ticket
     // add per block); the block drawing the last ticket reads every segment's
     // slab with sc1 loads in block order (a fixed summation order: the result
     // does not depend on which block arrives last) and runs the epilogue.
-    if (sk_t >= 0) {
+    if constexpr (SK) if (sk_t >= 0) {
       typedef int v4i __attribute__((ext_vector_type(4)));
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc(p.sk_slab, 0, 0x7fffffff, 0x00020000);
@@ -457,6 +507,8 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
     if (p.epi == kEpiPartial) {
       if (do_bias && m0 + tid < M) p.bias_part[(int64_t)split * M + m0 + tid] = bsum;
       float* C = p.c + (int64_t)split * M * p.ldc;
+      // (dword stores: the store epilogue's 16-B form, quad_transpose16,
+      // measured slower on these split-K slabs -- C2 dQ0 68 -> 77 us)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -498,6 +550,10 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
           const int row = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           dsts[r] = row < M ? (p.c_idx ? (int64_t)p.c_idx[row] : (int64_t)row) : -1;
         }
+        // (all scatter rows in registers before the first store: see the store
+        // epilogue below)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(dsts[r]));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int lrow = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -517,16 +573,74 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
         }
       }
     } else {
-      // the bias is read into registers before the first store (interleaved,
-      // each store may alias the next bias load, which was then re-issued and
-      // waited on per element)
+      // (the bias bj came in under the k loop: an epilogue load interleaved with
+      // stores that may alias it was re-issued and waited on per element)
       const bool accum = p.epi == kEpiAccum;
-      float bj[TN];
+      // 16-B rows (quad_transpose16): bias and activation per column first,
+      // then per lane four consecutive columns of one row -- its mask /
+      // accumulated values one 16-B load, its output one 16-B store (the store
+      // tail was bound by store-instruction issue: four times fewer).  Needs
+      // 16-B aligned rows of every operand the epilogue touches.
+      const bool wide = N % 4 == 0 && p.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(p.c) & 15) == 0 &&
+                        (!p.c2 || (p.ldc2 % 4 == 0 && p.N1 % 4 == 0 && (reinterpret_cast<uintptr_t>(p.c2) & 15) == 0)) &&
+                        (!p.mask || (p.ldm % 4 == 0 && (reinterpret_cast<uintptr_t>(p.mask) & 15) == 0));
+      if (wide) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + (wn * TN + j) * 32 + l32;
-        bj[j] = (p.bias && col < N) ? p.bias[col] : 0.f;
-      }
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              float x = acc[i][j][r] + bj[j];
+              if (p.act) x = lrelu(x);
+              v[r] = x;
+            }
+            quad_transpose16(v, lane);
+            const int col = n0 + (wn * TN + j) * 32 + 4 * (l32 >> 2);
+            const bool second = p.c2 && col >= p.N1;
+            int rows[4];
+            int64_t dst[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              rows[g] = m0 + (wm * TM + i) * 32 + (l32 & 3) + 8 * g + 4 * h;
+              dst[g] = rows[g] < M && col < N ? (p.c_idx ? (int64_t)p.c_idx[rows[g]] : (int64_t)rows[g]) : -1;
+            }
+            float4 pre[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              pre[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (dst[g] >= 0) {
+                if (p.mask) pre[g] = *reinterpret_cast<const float4*>(p.mask + (int64_t)rows[g] * p.ldm + col);
+                else if (accum && !second) pre[g] = *reinterpret_cast<const float4*>(p.c + dst[g] * p.ldc + col);
+              }
+            }
+            float4 val[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              float4 x = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+              if (p.mask) {
+                x.x *= lrelu_grad(pre[g].x);
+                x.y *= lrelu_grad(pre[g].y);
+                x.z *= lrelu_grad(pre[g].z);
+                x.w *= lrelu_grad(pre[g].w);
+              } else if (accum && !second) {
+                x.x = pre[g].x + x.x;
+                x.y = pre[g].y + x.y;
+                x.z = pre[g].z + x.z;
+                x.w = pre[g].w + x.w;
+              }
+              val[g] = x;
+              asm volatile("" : "+v"(val[g].x), "+v"(val[g].y), "+v"(val[g].z), "+v"(val[g].w));
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              if (dst[g] >= 0)
+                *reinterpret_cast<float4*>(second ? p.c2 + (int64_t)rows[g] * p.ldc2 + (col - p.N1)
+                                                  : p.c + dst[g] * p.ldc + col) = val[g];
+          }
+      } else {
+      // (the scalar form, any alignment)
       // Per 8 rows of a 32-row block: every load (scatter rows, lrelu' masks, the
       // values an accumulate adds to) is issued before those rows' first store --
       // loads interleaved with stores that may alias them were waited on one
@@ -543,7 +657,7 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
             dsts[r] = row < M ? (p.c_idx ? p.c_idx[row] : row) : -1;
           }
           // pre: lrelu'(mask) with a mask, else the values an accumulate adds to
-          // (mask and accumulate together -- no caller -- reload the old value)
+          // (launch_gemm refuses a mask with an accumulate)
           float pre[8][TN];
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
@@ -558,32 +672,57 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
               pre[r][j] = x;
             }
           }
+          // every value and row address is formed (and pinned in registers)
+          // before the first store: a use of a loaded value among the stores
+          // made the compiler wait for all earlier stores before each one
+          // (vmcnt counts stores too) -- ~8 us per 64 x 128 tile, more than the
+          // k loop of a K = 128 launch
+          float val[8][TN];
+          float* rowp[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            rowp[r] = p.c + (int64_t)(dsts[r] < 0 ? 0 : dsts[r]) * p.ldc;
+            asm volatile("" : "+v"(rowp[r]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int col = n0 + (wn * TN + j) * 32 + l32;
+              float v = acc[i][j][r0 + r] + bj[j];
+              if (p.act) v = lrelu(v);
+              if (p.mask) v *= pre[r][j];
+              else if (accum && !(p.c2 && col >= p.N1)) v = pre[r][j] + v;
+              val[r][j] = v;
+              asm volatile("" : "+v"(val[r][j]));
+            }
+          }
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
             const int row = m0 + (wm * TM + i) * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * h;
             if (row >= M) continue;
-            const int64_t dst = dsts[r];
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
               const int col = n0 + (wn * TN + j) * 32 + l32;
               if (col >= N) continue;
-              float v = acc[i][j][r0 + r] + bj[j];
-              if (p.act) v = lrelu(v);
-              if (p.mask) v *= pre[r][j];
-              if (p.c2 && col >= p.N1) {
-                p.c2[(int64_t)row * p.ldc2 + (col - p.N1)] = v;
-              } else {
-                float* o = p.c + dst * p.ldc + col;
-                *o = accum ? (p.mask ? *o : pre[r][j]) + v : v;
-              }
+              float* o = p.c2 && col >= p.N1 ? p.c2 + (int64_t)row * p.ldc2 + (col - p.N1) : rowp[r] + col;
+              *o = val[r][j];
             }
           }
         }
+      }
     }
-    __syncthreads();
+    // the next tile's stage buffers / the L2-norm partials reuse LDS: wait for
+    // this tile's LDS traffic only -- its global stores drain under the next
+    // tile's k loop (a __syncthreads would wait for every store to complete)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    PS_PROBE();
+#ifdef PS_GEMM_PROBE
+    if (blockIdx.x == 0 && tid == 0)
+      printf("gemm probe [10ns]: init %d wait0 %d kloop %d epi %d\n", (int)(pt[1] - pt[0]), (int)(pt[2] - pt[1]),
+             (int)(pt[3] - pt[2]), (int)(pt[4] - pt[3]));
+#endif
   };
 
-  if (p.sk_cnt) {
+  if constexpr (SK) if (p.sk_cnt) {
     // stream-K: the tiles' k-steps laid end to end and cut into equal runs,
     // at least sk_min_units k-steps each (launch_gemm: K-major or ungathered
     // operands, K > 0, no split-K partials)
@@ -860,7 +999,8 @@ static int launch_gemm_ws(const GemmParams& p, int Mmax, hipStream_t st) {
   return launch_ws_variant<32, 3, 1>(p, Mmax, st);
 }
 
-constexpr int kCfgBM[5] = {128, 64, 32, 64, 64};
+// rows per tile of each cfg (5: gemm_ws_kernel's 64-row tiles)
+constexpr int kCfgBM[6] = {128, 64, 32, 64, 64, 64};
 
 // the product arithmetic of GEMMs that do not choose (GemmParams::prec < 0):
 // PINSAGE_GEMM_PREC at load, then pinsage_gemm_set_prec
@@ -952,41 +1092,49 @@ static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
   if constexpr (BKM) {
     if (p.prec == 1 && p.b_split && (cfg == 0 || cfg == 3)) {  // pre-split B planes
       if (cfg == 0)
-        hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true, true>), g, dim3(256), 0,
-                           st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true, true, false>), g, dim3(256),
+                           0, st, p);
       else
-        hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true, true>), g, dim3(256), 0,
-                           st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true, true, false>), g, dim3(256),
+                           0, st, p);
       return;
     }
   }
   if (p.prec == 1) {  // split-bf16 products (same tiles, same LDS images)
     if (cfg == 0)
-      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true>), g, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, true, false, false>), g, dim3(256), 0,
+                         st, p);
     else if (cfg == 1)
       hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 32, 4, 2, true>), g, dim3(256), 0, st, p);
     else if (cfg == 2)
       hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32, 4, 2, true>), g, dim3(256), 0, st, p);
     else if (cfg == 3)
-      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true>), g, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true, false, false>), g, dim3(256), 0,
+                         st, p);
     else if constexpr (AK && BKM)
-      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 3, 4, true>), g, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 3, 4, true, false, false>), g, dim3(256), 0,
+                         st, p);
     else
-      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true>), g, dim3(256), 0, st, p);
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, true, false, false>), g, dim3(256), 0,
+                         st, p);
     return;
   }
   if (cfg == 0)
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16>), g, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 2, 2, 16, 4, 2, false, false, false>), g, dim3(256), 0, st,
+                       p);
   else if (cfg == 1)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 32>), g, dim3(256), 0, st, p);
   else if (cfg == 2)
     hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 1, 4, 1, 1, 32>), g, dim3(256), 0, st, p);
   else if (cfg == 3)
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3>), g, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, false, false, false>), g, dim3(256), 0, st,
+                       p);
   else if constexpr (AK && BKM)  // four per CU: K-major operands only (no k-row windows)
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 3, 4>), g, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 3, 4, false, false, false>), g, dim3(256), 0, st,
+                       p);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3>), g, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKM, 2, 2, 1, 2, 16, 4, 3, false, false, false>), g, dim3(256), 0, st,
+                       p);
 }
 
 // whether the calling thread's last launch_gemm ran stream-K (its k ranges cut
@@ -1016,6 +1164,7 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(!p.c2 || (p.N1 >= 0 && p.epi != kEpiL2Norm && p.epi != kEpiPartial), kErrArg,
              "gemm: split output needs N1 and a store/accumulate epilogue");
   PS_REQUIRE(p.epi != kEpiL2Norm || p.N <= 128, kErrArg, "gemm: L2-norm epilogue needs N <= 128");
+  PS_REQUIRE(!(p.mask && p.epi == kEpiAccum), kErrArg, "gemm: a mask with an accumulate epilogue");
   PS_REQUIRE(p.epi != kEpiPartial || (!p.M_dev && !p.c_idx), kErrArg,
              "gemm: split-K partials need a static M");
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
@@ -1050,9 +1199,10 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
     // whose 32-row tiles leave most slots idle (a lone workgroup per CU runs
     // ~1 us per k-step); the per-piece fill / publish / combine (~8 us) eats
     // the gain on short K and on launches that already fill the chip
+    // (the kernels of cfg 1 and 2 carry the schedule: gemm_f32_kernel's SK)
     const int skc = p.stream_k == 1 ? (p.cfg >= 0 ? p.cfg : 1) : 2;
     const int64_t tiles_max = (int64_t)((Mmax + kCfgBM[skc] - 1) / kCfgBM[skc]) * tiles_n;
-    if (skc != 0 && tiles_max <= p.sk_cnt_len) {
+    if ((skc == 1 || skc == 2) && tiles_max <= p.sk_cnt_len) {
       if (p.stream_k == 1) {
         sk = true;
       } else if (p.cfg < 0) {

@@ -32,7 +32,8 @@ def vp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_idx=False, presplit=False):
+def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_idx=False, presplit=False,
+        graph=False):
     # M,N,K,ak,bk[,gather[,splits]]: gather = rows of A (K-major A) or k-rows
     # of B (N-major B, the weight-gradient form); splits > 1 = split-K slabs
     M, N, K, ak, bk, *g = [int(x) for x in shape.split(",")]
@@ -77,11 +78,29 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_
     ai = 2 if presplit else 7  # position of a_idx
     all_args = [tuple(vp(ix) if i == ai else a for i, a in enumerate(args)) for ix in idx_sets] \
         if idx_sets[0] is not None else [args]
-    e0.record(stream)
-    for r in range(reps):
-        call(*all_args[r % len(all_args)])
-    e1.record(stream)
-    torch.cuda.synchronize()
+    if graph:  # the reps captured once and replayed: device time without the host's launch rate
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                cs = ctypes.c_void_p(side.cuda_stream)
+                for r in range(reps):
+                    a = all_args[r % len(all_args)]
+                    call(*(a[:-1] + (cs,)))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record(stream)
+        g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+    else:
+        e0.record(stream)
+        for r in range(reps):
+            call(*all_args[r % len(all_args)])
+        e1.record(stream)
+        torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     return us, 2.0 * M * N * K / us / 1e6, err
 
@@ -96,6 +115,7 @@ def main():
     ap.add_argument("--sets", type=int, default=1, help="row sets cycled over repetitions")
     ap.add_argument("--bias-act", action="store_true", help="bias + LeakyReLU epilogue (the Q projection)")
     ap.add_argument("--sorted", action="store_true", help="gathered rows in ascending order")
+    ap.add_argument("--graph", action="store_true", help="time a hipGraph of the reps (no host launch rate)")
     ap.add_argument("--prec", default="1",
                     help="product arithmetic(s): 0 fp32 MFMA, 1 split bf16, 2 split bf16 with pre-split B planes")
     a = ap.parse_args()
@@ -109,7 +129,7 @@ def main():
                 if sk == 1 and cfg == 0:
                     continue
                 us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets, a.bias_act, a.sorted,
-                                  presplit=prec == 2)
+                                  presplit=prec == 2, graph=a.graph)
                 print(f"{s:24s} prec={prec} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
                       flush=True)
 

@@ -1,0 +1,18 @@
+# Round 4: 16-B epilogue stores -- probe, GEMM + parity tests, microbench, C2 / C4 lines
+set -o pipefail
+out=gpurun_out/r4epi2
+mkdir -p $out
+PINSAGE_LIB=probe/libpinsage_hip.so timeout -k 10 120 python tools/gemm_bench.py --prec 1 --cfgs 3 --sk 0 --reps 6 --bias-act --shapes 64,128,32,1,1 2600,512,128,1,1 > $out/probe.txt 2>&1 || { tail $out/probe.txt; exit 1; }
+grep probe $out/probe.txt | sort | uniq -c | sort -rn | head -8
+timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_parity.py tests/test_gpu_micro.py -m gpu -x -q --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
+tail -1 $out/tests.log
+timeout -k 10 300 python tools/gemm_bench.py --graph --prec 1 --cfgs 1,3 --sk 0 --reps 40 --bias-act --shapes 64,128,32,1,1 2600,512,128,1,1 10541,512,512,1,1 23289,512,128,1,1 > $out/g.txt 2>&1 || { tail $out/g.txt; exit 1; }
+cat $out/g.txt
+timeout -k 10 300 python tools/gemm_bench.py --graph --prec 1 --cfgs 1,3 --sk 0 --reps 40 --shapes 5709,512,128,1,0,0 2600,128,512,1,0,0 > $out/g2.txt 2>&1 || { tail $out/g2.txt; exit 1; }
+cat $out/g2.txt
+timeout -k 10 150 python bench.py --no-cpu-baseline > $out/c2.json 2>$out/c2.err || { tail $out/c2.err; exit 1; }
+timeout -k 10 200 python bench.py --no-cpu-baseline --config c4 > $out/c4.json 2>$out/c4.err || { tail $out/c4.err; exit 1; }
+echo ok1
+PINSAGE_FUSED_NEXT_Q=1 timeout -k 10 150 python bench.py --no-cpu-baseline > $out/c2_nq.json 2>$out/c2_nq.err || { tail $out/c2_nq.err; exit 1; }
+PINSAGE_FUSED_NEXT_Q=1 timeout -k 10 200 python bench.py --no-cpu-baseline --config c4 > $out/c4_nq.json 2>$out/c4_nq.err || { tail $out/c4_nq.err; exit 1; }
+echo ok2

@@ -1,0 +1,7 @@
+# Round 4: Q projection with and without gathered A rows (latency of the row gather)
+set -o pipefail
+out=gpurun_out/r4gath
+mkdir -p $out
+timeout -k 10 300 python tools/gemm_bench.py --prec 1 --cfgs 0,1,3 --sk 0 --reps 30 --pool 100000 --sorted --bias-act --shapes 10541,512,512,1,1,1 10541,512,512,1,1,0 2600,512,128,1,1,1 2600,512,128,1,1,0 10541,512,512,1,0,0 > $out/q0.txt 2>&1 || { tail $out/q0.txt; exit 1; }
+cat $out/q0.txt
+echo ok
