@@ -252,7 +252,11 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   const int N = p.N;
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int splits = p.epi == kEpiPartial ? p.splits : 1;
-  const int kchunk = (((K + splits - 1) / splits) + BK - 1) / BK * BK;
+  // split-K chunks on a 32-k grid whatever the stage depth (BK 16 or 32): the
+  // cut points -- and with them every slab's summation order -- are the same
+  // for every tile config, so the tuner's choice cannot change the gradient
+  static_assert(32 % BK == 0, "split-K chunks are whole stages");
+  const int kchunk = (((K + splits - 1) / splits) + 31) / 32 * 32;
   const int32_t* idxA = GA ? p.a_idx : nullptr;
   const int32_t* idxB = GB ? p.b_idx : nullptr;
   const int32_t* idxB2 = GB ? p.b2_idx : nullptr;

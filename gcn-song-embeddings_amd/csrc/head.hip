@@ -8,9 +8,11 @@
 // node), so the kernels are latency-bound; what they save is launches and
 // round trips, not FLOPs.
 //
-// MFMA convention as in gemm.hip (v_mfma_f32_32x32x2_f32): in the r-th MFMA of
-// k-octet s, lane (l32, h) supplies k = 8s + 4h + r; accumulator element r of
-// lane (l32, h) is row (r & 3) + 8 (r >> 2) + 4h, column l32 of the 32 x 32 tile.
+// MFMA conventions as in gemm.hip: exact fp32 (v_mfma_f32_32x32x2_f32: in the
+// r-th MFMA of k-octet s, lane (l32, h) supplies k = 8s + 4h + r) or split bf16
+// (head_mm_bf); accumulator element r of lane (l32, h) is row (r & 3) + 8 (r >>
+// 2) + 4h, column l32 of the 32 x 32 tile.
+#include "bf16split.h"
 #include "common.h"
 
 namespace ps {
@@ -36,8 +38,8 @@ __device__ __forceinline__ float4 head_bfrag(const float* sW, int n, int k4) {
   }
 }
 template <bool kNK>
-__device__ __forceinline__ f32x16 head_mm(const float* sA, const float* sW, int n0, int l32,
-                                          int h) {
+__device__ __forceinline__ f32x16 head_mm_f32(const float* sA, const float* sW, int n0, int l32,
+                                              int h) {
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -61,6 +63,51 @@ __device__ __forceinline__ f32x16 head_mm(const float* sA, const float* sW, int 
     b = bn;
   }
   return acc;
+}
+
+// The same product with split-bf16 MFMAs (the GEMMs' arithmetic, gemm.hip):
+// each fp32 operand = hi + mid + lo bf16, six v_mfma_f32_32x32x16_bf16 per
+// 16-k step, smallest products first; lane (l32, h) supplies k = 16 s + 8 h
+// + [0, 8).  48 MFMAs of 32 cycles per wave against 64 f32 MFMAs of 64:
+// the head's two row-block products were a third of its kernels' time at C2.
+template <bool kNK>
+__device__ __forceinline__ f32x16 head_mm_bf(const float* sA, const float* sW, int n0, int l32, int h) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const float* arow = sA + l32 * kHeadLd + 8 * h;
+  const int n = n0 + l32;
+#pragma unroll 2
+  for (int s = 0; s < kHeadDim / 16; ++s) {
+    const float4 a0 = *reinterpret_cast<const float4*>(arow + 16 * s);
+    const float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * s + 4);
+    float4 b0, b1;
+    if constexpr (kNK) {
+      b0 = *reinterpret_cast<const float4*>(sW + n * kHeadLd + 16 * s + 8 * h);
+      b1 = *reinterpret_cast<const float4*>(sW + n * kHeadLd + 16 * s + 8 * h + 4);
+    } else {
+      const float* c = sW + (16 * s + 8 * h) * kHeadLd + n;
+      b0 = make_float4(c[0], c[kHeadLd], c[2 * kHeadLd], c[3 * kHeadLd]);
+      b1 = make_float4(c[4 * kHeadLd], c[5 * kHeadLd], c[6 * kHeadLd], c[7 * kHeadLd]);
+    }
+    bf16x8 aH, aM, aL, bH, bM, bL;
+    split3(a0, a1, aH, aM, aL);
+    split3(b0, b1, bH, bM, bL);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
+  }
+  return acc;
+}
+// products in the GEMMs' default arithmetic (gemm_default_prec: 1 split bf16,
+// 0 exact fp32 MFMA), a kernel template parameter chosen per launch
+template <bool kNK, bool BF>
+__device__ __forceinline__ f32x16 head_mm(const float* sA, const float* sW, int n0, int l32, int h) {
+  if constexpr (BF) return head_mm_bf<kNK>(sA, sW, n0, l32, h);
+  else return head_mm_f32<kNK>(sA, sW, n0, l32, h);
 }
 
 // rows [r0, r0+32) of src[R][o] -> sA (zero outside), all threads
@@ -103,6 +150,7 @@ __device__ __forceinline__ void head_load_weight(float* sW, const float* __restr
 __device__ __forceinline__ int head_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // H1 = lrelu(y G1^T + b1), Z = H1 G2^T over the *nrows rows of y
+template <bool BF>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int o,
                                                        const int* __restrict__ nrows,
                                                        const float* __restrict__ G1w,
@@ -123,7 +171,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   head_load_weight(sW1, G1w, o, tid);
   head_load_weight(sW2, G2w, o, tid);
   __syncthreads();
-  f32x16 acc = head_mm<true>(sA, sW1, n0, l32, h);
+  f32x16 acc = head_mm<true, BF>(sA, sW1, n0, l32, h);
   const float b = col < o ? G1b[col] : 0.f;
   __syncthreads();  // every wave is done reading y from sA
 #pragma unroll
@@ -134,7 +182,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     if (r0 + row < R && col < o) H1[(r0 + row) * o + col] = v;
   }
   __syncthreads();
-  acc = head_mm<true>(sA, sW2, n0, l32, h);
+  acc = head_mm<true, BF>(sA, sW2, n0, l32, h);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = head_row(r, h);
@@ -191,6 +239,7 @@ __device__ __forceinline__ void head_load_dz(float* sA, float* __restrict__ G, i
 // dP1 G1; then the top conv layer's normalisation backward (y = u / ||u||,
 // u = lrelu(pre)):  dp = lrelu'(y) * (dY - y (y . dY)) / ||u||.  The block
 // zeroes the multiplicity counters of its rows once every thread has read them.
+template <bool BF>
 __global__ __launch_bounds__(256) void head_bwd_kernel(
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ dZ, int o,
     const int* __restrict__ nrows, const float* __restrict__ H1, const float* __restrict__ G1w,
@@ -224,7 +273,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const int q = tid / kHeadRows, row = tid % kHeadRows;
     if (r0 + row < R) Kc[q * S_max + r0 + row] = 0;
   }
-  f32x16 acc = head_mm<false>(sA, sW2, n0, l32, h);
+  f32x16 acc = head_mm<false, BF>(sA, sW2, n0, l32, h);
   __syncthreads();  // every wave is done reading dZ from sA
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -237,7 +286,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     sA[row * kHeadLd + col] = v;
   }
   __syncthreads();
-  acc = head_mm<false>(sA, sW1, n0, l32, h);  // dY
+  acc = head_mm<false, BF>(sA, sW1, n0, l32, h);  // dY
   // row dots y . dY: lane-partial over this wave's 32 columns, then 4 waves
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -262,12 +311,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 constexpr size_t kHeadFwdLds = (size_t)(kHeadRows + 2 * kHeadDim) * kHeadLd * 4;
 constexpr size_t kHeadBwdLds = kHeadFwdLds + 4 * kHeadRows * 4;
 
+int gemm_default_prec();
+
 static int head_prepare() {
   static int rc = [] {
-    if (hipFuncSetAttribute((const void*)head_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kHeadFwdLds) != hipSuccess ||
-        hipFuncSetAttribute((const void*)head_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kHeadBwdLds) != hipSuccess)
+    auto lds = [](const void* f, size_t b) {
+      return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess;
+    };
+    if (!lds((const void*)head_fwd_kernel<true>, kHeadFwdLds) || !lds((const void*)head_fwd_kernel<false>, kHeadFwdLds) ||
+        !lds((const void*)head_bwd_kernel<true>, kHeadBwdLds) || !lds((const void*)head_bwd_kernel<false>, kHeadBwdLds))
       return (int)kErrHip;
     return (int)kOk;
   }();
@@ -282,8 +334,12 @@ int launch_head_fwd(const float* y, int o, const int* nrows, int64_t max_rows, c
   PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                     kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
+  if (gemm_default_prec() == 1)
+    hipLaunchKernelGGL(head_fwd_kernel<true>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                       kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<false>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                       kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -294,8 +350,12 @@ int launch_head_bwd(float* G, int* Kc, int64_t S_max, float* dZ, int o, const in
   PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
+  if (gemm_default_prec() == 1)
+    hipLaunchKernelGGL(head_bwd_kernel<true>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                       kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<false>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                       kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
   PS_CHECK_LAUNCH();
   return kOk;
 }
