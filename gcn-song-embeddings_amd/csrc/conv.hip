@@ -754,6 +754,81 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
     dsc = chunks[wid];
     if (lane < kDqChunk) oc = occ2[wid * kDqChunk + lane];
   }
+  if (!CM && h4 <= 64 * VEC) {
+    // One column pass per chunk: each chunk's result is stored only after the
+    // NEXT chunk's rows have been issued.  vmcnt counts stores and loads in
+    // issue order, so rows loaded behind a store also waited for it: every
+    // chunk paid a store round trip before its loads could land.
+    float4 pend[VEC];
+    float4* pend_o = nullptr;
+    for (int64_t ci = wid; ci < nch; ci += nw) {
+      int2 dsc_n = make_int2(0, 0), oc_n = make_int2(0, 0);
+      if (ci + nw < nch) {
+        dsc_n = chunks[ci + nw];
+        if (lane < kDqChunk) oc_n = occ2[(ci + nw) * kDqChunk + lane];
+      }
+      const int u = dsc.x, n = dsc.y & 0xff;
+      const bool split = (dsc.y & kDqSplit) != 0;
+      const int32_t my_row = oc.x;
+      const float my_w = __int_as_float(oc.y);
+      float4 qv[VEC], x[kDqChunk][VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) qv[v] = reinterpret_cast<const float4*>(q + (int64_t)u * hid)[min(v * 64 + lane, h4 - 1)];
+      const int ng = (n + 3) >> 2;
+#pragma unroll
+      for (int g = 0; g < kDqChunk / 4; ++g) {
+        if (g < ng) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * g + jj;
+            const int32_t row = __shfl(my_row, min(j, n - 1), 64);
+            const float4* dr = reinterpret_cast<const float4*>(dagg + (int64_t)row * ld_dagg);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) x[j][v] = dr[min(v * 64 + lane, h4 - 1)];
+          }
+        }
+      }
+      if (pend_o) {  // the previous chunk's result, behind this chunk's loads
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
+      }
+      float4 acc[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int g = 0; g < kDqChunk / 4; ++g) {
+        if (g < ng) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * g + jj;
+            const float w = j < n ? __shfl(my_w, j, 64) : 0.f;
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+              acc[v].x = fmaf(w, x[j][v].x, acc[v].x);
+              acc[v].y = fmaf(w, x[j][v].y, acc[v].y);
+              acc[v].z = fmaf(w, x[j][v].z, acc[v].z);
+              acc[v].w = fmaf(w, x[j][v].w, acc[v].w);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+        pend[v] = split ? acc[v]
+                        : make_float4(acc[v].x * lrelu_grad(qv[v].x), acc[v].y * lrelu_grad(qv[v].y),
+                                      acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
+      pend_o = reinterpret_cast<float4*>(split ? part + ci * hid : dpq + (int64_t)u * hid);
+      dsc = dsc_n;
+      oc = oc_n;
+    }
+    if (pend_o) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+        if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
+    }
+    return;
+  }
   for (int64_t ci = wid; ci < nch; ci += nw) {
     int2 dsc_n = make_int2(0, 0), oc_n = make_int2(0, 0);
     if (ci + nw < nch) {  // the next chunk's descriptor and pairs, under this one
@@ -908,12 +983,6 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
                                                              int* __restrict__ zi, int64_t zi_n) {
   const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t gs = (int64_t)gridDim.x * blockDim.x;
-  if (z) {
-    const int64_t zn = (int64_t)(*z_rows) * z_n;
-    for (int64_t i = gt; i < zn; i += gs) z[i] = 0.f;
-  }
-  if (zi)
-    for (int64_t i = gt; i < zi_n; i += gs) zi[i] = 0;
   const int64_t R = nrows ? (int64_t)*nrows : n_static;
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -928,6 +997,13 @@ __global__ __launch_bounds__(256) void norm_lrelu_bwd_kernel(const float* __rest
       dp[r * n + c] = lrelu_grad(yy) * (dy[r * n + c] - yy * dot) * inv;
     }
   }
+  // the zeroing after the rows: loads issued behind stores wait for them
+  if (z) {
+    const int64_t zn = (int64_t)(*z_rows) * z_n;
+    for (int64_t i = gt; i < zn; i += gs) z[i] = 0.f;
+  }
+  if (zi)
+    for (int64_t i = gt; i < zi_n; i += gs) zi[i] = 0;
 }
 
 // In-place row L2 normalisation of y [n][out] (the W projection's last step,

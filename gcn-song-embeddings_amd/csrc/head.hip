@@ -8,11 +8,9 @@
 // node), so the kernels are latency-bound; what they save is launches and
 // round trips, not FLOPs.
 //
-// MFMA conventions as in gemm.hip: exact fp32 (v_mfma_f32_32x32x2_f32: in the
-// r-th MFMA of k-octet s, lane (l32, h) supplies k = 8s + 4h + r) or split bf16
-// (head_mm_bf); accumulator element r of lane (l32, h) is row (r & 3) + 8 (r >>
-// 2) + 4h, column l32 of the 32 x 32 tile.
-#include "bf16split.h"
+// MFMA convention as in gemm.hip (v_mfma_f32_32x32x2_f32): in the r-th MFMA of
+// k-octet s, lane (l32, h) supplies k = 8s + 4h + r; accumulator element r of
+// lane (l32, h) is row (r & 3) + 8 (r >> 2) + 4h, column l32 of the 32 x 32 tile.
 #include "common.h"
 
 namespace ps {
@@ -38,8 +36,8 @@ __device__ __forceinline__ float4 head_bfrag(const float* sW, int n, int k4) {
   }
 }
 template <bool kNK>
-__device__ __forceinline__ f32x16 head_mm_f32(const float* sA, const float* sW, int n0, int l32,
-                                              int h) {
+__device__ __forceinline__ f32x16 head_mm(const float* sA, const float* sW, int n0, int l32,
+                                          int h) {
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -65,83 +63,46 @@ __device__ __forceinline__ f32x16 head_mm_f32(const float* sA, const float* sW, 
   return acc;
 }
 
-// The same product with split-bf16 MFMAs (the GEMMs' arithmetic, gemm.hip):
-// each fp32 operand = hi + mid + lo bf16, six v_mfma_f32_32x32x16_bf16 per
-// 16-k step, smallest products first; lane (l32, h) supplies k = 16 s + 8 h
-// + [0, 8).  48 MFMAs of 32 cycles per wave against 64 f32 MFMAs of 64:
-// the head's two row-block products were a third of its kernels' time at C2.
-template <bool kNK>
-__device__ __forceinline__ f32x16 head_mm_bf(const float* sA, const float* sW, int n0, int l32, int h) {
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const float* arow = sA + l32 * kHeadLd + 8 * h;
-  const int n = n0 + l32;
-#pragma unroll 2
-  for (int s = 0; s < kHeadDim / 16; ++s) {
-    const float4 a0 = *reinterpret_cast<const float4*>(arow + 16 * s);
-    const float4 a1 = *reinterpret_cast<const float4*>(arow + 16 * s + 4);
-    float4 b0, b1;
-    if constexpr (kNK) {
-      b0 = *reinterpret_cast<const float4*>(sW + n * kHeadLd + 16 * s + 8 * h);
-      b1 = *reinterpret_cast<const float4*>(sW + n * kHeadLd + 16 * s + 8 * h + 4);
-    } else {
-      const float* c = sW + (16 * s + 8 * h) * kHeadLd + n;
-      b0 = make_float4(c[0], c[kHeadLd], c[2 * kHeadLd], c[3 * kHeadLd]);
-      b1 = make_float4(c[4 * kHeadLd], c[5 * kHeadLd], c[6 * kHeadLd], c[7 * kHeadLd]);
-    }
-    bf16x8 aH, aM, aL, bH, bM, bL;
-    split3(a0, a1, aH, aM, aL);
-    split3(b0, b1, bH, bM, bL);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
-  }
-  return acc;
-}
-// products in the GEMMs' default arithmetic (gemm_default_prec: 1 split bf16,
-// 0 exact fp32 MFMA), a kernel template parameter chosen per launch
-template <bool kNK, bool BF>
-__device__ __forceinline__ f32x16 head_mm(const float* sA, const float* sW, int n0, int l32, int h) {
-  if constexpr (BF) return head_mm_bf<kNK>(sA, sW, n0, l32, h);
-  else return head_mm_f32<kNK>(sA, sW, n0, l32, h);
-}
-
 // rows [r0, r0+32) of src[R][o] -> sA (zero outside), all threads
 // (every global load of a staging pass is issued before the first LDS write:
 // one memory round trip per pass, not one per float4)
-__device__ __forceinline__ void head_load_rows(float* sA, const float* __restrict__ src, int64_t r0,
-                                               int64_t R, int o, int tid) {
+__device__ __forceinline__ void head_fetch_rows(float4 (&v)[kHeadRows * (kHeadDim / 4) / 256],
+                                                const float* __restrict__ src, int64_t r0, int64_t R, int o,
+                                                int tid) {
   constexpr int NI = kHeadRows * (kHeadDim / 4) / 256;
-  float4 v[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
     v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (r0 + row < R && c < o) v[j] = *reinterpret_cast<const float4*>(src + (r0 + row) * o + c);
   }
+}
+__device__ __forceinline__ void head_put_rows(float* sA, const float4 (&v)[kHeadRows * (kHeadDim / 4) / 256],
+                                              int tid) {
+  constexpr int NI = kHeadRows * (kHeadDim / 4) / 256;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
     *reinterpret_cast<float4*>(sA + row * kHeadLd + c) = v[j];
   }
 }
-// W[o][o] row-major -> sW (same layout, zero padded to 128 x 128)
-__device__ __forceinline__ void head_load_weight(float* sW, const float* __restrict__ W, int o,
-                                                 int tid) {
-  constexpr int NI = kHeadDim * (kHeadDim / 4) / 256;
-  float4 v[NI];
+// W[o][o] row-major -> sW (same layout, zero padded to 128 x 128), in two
+// halves: the loads into registers (head_fetch_weight), then the LDS writes
+// (head_put_weight) -- a kernel issues all of its global loads before its
+// first store or LDS write, so its staging costs one memory round trip
+constexpr int kHeadWNI = kHeadDim * (kHeadDim / 4) / 256;
+__device__ __forceinline__ void head_fetch_weight(float4 (&v)[kHeadWNI], const float* __restrict__ W, int o,
+                                                  int tid) {
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
+  for (int j = 0; j < kHeadWNI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
     v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row < o && c < o) v[j] = *reinterpret_cast<const float4*>(W + (int64_t)row * o + c);
   }
+}
+__device__ __forceinline__ void head_put_weight(float* sW, const float4 (&v)[kHeadWNI], int tid) {
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
+  for (int j = 0; j < kHeadWNI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
     *reinterpret_cast<float4*>(sW + row * kHeadLd + c) = v[j];
   }
@@ -150,7 +111,6 @@ __device__ __forceinline__ void head_load_weight(float* sW, const float* __restr
 __device__ __forceinline__ int head_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // H1 = lrelu(y G1^T + b1), Z = H1 G2^T over the *nrows rows of y
-template <bool BF>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ y, int o,
                                                        const int* __restrict__ nrows,
                                                        const float* __restrict__ G1w,
@@ -167,12 +127,17 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   if (r0 >= R) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = 32 * w, col = n0 + l32;
-  head_load_rows(sA, y, r0, R, o, tid);
-  head_load_weight(sW1, G1w, o, tid);
-  head_load_weight(sW2, G2w, o, tid);
-  __syncthreads();
-  f32x16 acc = head_mm<true, BF>(sA, sW1, n0, l32, h);
+  // every global load first (rows, both weights, the bias), then the LDS writes
+  float4 yr[kHeadRows * (kHeadDim / 4) / 256], w1[kHeadWNI], w2[kHeadWNI];
+  head_fetch_rows(yr, y, r0, R, o, tid);
+  head_fetch_weight(w1, G1w, o, tid);
+  head_fetch_weight(w2, G2w, o, tid);
   const float b = col < o ? G1b[col] : 0.f;
+  head_put_rows(sA, yr, tid);
+  head_put_weight(sW1, w1, tid);
+  head_put_weight(sW2, w2, tid);
+  __syncthreads();
+  f32x16 acc = head_mm<true>(sA, sW1, n0, l32, h);
   __syncthreads();  // every wave is done reading y from sA
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -182,7 +147,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
     if (r0 + row < R && col < o) H1[(r0 + row) * o + col] = v;
   }
   __syncthreads();
-  acc = head_mm<true, BF>(sA, sW2, n0, l32, h);
+  acc = head_mm<true>(sA, sW2, n0, l32, h);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = head_row(r, h);
@@ -197,12 +162,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // block is loaded in one round; the block then zeroes what it read (the next
 // step's loss accumulates into zeros).  K[c][r] = 0 means G[c][r] is +0, so the
 // terms it adds change nothing (bitwise the old dZ = sum over k != 0).
-__device__ __forceinline__ void head_load_dz(float* sA, float* __restrict__ G, int* __restrict__ Kc,
-                                             int64_t S_max, float* __restrict__ dZ, int64_t r0, int64_t R,
-                                             int o, int tid) {
-  constexpr int NI = kHeadRows * (kHeadDim / 4) / 256;
-  float4 g[3][NI];
-  int k[3][NI];
+constexpr int kHeadRNI = kHeadRows * (kHeadDim / 4) / 256;
+__device__ __forceinline__ void head_fetch_dz(float4 (&g)[3][kHeadRNI], int (&k)[3][kHeadRNI],
+                                              const float* __restrict__ G, const int* __restrict__ Kc,
+                                              int64_t S_max, int64_t r0, int64_t R, int o, int tid) {
+  constexpr int NI = kHeadRNI;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
@@ -214,6 +178,11 @@ __device__ __forceinline__ void head_load_dz(float* sA, float* __restrict__ G, i
                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+}
+__device__ __forceinline__ void head_put_dz(float* sA, float* __restrict__ G, const float4 (&g)[3][kHeadRNI],
+                                            const int (&k)[3][kHeadRNI], int64_t S_max, float* __restrict__ dZ,
+                                            int64_t r0, int64_t R, int o, int tid) {
+  constexpr int NI = kHeadRNI;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
@@ -239,7 +208,6 @@ __device__ __forceinline__ void head_load_dz(float* sA, float* __restrict__ G, i
 // dP1 G1; then the top conv layer's normalisation backward (y = u / ||u||,
 // u = lrelu(pre)):  dp = lrelu'(y) * (dY - y (y . dY)) / ||u||.  The block
 // zeroes the multiplicity counters of its rows once every thread has read them.
-template <bool BF>
 __global__ __launch_bounds__(256) void head_bwd_kernel(
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ dZ, int o,
     const int* __restrict__ nrows, const float* __restrict__ H1, const float* __restrict__ G1w,
@@ -256,6 +224,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   if (r0 >= R) return;
   const int lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = 32 * w, col = n0 + l32;
+#ifdef PS_HEAD_PROBE  // (diagnostic build only) wall-clock phases of block 0
+  uint64_t pt[6] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0};
+  int pti = 1;
+#define PS_HPROBE() do { if (pti < 6) pt[pti++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PS_HPROBE() do { } while (0)
+#endif
   // this lane's H1 (mask) and y values, fetched beside the staging loads
   float hv[16], yv[16];
 #pragma unroll
@@ -265,15 +240,32 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     hv[r] = ok ? H1[(r0 + row) * o + col] : 0.f;
     yv[r] = ok ? y[(r0 + row) * o + col] : 0.f;
   }
-  head_load_dz(sA, G, Kc, S_max, dZ, r0, R, o, tid);
-  head_load_weight(sW2, G2w, o, tid);
-  head_load_weight(sW1, G1w, o, tid);
+  // every global load first (the loss accumulators, both weights, the norms),
+  // then the stores and LDS writes: a load issued behind a store waits for it
+  // (vmcnt counts both), which made this staging ~10 us of the kernel's ~21
+  float4 g[3][kHeadRNI], w1[kHeadWNI], w2[kHeadWNI];
+  int k[3][kHeadRNI];
+  head_fetch_dz(g, k, G, Kc, S_max, r0, R, o, tid);
+  head_fetch_weight(w2, G2w, o, tid);
+  head_fetch_weight(w1, G1w, o, tid);
+  float inv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = head_row(r, h);
+    inv[r] = r0 + row < R ? nrm[r0 + row] : 1.f;
+  }
+  head_put_dz(sA, G, g, k, S_max, dZ, r0, R, o, tid);
+  head_put_weight(sW2, w2, tid);
+  head_put_weight(sW1, w1, tid);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) inv[r] = 1.f / inv[r];
   __syncthreads();
+  PS_HPROBE();
   if (tid < 3 * kHeadRows) {  // every K of the block's rows has been read
     const int q = tid / kHeadRows, row = tid % kHeadRows;
     if (r0 + row < R) Kc[q * S_max + r0 + row] = 0;
   }
-  f32x16 acc = head_mm<false, BF>(sA, sW2, n0, l32, h);
+  f32x16 acc = head_mm<false>(sA, sW2, n0, l32, h);
   __syncthreads();  // every wave is done reading dZ from sA
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -286,7 +278,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     sA[row * kHeadLd + col] = v;
   }
   __syncthreads();
-  acc = head_mm<false, BF>(sA, sW1, n0, l32, h);  // dY
+  PS_HPROBE();
+  acc = head_mm<false>(sA, sW1, n0, l32, h);  // dY
+  PS_HPROBE();
   // row dots y . dY: lane-partial over this wave's 32 columns, then 4 waves
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -302,24 +296,27 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const int row = head_row(r, h);
     if (r0 + row < R && col < o) {
       const float dot = (red[row] + red[kHeadRows + row]) + (red[2 * kHeadRows + row] + red[3 * kHeadRows + row]);
-      const float inv = 1.f / nrm[r0 + row];
-      dp[(r0 + row) * o + col] = lrelu_grad(yv[r]) * (acc[r] - yv[r] * dot) * inv;
+      dp[(r0 + row) * o + col] = lrelu_grad(yv[r]) * (acc[r] - yv[r] * dot) * inv[r];
     }
   }
+#ifdef PS_HEAD_PROBE
+  __syncthreads();
+  PS_HPROBE();
+  if (blockIdx.x == 0 && tid == 0)
+    printf("head_bwd probe [10ns]: loads %d mm1+dP1 %d mm2 %d tail %d\n", (int)(pt[1] - pt[0]),
+           (int)(pt[2] - pt[1]), (int)(pt[3] - pt[2]), (int)(pt[4] - pt[3]));
+#endif
 }
 
 constexpr size_t kHeadFwdLds = (size_t)(kHeadRows + 2 * kHeadDim) * kHeadLd * 4;
 constexpr size_t kHeadBwdLds = kHeadFwdLds + 4 * kHeadRows * 4;
 
-int gemm_default_prec();
-
 static int head_prepare() {
   static int rc = [] {
-    auto lds = [](const void* f, size_t b) {
-      return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess;
-    };
-    if (!lds((const void*)head_fwd_kernel<true>, kHeadFwdLds) || !lds((const void*)head_fwd_kernel<false>, kHeadFwdLds) ||
-        !lds((const void*)head_bwd_kernel<true>, kHeadBwdLds) || !lds((const void*)head_bwd_kernel<false>, kHeadBwdLds))
+    if (hipFuncSetAttribute((const void*)head_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kHeadFwdLds) != hipSuccess ||
+        hipFuncSetAttribute((const void*)head_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kHeadBwdLds) != hipSuccess)
       return (int)kErrHip;
     return (int)kOk;
   }();
@@ -334,12 +331,8 @@ int launch_head_fwd(const float* y, int o, const int* nrows, int64_t max_rows, c
   PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
-  if (gemm_default_prec() == 1)
-    hipLaunchKernelGGL(head_fwd_kernel<true>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                       kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
-  else
-    hipLaunchKernelGGL(head_fwd_kernel<false>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                       kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                     kHeadFwdLds, st, y, o, nrows, G1w, G1b, G2w, H1, Z);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -350,12 +343,8 @@ int launch_head_bwd(float* G, int* Kc, int64_t S_max, float* dZ, int o, const in
   PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
-  if (gemm_default_prec() == 1)
-    hipLaunchKernelGGL(head_bwd_kernel<true>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                       kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
-  else
-    hipLaunchKernelGGL(head_bwd_kernel<false>, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                       kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
+                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
   PS_CHECK_LAUNCH();
   return kOk;
 }
