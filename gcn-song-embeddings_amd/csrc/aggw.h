@@ -28,6 +28,10 @@ int agg_wf_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
 int64_t agg_wf_planes_bytes(int64_t d, int64_t hid);
 // the fragment form's rows per tile (16 or 32) for an expected row count
 int agg_wf_rows(int64_t S_max);
+// whether fusing the next layer's Q projection (AggNextQ) is expected to pay
+// at S_est rows: the 32-row form runs and its tiles fit one pass over the CUs
+// (the fused products lengthen every tile; a second pass of tiles doubles that)
+int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est);
 // W [128][K] -> fragment-order planes for the rows form `rows`
 int launch_split_wfrag(const float* W, int64_t ldw, int K, int rows, uint16_t* planes, hipStream_t st);
 // next (optional): fuse the next layer's Q projection; *next_done is set to 1

@@ -811,6 +811,24 @@ int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
          T >= 1 && T <= kAwTMax && 2 * lds <= 160 * 1024;
 }
 
+static int64_t aggw_min_rows32(int cus) {
+  return getenv("PINSAGE_AGGW32_MIN_ROWS") ? atoll(getenv("PINSAGE_AGGW32_MIN_ROWS")) : 16 * (int64_t)cus;
+}
+
+static int device_cus() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  return cus;
+}
+
+int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est) {
+  const int cus = device_cus();
+  return S_est > 0 && S_est >= aggw_min_rows32(cus) && agg_w32_supported(d, hid, T) &&
+         (S_est + kAw32Rows - 1) / kAw32Rows <= cus;
+}
+
 // S_max: the expected row count (the frontier size hint; the kernels read the
 // actual count from nS, or take n_static when nS is null, and deal it over
 // their blocks)
@@ -840,10 +858,7 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
     prepared = 160 * 1024;
   }
   if (S_max <= 0) return kOk;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
+  const int cus = device_cus();
   // ~12 rows per block (a 16-row tile with headroom), two blocks per CU
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(2 * (int64_t)cus, (S_max + 11) / 12));
   // The 32-row form (one block per CU, W read once per 32 rows) when the rows
@@ -852,8 +867,7 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
   // C2 layer 0 (5.7k rows, K 1024) 36.5 vs 55.3 us, C4 layer 0 (8.6k, K 640)
   // 50.2 vs 73.4 us; the layers 1 (1.5-2k rows, K 640) 21.5-21.8 vs 24.7-25.3 us.
   // PINSAGE_AGGW32_MIN_ROWS overrides the switch point (A/B).
-  const int64_t min_rows32 =
-      getenv("PINSAGE_AGGW32_MIN_ROWS") ? atoll(getenv("PINSAGE_AGGW32_MIN_ROWS")) : 16 * (int64_t)cus;
+  const int64_t min_rows32 = aggw_min_rows32(cus);
   if (S_max >= min_rows32 && agg_w32_supported(d, hid, T)) {
     const int lds32 = kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
     static bool prepared32 = false;

@@ -141,13 +141,16 @@ struct Engine {
   // Q projections read their weight pre-split into bf16 planes (one small
   // split launch per layer per forward; the GEMM then converts A only)
   bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
-  // PINSAGE_FUSED_NEXT_Q=1: the next layer's Q projection inside the 32-row
-  // aggregation + W kernel (AggNextQ, aggw.h), one launch less per upper
-  // layer.  Measured slower (one session, ms/step): C2 0.439 -> 0.442 (layer
-  // 0's kernel 37.2 -> 49.7 us against the 24 us Q GEMM it replaces), C4
-  // 0.479 -> 0.485 (50.5 -> 76.0 us): each 32-row tile reads all of Q (256 KB)
-  // from L2 with little in flight per wave, so it is kept opt-in.
-  bool fused_next_q = getenv("PINSAGE_FUSED_NEXT_Q") && atoi(getenv("PINSAGE_FUSED_NEXT_Q")) != 0;
+  // The next layer's Q projection inside the 32-row aggregation + W kernel
+  // (AggNextQ, aggw.h): one launch less per upper layer, at the price of the
+  // products of every output row (not only the next layer's neighbours) and
+  // a longer tile.  Default (-1): per layer, where agg_w_next_q_pays -- the
+  // 32-row form's tiles fit one pass over the CUs.  Measured (one session,
+  // ms/step, layer 0's kernel µs): C2 (179 tiles) 0.4248/0.4296 -> 0.4194/0.4217,
+  // 36.7 -> 49.2 against the 16 µs Q GEMM it replaces; C4 (268 tiles, a second
+  // pass) 0.4645 -> 0.4665, 50.5 -> 75.2.  PINSAGE_FUSED_NEXT_Q=0 / 1 forces
+  // it off / on wherever the 32-row form runs.
+  int fused_next_q = getenv("PINSAGE_FUSED_NEXT_Q") ? atoi(getenv("PINSAGE_FUSED_NEXT_Q")) : -1;
   // PINSAGE_DQ_CHUNK_ROWS=1: the bottom layer's Q weight gradient over dq
   // chunk rows (masked per-chunk partials, h gathered per chunk) instead of
   // combined dpq rows, so the combine launch leaves the chain.  Measured (one
@@ -586,12 +589,17 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   LayerBuf& top = E.L[(size_t)Lc - 1];
   // W of every layer split once into the aggregation kernel's fragment-order
   // bf16 planes (the rows form picked by the expected frontier size)
-  std::vector<int> wf_rows((size_t)Lc, 0);
-  if (E.fused_aggw == 1 && !E.fused_next_q) {
+  std::vector<int> wf_rows((size_t)Lc, 0), next_q((size_t)Lc, 0);
+  for (int l = 0; E.fused_aggw && E.fused_next_q && l + 1 < Lc; ++l) {
+    const LayerBuf& lb = E.L[(size_t)l];
+    const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
+    next_q[(size_t)l] = E.fused_next_q > 0 || agg_w_next_q_pays(lb.d, c.hid, T, S_est);
+  }
+  if (E.fused_aggw == 1) {
     Timed ts(E, "fwd.wsplit", st);
     for (int l = 0; l < Lc; ++l) {
       LayerBuf& lb = E.L[(size_t)l];
-      if (!agg_wf_supported(lb.d, c.hid, c.out, T)) continue;
+      if (next_q[(size_t)l] || !agg_wf_supported(lb.d, c.hid, c.out, T)) continue;
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
       wf_rows[(size_t)l] = agg_wf_rows(S_est);
       PS_TRY(launch_split_wfrag(E.params + lb.pWw, lb.d + c.hid, (int)(lb.d + c.hid), wf_rows[(size_t)l],
@@ -648,7 +656,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       Timed taw(E, lname("fwd.aggw", l), st);
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
       AggNextQ nx;
-      if (E.fused_next_q && l + 1 < Lc) {  // the next layer's neighbours are rows of this y
+      if (next_q[(size_t)l]) {  // the next layer's neighbours are rows of this y
         const LayerBuf& nb = E.L[(size_t)l + 1];
         nx.S_mem = at<int32_t>(ws, lb.S.members);
         nx.bits = at<unsigned long long>(ws, nb.N.bits);

@@ -628,7 +628,9 @@ class _FusedStep:
             o = best[site][1]
             nat.check(L.pinsage_engine_set_gemm_choice(e.h, site.encode(), *(o if o else (-1, -1, 0))),
                       "set_gemm_choice")
-        self.tuned_choices = {k: {"us": v[0] * 1e3, "cfg": v[1]} for k, v in best.items()}
+        # a site that never launched (e.g. a Q GEMM fused into the layer below's
+        # kernel) keeps the size model and is left out of the record
+        self.tuned_choices = {k: {"us": v[0] * 1e3, "cfg": v[1]} for k, v in best.items() if v[1] is not None}
 
     def _load_choices(self, path):
         """Fixed per-site GEMM choices instead of the tuner (a bench line's
