@@ -408,13 +408,16 @@ def main():
             ws = tr._fused.ws if tr._fused is not None else (rn._ws if rn._ws is not None else rn.last_ws)
             cN0 = int(eng.view(ws, int(off.count_N[0]), torch.int32, 1).item())
             cS0 = int(eng.view(ws, int(off.count_S[0]), torch.int32, 1).item())
-            sizes.append((cN0, cS0))
+            cN1 = (int(eng.view(ws, int(off.count_N[1]), torch.int32, 1).item())
+                   if cfg["n_layers"] > 1 else 0)
+            sizes.append((cN0, cS0, cN1))
         kt = kernel_table(eng)
         nat.lib().pinsage_engine_timing(eng.h, 0)
         os.chdir(cwd)
 
     U0 = float(np.mean([s[0] for s in sizes]))
     F0 = float(np.mean([s[1] for s in sizes]))
+    U1 = float(np.mean([s[2] for s in sizes]))
     d, hid, T = cfg["d_in"], 512, cfg["T"]
     q_ms, q_calls = kt.get("fwd.q_gemm.l0", (0.0, 1))
     q_avg = q_ms / max(q_calls, 1)
@@ -439,6 +442,15 @@ def main():
         agg_bytes += extra
         agg_logical += extra
         agg_flops = 2.0 * F0 * (d + hid) * 128
+    # layer 1's Q projection fused into this kernel (engine.hip next_q: no
+    # fwd.q_gemm.l1 launch): every output row's product with Q1 (hid x 128) is
+    # computed, the U1 rows of layer 1's neighbour set are stored
+    next_q = fused and cfg["n_layers"] > 1 and "fwd.q_gemm.l1" not in kt
+    if next_q:
+        agg_flops += 2.0 * F0 * 128 * hid
+        nq_bytes = hid * 128 * 4 + hid * 4 + U1 * hid * 4
+        agg_bytes += nq_bytes
+        agg_logical += nq_bytes
     # committed PMC summaries are keyed by config (+ the per-GPU batch when it is not the
     # config's own, e.g. c4_b4096 = C4's global batch on one GPU)
     pmc_key = args.config if cfg["batch"] == CONFIGS[args.config]["batch"] else f"{args.config}_b{cfg['batch']}"
@@ -480,7 +492,10 @@ def main():
                      "algorithmic_per_launch": q_flops, "avg_launch_ms": q_avg,
                      "algorithmic_bytes_per_launch": 4.0 * (U0 * d + d * hid + U0 * hid)},
         "gather_kernel": {"kernel": a_site + (" (weighted aggregation + [h_self || agg] W projection, "
-                                              "bias, lrelu, row L2 norm in one launch)" if fused else ""),
+                                              "bias, lrelu, row L2 norm in one launch"
+                                              + (", + layer 1's Q projection of its rows" if next_q else "")
+                                              + ")" if fused else ""),
+                          "fused_next_q": next_q,
                           "bound": "hbm", "avg_launch_ms": a_avg,
                           "achieved_GBs": agg_bytes / (a_avg * 1e-3) / 1e9 if a_avg > 0 else 0.0,
                           "peak_GBs": PEAK_HBM_GBS, "frac": (agg_bytes / (a_avg * 1e-3) / 1e9 / PEAK_HBM_GBS
@@ -502,9 +517,11 @@ def main():
                                                    / a_avg if a_avg > 0 else 0.0),
                           "note": "algorithmic = unique q rows + index/weight + agg"
                                   + (" + self rows + W + y/norm outputs" if fused else "")
+                                  + (" + Q1 weights and the U1 q rows it stores (flops: every row x Q1)"
+                                     if next_q else "")
                                   + "; logical counts every (row, slot) read, most served by L2 / "
                                     "Infinity Cache"},
-        "frontier": {"U0_mean": U0, "F0_mean": F0},
+        "frontier": {"U0_mean": U0, "F0_mean": F0, "U1_mean": U1},
         "host_ms_per_step": {"sample_batch": t_sample / args.steps * 1e3,
                              "train_batch_enqueue": t_enqueue / args.steps * 1e3,
                              # the enqueue's own host work: without the time blocked on

@@ -1927,8 +1927,8 @@ int launch_norm_lrelu_bwd(const float* y, const float* nrm, const float* dy, int
 int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float margin,
                 const float* feats, int64_t ld_f, int d_in, const int64_t* batch, float* G, int* Kc,
                 int64_t S_max, const int* nS, float* dZ, float* part, float* colpart, float* scal,
-                float* hinge, bool combine_dz, const int* rank_off, const int32_t* pos_sorted, float* Gp,
-                hipStream_t st) {
+                float* hinge, bool combine_dz, bool rep_sum, const int* rank_off, const int32_t* pos_sorted,
+                float* Gp, hipStream_t st) {
   // G and Kc are zero on entry (init_workspace; then the head backward (or
   // dz_combine) and the first backward kernel leave them zero)
   PS_REQUIRE(d <= 256, kErrArg, "loss: out_dim must be <= 256");
@@ -1949,10 +1949,13 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   }
 #undef PS_LOSS
   PS_CHECK_LAUNCH();
-  if (d <= 128)
+  // rep_sum false: the consumer (the fused head backward, head.hip) sums the
+  // repeated ranks' Gp rows itself, in the same order
+  PS_REQUIRE(rep_sum || !combine_dz, kErrArg, "loss: dz_combine reads G: the repeated ranks need rep_sum");
+  if (rep_sum && d <= 128)
     hipLaunchKernelGGL((rep_sum_kernel<2, 3>), dim3(grid_for(S_max * 64, 256)), dim3(256), 0, st, rank_off,
                        pos_sorted, nS, d, Gp, G, S_max);
-  else
+  else if (rep_sum)
     hipLaunchKernelGGL((rep_sum_kernel<4, 3>), dim3(grid_for(S_max * 64, 256)), dim3(256), 0, st, rank_off,
                        pos_sorted, nS, d, Gp, G, S_max);
   PS_CHECK_LAUNCH();

@@ -57,7 +57,7 @@ int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const i
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
-                float*, bool, const int*, const int32_t*, float*, hipStream_t);
+                float*, bool, bool, const int*, const int32_t*, float*, hipStream_t);
 int launch_pos_csr(const int32_t*, int64_t, int*, int32_t*, hipStream_t);
 int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
@@ -70,7 +70,7 @@ int launch_head_fwd(const float*, int, const int*, int64_t, const float*, const 
                     const float*, float*, float*, hipStream_t);
 int launch_head_bwd(float*, int*, int64_t, float*, int, const int*, int64_t, const float*,
                     const float*, const float*, const float*, const float*, float*, float*,
-                    hipStream_t);
+                    const int*, const int32_t*, const float*, hipStream_t);
 int launch_dz_from_dout(const float*, int, const int32_t*, int64_t, const int*, int64_t, float*,
                         int*, float*, bool, const int*, const int32_t*, float*, hipStream_t);
 
@@ -133,6 +133,13 @@ struct Engine {
   int side_grid = getenv("PINSAGE_SIDE_GRID") ? atoi(getenv("PINSAGE_SIDE_GRID")) : 0;
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
+  // the fused head backward sums repeated batch nodes' loss rows itself (no
+  // rep_sum launch between the loss and it); PINSAGE_HEAD_REP_SUM=0: rep_sum
+  // launch (A/B; bitwise the same G rows)
+  bool head_rep_sum = !getenv("PINSAGE_HEAD_REP_SUM") || atoi(getenv("PINSAGE_HEAD_REP_SUM")) != 0;
+  // the last enqueued G producer was the loss with rep_sum left to the head
+  // (G's repeated ranks still in Gp, three groups); dz_from_dout clears it
+  bool reps_in_gp = false;
   // PINSAGE_FUSED_AGGW=0: aggregation and W projection as two launches (A/B);
   // 1 (default): one launch (aggw.hip).  Experimental forms measured slower and
   // removed: register-pipelined split-bf16 (C2 layer 0 39.7 us),
@@ -902,7 +909,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
     PS_TRY(launch_head_bwd(at<float>(ws, E.G), at<int>(ws, E.Kc), top.S.cap, at<float>(ws, E.dZ), o,
                            cnt(top.S), top.S.cap, at<float>(ws, E.H1), E.params + E.pG1w,
                            E.params + E.pG2w, at<float>(ws, top.y), at<float>(ws, top.nrm),
-                           at<float>(ws, E.dP1), at<float>(ws, top.dp), st));
+                           at<float>(ws, E.dP1), at<float>(ws, top.dp), at<int>(ws, E.rank_off),
+                           at<int32_t>(ws, E.pos_sorted), E.reps_in_gp ? at<float>(ws, E.Gp) : nullptr, st));
     PS_TRY(run_pend(E));  // the loss monitors (PINSAGE_DEFER_SIDE bit 1)
     PS_TRY(fork_side(E, st, s_wg, dfr, wgrad_g2));
   } else {
@@ -1392,13 +1400,14 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
   hipStream_t st = (hipStream_t)stream;
   {
     Timed t(*E, "loss", st);
+    E->reps_in_gp = E->fused_head && E->head_rep_sum;
     PS_TRY(launch_loss(at<float>(ws, E->Z), (int)c.out, at<int32_t>(ws, E->pos_rank), (int)batch_size,
                        margin, with_monitors ? E->feats : nullptr, E->ld_f, (int)c.d_in,
                        at<int64_t>(ws, E->ids), at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap,
                        at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
                        at<float>(ws, E->varpart), at<float>(ws, E->scal), at<float>(ws, E->hinge),
-                       !E->fused_head, at<int>(ws, E->rank_off), at<int32_t>(ws, E->pos_sorted),
-                       at<float>(ws, E->Gp), st));
+                       !E->fused_head, !E->fused_head || !E->head_rep_sum, at<int>(ws, E->rank_off),
+                       at<int32_t>(ws, E->pos_sorted), at<float>(ws, E->Gp), st));
   }
   // the monitors (loss, node-feature loss, variance scalars) beside the
   // backward, on side stream 0, joined at the backward's end (with
@@ -1423,6 +1432,7 @@ int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dou
   Engine* E = reinterpret_cast<Engine*>(e);
   PS_TRY(run_pend(*E));
   LayerBuf& top = E->L.back();
+  E->reps_in_gp = false;
   return launch_dz_from_dout(dout, (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
                              at<int>(ws, top.S.count), top.S.cap, at<float>(ws, E->G),
                              at<int>(ws, E->Kc), at<float>(ws, E->dZ), !E->fused_head,

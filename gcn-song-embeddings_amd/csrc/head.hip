@@ -163,9 +163,19 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
 // step's loss accumulates into zeros).  K[c][r] = 0 means G[c][r] is +0, so the
 // terms it adds change nothing (bitwise the old dZ = sum over k != 0).
 constexpr int kHeadRNI = kHeadRows * (kHeadDim / 4) / 256;
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+// Gp (optional): the loss left a repeated rank's rows in Gp (det_put, conv.hip)
+// and no rep_sum pass ran; head_sum_reps sums its group rows, from zero in
+// position order (pos_sorted, groups p % 3) -- the additions rep_sum_kernel
+// makes, so the rows come out bitwise the same.  head_fetch_dz also loads each
+// row's position range (o0, o1).
 __device__ __forceinline__ void head_fetch_dz(float4 (&g)[3][kHeadRNI], int (&k)[3][kHeadRNI],
+                                              int (&o0)[kHeadRNI], int (&o1)[kHeadRNI],
                                               const float* __restrict__ G, const int* __restrict__ Kc,
-                                              int64_t S_max, int64_t r0, int64_t R, int o, int tid) {
+                                              int64_t S_max, int64_t r0, int64_t R, int o, int tid,
+                                              const int* __restrict__ rank_off, bool reps) {
   constexpr int NI = kHeadRNI;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -177,6 +187,42 @@ __device__ __forceinline__ void head_fetch_dz(float4 (&g)[3][kHeadRNI], int (&k)
       g[q][j] = ok ? *reinterpret_cast<const float4*>(G + ((int64_t)q * S_max + r0 + row) * o + c)
                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    o0[j] = reps && ok ? rank_off[r0 + row] : 0;
+    o1[j] = reps && ok ? rank_off[r0 + row + 1] : 0;
+  }
+}
+constexpr int kHeadRepBatch = 8;  // positions whose rows are in flight together
+__device__ __forceinline__ void head_sum_reps(float4 (&g)[3][kHeadRNI], const int (&o0)[kHeadRNI],
+                                              const int (&o1)[kHeadRNI], int o, int tid,
+                                              const int32_t* __restrict__ pos_sorted,
+                                              const float* __restrict__ Gp) {
+#pragma unroll
+  for (int j = 0; j < kHeadRNI; ++j) {
+    if (o1[j] - o0[j] < 2) continue;
+    const int c = 4 * ((tid + 256 * j) % (kHeadDim / 4));
+    float4 a[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u0 = o0[j]; u0 < o1[j]; u0 += kHeadRepBatch) {
+      int pp[kHeadRepBatch];
+      float4 v[kHeadRepBatch];
+#pragma unroll
+      for (int t = 0; t < kHeadRepBatch; ++t) pp[t] = u0 + t < o1[j] ? pos_sorted[u0 + t] : -1;
+#pragma unroll
+      for (int t = 0; t < kHeadRepBatch; ++t)
+        v[t] = pp[t] >= 0 ? *reinterpret_cast<const float4*>(Gp + (int64_t)pp[t] * o + c)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < kHeadRepBatch; ++t) {
+        if (pp[t] < 0) continue;
+        const int grp = pp[t] % 3;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (q == grp) a[q] = add4(a[q], v[t]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) g[q][j] = a[q];
   }
 }
 __device__ __forceinline__ void head_put_dz(float* sA, float* __restrict__ G, const float4 (&g)[3][kHeadRNI],
@@ -212,7 +258,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, float* __restrict__ dZ, int o,
     const int* __restrict__ nrows, const float* __restrict__ H1, const float* __restrict__ G1w,
     const float* __restrict__ G2w, const float* __restrict__ y, const float* __restrict__ nrm,
-    float* __restrict__ dP1, float* __restrict__ dp) {
+    float* __restrict__ dP1, float* __restrict__ dp, const int* __restrict__ rank_off,
+    const int32_t* __restrict__ pos_sorted, const float* __restrict__ Gp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* sA = lds;
   float* sW2 = sA + kHeadRows * kHeadLd;
@@ -245,7 +292,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   // (vmcnt counts both), which made this staging ~10 us of the kernel's ~21
   float4 g[3][kHeadRNI], w1[kHeadWNI], w2[kHeadWNI];
   int k[3][kHeadRNI];
-  head_fetch_dz(g, k, G, Kc, S_max, r0, R, o, tid);
+  // repeated ranks summed here (Gp set, rank_off[0] >= 0; rank_off[0] < 0:
+  // the loss used atomics into G)
+  const bool reps = Gp && rank_off[0] >= 0;
+  int o0[kHeadRNI], o1[kHeadRNI];
+  head_fetch_dz(g, k, o0, o1, G, Kc, S_max, r0, R, o, tid, rank_off, reps);
   head_fetch_weight(w2, G2w, o, tid);
   head_fetch_weight(w1, G1w, o, tid);
   float inv[16];
@@ -254,6 +305,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const int row = head_row(r, h);
     inv[r] = r0 + row < R ? nrm[r0 + row] : 1.f;
   }
+  if (reps) head_sum_reps(g, o0, o1, o, tid, pos_sorted, Gp);
   head_put_dz(sA, G, g, k, S_max, dZ, r0, R, o, tid);
   head_put_weight(sW2, w2, tid);
   head_put_weight(sW1, w1, tid);
@@ -339,12 +391,15 @@ int launch_head_fwd(const float* y, int o, const int* nrows, int64_t max_rows, c
 
 int launch_head_bwd(float* G, int* Kc, int64_t S_max, float* dZ, int o, const int* nrows,
                     int64_t max_rows, const float* H1, const float* G1w, const float* G2w,
-                    const float* y, const float* nrm, float* dP1, float* dp, hipStream_t st) {
+                    const float* y, const float* nrm, float* dP1, float* dp, const int* rank_off,
+                    const int32_t* pos_sorted, const float* Gp, hipStream_t st) {
   PS_REQUIRE(head_supported(o), kErrArg, "head: out_dim must be a multiple of 4, <= 128");
+  PS_REQUIRE(!Gp || (rank_off && pos_sorted), kErrArg, "head: repeated-rank rows need rank_off and pos_sorted");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
   hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp);
+                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp, rank_off,
+                     pos_sorted, Gp);
   PS_CHECK_LAUNCH();
   return kOk;
 }

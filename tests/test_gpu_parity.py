@@ -761,3 +761,55 @@ def test_default_step_is_bitwise_reproducible():
             os.chdir(cwd)
             if old is not None:
                 os.environ["PINSAGE_AUTOTUNE"] = old
+
+
+def test_head_sums_repeated_ranks_bitwise():
+    """The fused head backward sums a repeated batch node's per-position loss
+    rows itself (head.hip head_fetch_dz, from zero in position order) instead
+    of a rep_sum_kernel launch between the loss and it (PINSAGE_HEAD_REP_SUM=0):
+    the same additions in the same order, so three steps end with bitwise-equal
+    parameters and losses.  GEMM choices from the size model in both runs; the
+    batch repeats nodes three and more times per call."""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(3000, 600, 20000, seed=61)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(3000, 256, seed=62))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 15000, seed=63))
+    old = {k: os.environ.get(k) for k in ("PINSAGE_HEAD_REP_SUM", "PINSAGE_AUTOTUNE")}
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
+            pt.PinSage(g, 3000, feats, pos, log=False, load_save=False)
+            os.environ["PINSAGE_AUTOTUNE"] = "0"
+
+            def run(mode):
+                os.environ["PINSAGE_HEAD_REP_SUM"] = mode  # read when the engine is built
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, 3000, feats, pos, log=False, load_save=False)
+                tr.batch_size = 512
+                torch.manual_seed(6)
+                losses, reps = [], 0
+                for _ in range(3):
+                    batch, _ = tr.next_batch()
+                    for c in range(3):
+                        reps = max(reps, int(torch.bincount(batch[:, c].reshape(-1)).max()))
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                return losses, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).cpu(), reps
+
+            l0, p0, reps = run("0")
+            l1, p1, _ = run("1")
+            assert reps >= 3, reps
+            assert l0 == l1, (l0, l1)
+            assert torch.equal(p0, p1), (p0 - p1).abs().max().item()
+        finally:
+            os.chdir(cwd)
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
