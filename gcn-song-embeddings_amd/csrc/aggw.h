@@ -21,6 +21,17 @@ struct AggNextQ {
   int hid = 0;
 };
 
+// The model head fused into the top layer's 16-row tile (engine: the last
+// layer): H1 = lrelu(y G1^T + b1), Z = H1 G2^T on exact fp32 MFMAs, both
+// [rows][128] -- what head_fwd_kernel (head.hip) computes from y.
+struct AggHead {
+  const float* G1w = nullptr;  // [128][128]
+  const float* G1b = nullptr;
+  const float* G2w = nullptr;  // [128][128]
+  float* H1 = nullptr;
+  float* Z = nullptr;
+};
+
 int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
 // the fragment form (agg_wf_kernel): d, hid multiples of 32, out 128, T <= 64
 int agg_wf_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
@@ -39,10 +50,12 @@ int launch_split_wfrag(const float* W, int64_t ldw, int K, int rows, uint16_t* p
 // planes (optional, agg_wf_planes_bytes): run the fragment form (unless next
 // is set or PINSAGE_AGGW_FORM=0); planes_rows 0: split W into them first,
 // 16 / 32: they already hold W split for that rows form (launch_split_wfrag)
+// head (optional): fuse the model head (AggHead); *head_done is set to 1 when
+// the chosen kernel form did it (the 16-row form), else 0.
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
                  const AggNextQ* next = nullptr, int* next_done = nullptr, uint16_t* planes = nullptr,
-                 int planes_rows = 0);
+                 int planes_rows = 0, const AggHead* head = nullptr, int* head_done = nullptr);
 
 }  // namespace ps

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
     const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
     const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
     const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y,
-    float* __restrict__ nrm_out, float* __restrict__ agg) {
+    float* __restrict__ nrm_out, float* __restrict__ agg, AggHead hd) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int K = d + hid, lda = aw_lda(K);
   float* sA = lds;                                          // [16][lda]
@@ -166,9 +166,24 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
       b0 = n0;
       b1 = n1;
     }
+    // the head's weight rows (column 16 wave + l16, k = 32 g .. 32 g + 31 of G1
+    // and G2), fetched under the epilogue
+    float4 hw1[8], hw2[8];
+    float hb1 = 0.f;
+    if (hd.G1w) {
+      const int hc = wave * 16 + l16;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        hw1[i] = *reinterpret_cast<const float4*>(hd.G1w + hc * kAwOut + 32 * g + 4 * i);
+        hw2[i] = *reinterpret_cast<const float4*>(hd.G2w + hc * kAwOut + 32 * g + 4 * i);
+      }
+      hb1 = hd.G1b[hc];
+    }
     __syncthreads();  // every wave is done reading the A tile
     // ---- the [16][128] output tile -> LDS, then bias, lrelu, row L2 norm
     float* red = sA;
+    float* sY = sA + kAwRows * kAwOut;         // [16][kAwHd] the head's y, then H1 rows
+    constexpr int kAwHd = kAwOut + 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[(4 * g + r) * kAwOut + wave * 16 + l16] = acc[r];
     __syncthreads();
@@ -186,13 +201,53 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
       const float nrm = sqrtf(s2);
+      const float4 yv = row < nrows ? make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (hd.G1w) *reinterpret_cast<float4*>(sY + row * kAwHd + 4 * c4) = yv;
       if (row < nrows) {
-        *reinterpret_cast<float4*>(y + (r0 + row) * kAwOut + 4 * c4) =
-            make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
+        *reinterpret_cast<float4*>(y + (r0 + row) * kAwOut + 4 * c4) = yv;
         if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
       }
     }
-    __syncthreads();  // LDS is reused by the next tile
+    __syncthreads();  // LDS is reused by the next tile (or the head below)
+    if (hd.G1w) {
+      // ---- head: wave w, columns 16 w .. 16 w + 15 of H1 and Z; lane l
+      // supplies row l16 and k = 32 g + s at step s (v_mfma_f32_16x16x4_f32)
+      const int hc = wave * 16 + l16;
+      f32x4 a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 av = *reinterpret_cast<const float4*>(sY + l16 * kAwHd + 32 * g + 4 * i);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, hw1[i].x, a1, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, hw1[i].y, a1, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, hw1[i].z, a1, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, hw1[i].w, a1, 0, 0, 0);
+      }
+      __syncthreads();  // every wave is done reading y
+      float hv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[r] = lrelu(a1[r] + hb1);
+        sY[(4 * g + r) * kAwHd + hc] = hv[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < nrows) hd.H1[(r0 + 4 * g + r) * kAwOut + hc] = hv[r];
+      __syncthreads();
+      f32x4 a2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 av = *reinterpret_cast<const float4*>(sY + l16 * kAwHd + 32 * g + 4 * i);
+        a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, hw2[i].x, a2, 0, 0, 0);
+        a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, hw2[i].y, a2, 0, 0, 0);
+        a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, hw2[i].z, a2, 0, 0, 0);
+        a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, hw2[i].w, a2, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < nrows) hd.Z[(r0 + 4 * g + r) * kAwOut + hc] = a2[r];
+      __syncthreads();  // every wave is done reading H1 from LDS
+    }
   }
 }
 
@@ -835,8 +890,10 @@ int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est) {
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
-                 const AggNextQ* next, int* next_done, uint16_t* planes, int planes_rows) {
+                 const AggNextQ* next, int* next_done, uint16_t* planes, int planes_rows,
+                 const AggHead* head, int* head_done) {
   if (next_done) *next_done = 0;
+  if (head_done) *head_done = 0;
   if (planes && !(next && next->q) && agg_wf_supported(d, hid, kWfOut, T)) {
     if (S_max <= 0) return kOk;
     int rows = planes_rows;
@@ -889,8 +946,14 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
     hipLaunchKernelGGL(agg_w32_kernel, dim3((int)g32), dim3(kAw32Threads), lds32,
                        st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, nx);
   } else {
+    AggHead hd;
+    if (head && head->G1w && K >= 2 * kAwOut) {  // (y and H1 beside the output tile in the A tile's LDS)
+      PS_REQUIRE(head->G1b && head->G2w && head->H1 && head->Z, kErrArg, "agg_w: the fused head needs every pointer");
+      hd = *head;
+      if (head_done) *head_done = 1;
+    }
     hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
-                       loc, wloc, T, nS, n_static, W, bias, y, nrm, agg);
+                       loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, hd);
   }
   PS_CHECK_LAUNCH();
   return kOk;

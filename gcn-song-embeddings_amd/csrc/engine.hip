@@ -137,6 +137,9 @@ struct Engine {
   // rep_sum launch between the loss and it); PINSAGE_HEAD_REP_SUM=0: rep_sum
   // launch (A/B; bitwise the same G rows)
   bool head_rep_sum = !getenv("PINSAGE_HEAD_REP_SUM") || atoi(getenv("PINSAGE_HEAD_REP_SUM")) != 0;
+  // the fused head's forward inside the top layer's 16-row aggregation + W
+  // tile (AggHead, aggw.h): one launch less; PINSAGE_HEAD_IN_AGGW=0: head_fwd launch
+  bool head_in_aggw = !getenv("PINSAGE_HEAD_IN_AGGW") || atoi(getenv("PINSAGE_HEAD_IN_AGGW")) != 0;
   // the last enqueued G producer was the loss with rep_sum left to the head
   // (G's repeated ranks still in Gp, three groups); dz_from_dout clears it
   bool reps_in_gp = false;
@@ -614,6 +617,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     }
   }
   int q_done = 0;  // this layer's q rows came out of the layer below's kernel (AggNextQ)
+  int head_done = 0;  // the head ran inside the top layer's kernel (AggHead)
   for (int l = 0; l < Lc; ++l) {
     LayerBuf& lb = E.L[(size_t)l];
     const float* h = l == 0 ? E.feats : at<float>(ws, E.L[(size_t)l - 1].y);
@@ -673,11 +677,20 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
         nx.q = at<float>(ws, nb.q);
         nx.hid = (int)c.hid;
       }
+      AggHead hd;
+      if (l == Lc - 1 && E.fused_head && E.head_in_aggw) {
+        hd.G1w = E.params + E.pG1w;
+        hd.G1b = E.params + E.pG1b;
+        hd.G2w = E.params + E.pG2w;
+        hd.H1 = at<float>(ws, E.H1);
+        hd.Z = at<float>(ws, E.Z);
+      }
       PS_TRY(launch_agg_w(h, ldh, (int)lb.d, at<int32_t>(ws, lb.self_src), at<float>(ws, lb.q),
                           (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0,
                           S_est, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
                           at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st, nx.q ? &nx : nullptr, &q_done,
-                          wf_rows[(size_t)l] ? at<uint16_t>(ws, lb.wplanes) : nullptr, wf_rows[(size_t)l]));
+                          wf_rows[(size_t)l] ? at<uint16_t>(ws, lb.wplanes) : nullptr, wf_rows[(size_t)l],
+                          hd.G1w ? &hd : nullptr, &head_done));
       continue;
     }
     Timed t_agg(E, lname("fwd.agg", l), st);
@@ -711,6 +724,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     E.sk_used[lname("fwd.w_gemm", l)] = gemm_last_stream_k();
   }
   // head: G2(lrelu(G1 y))
+  if (head_done) return kOk;
   Timed t_head(E, "fwd.head", st);
   if (E.fused_head)
     return launch_head_fwd(at<float>(ws, top.y), (int)c.out, cnt(top.S), top.S.cap,

@@ -397,7 +397,7 @@ def test_frontier_ahead_matches_serial_step(mode):
 
 
 @pytest.mark.parametrize("var,a,b", [("PINSAGE_DEFER_SIDE", "0", "3"), ("PINSAGE_DQ_CHUNK_ROWS", "0", "1"),
-                                     ("PINSAGE_FUSED_NEXT_Q", "0", "1")])
+                                     ("PINSAGE_FUSED_NEXT_Q", "0", "1"), ("PINSAGE_HEAD_IN_AGGW", "0", "1")])
 def test_engine_variants_train_alike(var, a, b, monkeypatch):
     """Engine variants that change only launch order or summation order train
     alike -- same published losses (the monitors' output) and parameters within
@@ -407,8 +407,11 @@ def test_engine_variants_train_alike(var, a, b, monkeypatch):
     and PINSAGE_DQ_CHUNK_ROWS (the bottom layer's Q weight gradient summed
     over masked dq chunk partials instead of combined dpq rows) and
     PINSAGE_FUSED_NEXT_Q (layer 1's Q projection inside layer 0's 32-row
-    aggregation + W kernel, that form forced here)."""
-    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
+    aggregation + W kernel, that form forced here) and PINSAGE_HEAD_IN_AGGW
+    (the model head's forward inside the top layer's 16-row tile, exact fp32
+    MFMAs in another k order than head_fwd_kernel's)."""
+    if var != "PINSAGE_HEAD_IN_AGGW":  # (the head is fused into the 16-row form only)
+        monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
     import graph
     import pinsage_training as pt
     import synthetic
