@@ -131,6 +131,9 @@ struct Engine {
   // weight-gradient GEMMs beside the chain use at most this many workgroups
   // (PINSAGE_SIDE_GRID; 0 = no cap), leaving the other CUs to the chain
   int side_grid = getenv("PINSAGE_SIDE_GRID") ? atoi(getenv("PINSAGE_SIDE_GRID")) : 0;
+  // workgroups the size model aims a side-stream weight gradient's split-K at
+  // (the chain's own: 512)
+  int side_wg_target = getenv("PINSAGE_SIDE_WG_TARGET") ? std::max(1, atoi(getenv("PINSAGE_SIDE_WG_TARGET"))) : 512;
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // the fused head backward sums repeated batch nodes' loss rows itself (no
@@ -364,11 +367,11 @@ static size_t carve(size_t& cur, int64_t bytes) {
 // rows per split (the slabs cost S*M*N*8 bytes of traffic, so no more splits than
 // that); small outputs (128 x 128 head weights) fall back to 32 x 128 tiles.
 constexpr int kMaxSplits = 64;
-static void choose_wgrad(int64_t M, int64_t N, int64_t Kest, int* cfg, int* splits) {
+static void choose_wgrad(int64_t M, int64_t N, int64_t Kest, int* cfg, int* splits, int64_t target = 512) {
   static const int bm[3] = {128, 64, 32};
   for (int c = 0; c < 3; ++c) {
     const int64_t tiles = ((M + bm[c] - 1) / bm[c]) * ((N + 127) / 128);
-    int64_t s = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+    int64_t s = std::max<int64_t>(1, (target + tiles - 1) / tiles);
     s = std::min<int64_t>(s, std::max<int64_t>(1, Kest / 128));
     s = std::min<int64_t>(s, kMaxSplits);
     if (tiles * s >= 256 || c == 2) {
@@ -816,7 +819,8 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
   float* const slab = at<float>(ws, main ? E.slab_main : E.slab);
   float* const bslab = at<float>(ws, main ? E.bslab_main : E.bslab);
   int cfg = 0, S = 1;
-  choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
+  choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S,
+               beside ? E.side_wg_target : 512);
   {
     auto it = E.choice.find(site);
     if (it != E.choice.end()) {
