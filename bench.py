@@ -269,6 +269,31 @@ def cpu_baseline(cfg, pg, feats, pos, nbhds, seconds=45.0, steps=20, warmup=3):
                 refcpu_over_reference_source="profiles/r02/refcpu_ratio.json (dev container, 8 threads)")
 
 
+def launch_ranks(n_gpus):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run the same
+    command under torch.distributed.run, one rank per GPU, as a child process
+    (nothing here has touched the GPU, so no exec is involved), relay its
+    output and exit with its code.  Started BY a launcher, WORLD_SIZE must
+    equal --gpus."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != n_gpus:
+            raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
+        return
+    if n_gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n_gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n_gpus} without a launcher: {' '.join(cmd)}")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    raise SystemExit(subprocess.call(cmd, env=env))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -286,6 +311,7 @@ def main():
                          "fly: every call walks its nodes' neighbourhoods inside the step "
                          "(relevant_nodes_per_layer, pinsage_model.py:142-154), RNG per --precompute-rng")
     args = ap.parse_args()
+    launch_ranks(args.gpus)
     cfg = dict(CONFIGS[args.config])
     if args.scale != 1.0:
         for k in ("n_tracks", "n_cols", "memberships"):

@@ -33,29 +33,28 @@ struct AggHead {
 };
 
 int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
-// the fragment form (agg_wf_kernel): d, hid multiples of 32, out 128, T <= 64
-int agg_wf_supported(int64_t d, int64_t hid, int64_t out, int64_t T);
 // bytes of W's fragment-order bf16 planes (3 x 128 x (d + hid) x 2)
-int64_t agg_wf_planes_bytes(int64_t d, int64_t hid);
-// the fragment form's rows per tile (16 or 32) for an expected row count
-int agg_wf_rows(int64_t S_max);
+int64_t agg_w_planes_bytes(int64_t d, int64_t hid);
+// whether launch_agg_w runs the pipelined 32-row form (which reads W from its
+// bf16 planes) at an expected row count S_est
+int agg_w_uses_planes(int64_t d, int64_t hid, int64_t out, int64_t T, int64_t S_est);
 // whether fusing the next layer's Q projection (AggNextQ) is expected to pay
 // at S_est rows: the 32-row form runs and its tiles fit one pass over the CUs
 // (the fused products lengthen every tile; a second pass of tiles doubles that)
 int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est);
-// W [128][K] -> fragment-order planes for the rows form `rows`
-int launch_split_wfrag(const float* W, int64_t ldw, int K, int rows, uint16_t* planes, hipStream_t st);
+// W [128][K] -> the pipelined form's fragment-order bf16 planes
+int launch_split_wplanes(const float* W, int64_t ldw, int K, uint16_t* planes, hipStream_t st);
 // next (optional): fuse the next layer's Q projection; *next_done is set to 1
-// when the chosen kernel form did it (the 32-row form), else 0.
-// planes (optional, agg_wf_planes_bytes): run the fragment form (unless next
-// is set or PINSAGE_AGGW_FORM=0); planes_rows 0: split W into them first,
-// 16 / 32: they already hold W split for that rows form (launch_split_wfrag)
+// when the chosen kernel form did it (the 32-row forms), else 0.
+// planes (optional, agg_w_planes_bytes): lets the 32-row form run pipelined
+// (agg_w_uses_planes); planes_ready 0: split W into them first, 1: they
+// already hold W (launch_split_wplanes)
 // head (optional): fuse the model head (AggHead); *head_done is set to 1 when
 // the chosen kernel form did it (the 16-row form), else 0.
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
                  const AggNextQ* next = nullptr, int* next_done = nullptr, uint16_t* planes = nullptr,
-                 int planes_rows = 0, const AggHead* head = nullptr, int* head_done = nullptr);
+                 int planes_ready = 0, const AggHead* head = nullptr, int* head_done = nullptr);
 
 }  // namespace ps

@@ -513,68 +513,38 @@ __global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
   }
 }
 
-// ---------------------------------------------------------------- fragment form
-// Opt-in (PINSAGE_AGGW_FORM=1; round 4, measured even with the forms above).  W is split ONCE per forward (split_wfrag_kernel)
-// into its bf16 hi / mid / lo planes, stored in MFMA fragment order: every B
-// fragment a wave needs is one coalesced 1 KiB load, and no wave converts W
-// (the LDS-tile forms above re-split W in every workgroup, and their per-lane
-// W reads touch a different 64-B segment per lane).  Per tile of ROWS rows:
-//   1. [h_self || agg] staged in LDS as before (coalesced row reads; the
-//      aggregate is the fma chain in slot order t = 0, 1, ..., bitwise
-//      agg_kernel's, and is written out once);
-//   2. the projection: K is cut into KS-wide MFMA steps dealt round-robin to
-//      the 8 waves (step s to wave s % 8), and each wave accumulates ALL 128
-//      output columns over its steps (4 accumulators of 32x32, or 8 of
-//      16x16), so one A fragment (read from LDS, split once) feeds 24 MFMAs;
-//      the wave's next step's B fragments load while the current step runs;
-//   3. the 8 partial tiles meet in LDS in wave order, then bias, LeakyReLU
-//      and the row L2 norm.
-//   ROWS 32: v_mfma_f32_32x32x16_bf16, KS 16: lane (row l % 32, half l / 32)
-//            supplies k = 16 s + 8 (l / 32) + [0, 8);
-//   ROWS 16: v_mfma_f32_16x16x32_bf16, KS 32: lane (row l % 16, quarter
-//            l / 16) supplies k = 32 s + 8 (l / 16) + [0, 8).
-template <int ROWS>
-struct WfGeom;
-template <>
-struct WfGeom<32> {
-  static constexpr int CW = 32, NCG = 4, KS = 16, NJ = 8;  // NJ: float4 columns per thread per gather pass
-  typedef float acc_t __attribute__((ext_vector_type(16)));
-};
-template <>
-struct WfGeom<16> {
-  static constexpr int CW = 16, NCG = 8, KS = 32, NJ = 4;
-  typedef float acc_t __attribute__((ext_vector_type(4)));
-};
+// ---------------------------------------------------------------- 32-row form, A split once per two column groups
+// The default 32-row tile (agg_w32_kernel above is the unfused-W reference
+// form, PINSAGE_AGGW_FORM=0).  The gather is agg_w32_kernel's (every thread's
+// loads in flight at once; agg bitwise agg_kernel's); the projection is cut
+// differently: wave w owns k eighth w / 2 and column groups 2 (w % 2), +1, so
+// each A fragment read from LDS is split into bf16 hi / mid / lo once for 12
+// MFMAs (agg_w32_kernel: once per 6, every fragment split by four waves), and W
+// comes pre-split from its fragment-order planes (split_wplanes_kernel, one
+// coalesced 1 KiB load per plane and fragment; the next 16-k step's fragments
+// load while the current step's products run).  Without planes (PL false) W is
+// split in registers.  The eight k-eighth partial tiles meet in LDS in order.
+constexpr int kWpOut = 128;   // out_dim
+constexpr int kWpCG = 4;      // 32-column groups of the output
+#ifndef PS_AGGWS_PROBE  // timing-only builds (results wrong by construction): bit 0 no products, bit 1 no aggregate gather
+#define PS_AGGWS_PROBE 0
+#endif
 
-constexpr int kWfThreads = 512;
-constexpr int kWfWaves = kWfThreads / 64;
-constexpr int kWfOut = 128;   // out_dim
-constexpr int kWfTMax = 64;   // fanout held in LDS per row
-constexpr int kWfRed = kWfOut + 4;  // LDS row of a partial output tile
-
-template <int ROWS>
-int64_t wf_lds_bytes(int64_t K) {
-  const int64_t tile = std::max<int64_t>((int64_t)ROWS * (K + 4), (int64_t)kWfWaves * ROWS * kWfRed);
-  return (tile + 2 * ROWS * kWfTMax + ROWS) * 4;
-}
-
-// Fragment-order planes of W [128][K] (row stride ldw): chunk c = (s, cg,
-// lane) of 8 bf16 at planes[((c >> 6) * 3 + p) * 512 + (c & 63) * 8], holding
-// plane p of W[CW cg + lane % CW][KS s + 8 (lane / CW) + i], i < 8 -- the B
-// fragment lane `lane` supplies in step s for column group cg.  The split is
-// split3's (bf16split.h), so the products equal the GEMM's.
-template <int ROWS>
-__global__ __launch_bounds__(256) void split_wfrag_kernel(const float* __restrict__ W, int64_t ldw, int K,
-                                                          uint16_t* __restrict__ planes) {
-  using Gm = WfGeom<ROWS>;
-  const int64_t n = (int64_t)K * kWfOut / 8;  // chunks
+// W [128][K] (row stride ldw) -> fragment-order planes: chunk c = (s, cg, lane)
+// of 8 bf16 at planes[((c >> 6) * 3 + p) * 512 + (c & 63) * 8] holds plane p of
+// W[32 cg + lane % 32][16 s + 8 (lane / 32) + i], i < 8 -- the B fragment lane
+// `lane` supplies to v_mfma_f32_32x32x16_bf16 in 16-k step s for column group
+// cg.  The split is split3's (bf16split.h), so the products equal the
+// in-register split's.
+__global__ __launch_bounds__(256) void split_wplanes_kernel(const float* __restrict__ W, int64_t ldw, int K,
+                                                            uint16_t* __restrict__ planes) {
+  const int64_t n = (int64_t)K * kWpOut / 8;  // chunks
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
   const int lane = (int)(c & 63);
   const int64_t rest = c >> 6;
-  const int cg = (int)(rest % Gm::NCG), s = (int)(rest / Gm::NCG);
-  const int col = Gm::CW * cg + lane % Gm::CW, k = Gm::KS * s + 8 * (lane / Gm::CW);
-  const float* src = W + (int64_t)col * ldw + k;
+  const int cg = (int)(rest % kWpCG), s = (int)(rest / kWpCG);
+  const float* src = W + (int64_t)(32 * cg + (lane & 31)) * ldw + 16 * s + 8 * (lane >> 5);
   bf16x8 H, M, L;
   split3(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 4), H, M, L);
   uint16_t* o = planes + (rest * 3) * 512 + lane * 8;
@@ -583,104 +553,95 @@ __global__ __launch_bounds__(256) void split_wfrag_kernel(const float* __restric
   *reinterpret_cast<bf16x8*>(o + 1024) = L;
 }
 
-template <int ROWS>
-__global__ __launch_bounds__(kWfThreads) void agg_wf_kernel(
+// LDS: max(A tile [32][K + 4], the partial tiles [8][32][128]), then the slot lists
+static int64_t ws_lds_bytes(int64_t K) {
+  const int64_t tile = std::max<int64_t>((int64_t)kAw32Rows * (K + 4), (int64_t)8 * kAw32Rows * kWpOut);
+  return (tile + 2 * kAw32Rows * kAw32TMax + kAw32Rows) * 4;
+}
+
+template <bool PL>
+__global__ __launch_bounds__(kAw32Threads) void agg_w32s_kernel(
     const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
-    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc, const float* __restrict__ wloc,
-    int T, const int* __restrict__ nS, int64_t n_static, const uint16_t* __restrict__ planes,
-    const float* __restrict__ bias, float* __restrict__ y, float* __restrict__ nrm_out, float* __restrict__ agg) {
-  using Gm = WfGeom<ROWS>;
-  using acc_t = typename Gm::acc_t;
-  constexpr int NA = (int)(sizeof(acc_t) / 4);
+    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
+    const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
+    const float* __restrict__ W, const uint16_t* __restrict__ planes, const float* __restrict__ bias,
+    float* __restrict__ y, float* __restrict__ nrm_out, float* __restrict__ agg, AggNextQ nx) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int K = d + hid, lda = K + 4;  // row stride 4 mod 64 banks: b128 fragment reads spread
-  const int64_t tile_f = std::max<int64_t>((int64_t)ROWS * lda, (int64_t)kWfWaves * ROWS * kWfRed);
-  float* sA = lds;   // [ROWS][lda]; the partial output tiles [waves][ROWS][kWfRed] after the products
-  float* red = lds;
-  int* sLoc = reinterpret_cast<int*>(lds + tile_f);           // [ROWS][kWfTMax]
-  float* sW = reinterpret_cast<float*>(sLoc + ROWS * kWfTMax);  // [ROWS][kWfTMax]
-  int* sSelf = reinterpret_cast<int*>(sW + ROWS * kWfTMax);     // [ROWS]
+  const int K = d + hid, lda = aw32_lda(K);
+  const int64_t tile_f = std::max<int64_t>((int64_t)kAw32Rows * lda, (int64_t)8 * kAw32Rows * kWpOut);
+  float* sA = lds;                                            // [32][lda]; the partial tiles after the products
+  int* sLoc = reinterpret_cast<int*>(lds + tile_f);           // [32][T]
+  float* sW = reinterpret_cast<float*>(sLoc + kAw32Rows * kAw32TMax);  // [32][T]
+  int* sSelf = reinterpret_cast<int*>(sW + kAw32Rows * kAw32TMax);     // [32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int S = K / Gm::KS;
-  const int lr = lane % ROWS, kq = lane / ROWS;
-  // B fragments of step s: 3 planes x NCG column groups, 1 KiB each
-  auto load_b = [&](int s, bf16x8 (&bH)[Gm::NCG], bf16x8 (&bM)[Gm::NCG], bf16x8 (&bL)[Gm::NCG])
-      __attribute__((always_inline)) {
-    const bf16x8* bp = reinterpret_cast<const bf16x8*>(planes + ((int64_t)(s * Gm::NCG) * 3 * 64 + lane) * 8);
-#pragma unroll
-    for (int c = 0; c < Gm::NCG; ++c) {
-      bH[c] = bp[(c * 3 + 0) * 64];
-      bM[c] = bp[(c * 3 + 1) * 64];
-      bL[c] = bp[(c * 3 + 2) * 64];
-    }
-  };
-  // rows dealt in contiguous ranges: block b of G owns [F b / G, F (b+1) / G)
-  // in near-equal tiles of <= ROWS rows
   const int64_t F = nS ? (int64_t)*nS : n_static;
-  const int64_t nb = gridDim.x, b = blockIdx.x;
-  const int64_t rb = F * b / nb, len = F * (b + 1) / nb - rb;
-  const int ntile = (int)((len + ROWS - 1) / ROWS);
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t rb = F * b / G, len = F * (b + 1) / G - rb;
+  const int ntile = (int)((len + kAw32Rows - 1) / kAw32Rows);
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
   for (int tile = 0; tile < ntile; ++tile) {
     const int64_t r0 = rb + len * tile / ntile;
     const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
     // ---- slot lists and self-row indices of the tile
-    for (int i = tid; i < ROWS * T; i += kWfThreads) {
+    for (int i = tid; i < kAw32Rows * T; i += kAw32Threads) {
       const int row = i / T, t = i - row * T;
       const bool ok = row < nrows;
-      sLoc[row * kWfTMax + t] = ok ? loc[(r0 + row) * T + t] : 0;
-      sW[row * kWfTMax + t] = ok ? wloc[(r0 + row) * T + t] : 0.f;
+      sLoc[row * kAw32TMax + t] = ok ? loc[(r0 + row) * T + t] : 0;
+      sW[row * kAw32TMax + t] = ok ? wloc[(r0 + row) * T + t] : 0.f;
     }
-    if (tid < ROWS) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : 0;
+    if (tid < kAw32Rows) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : 0;
     __syncthreads();
     // ---- self rows -> A[:, 0:d)
     {
       const int d4 = d >> 2;
-      for (int i = tid; i < ROWS * d4; i += kWfThreads) {
+      for (int i = tid; i < kAw32Rows * d4; i += kAw32Threads) {
         const int row = i / d4, c4 = i - row * d4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (row < nrows) v = *reinterpret_cast<const float4*>(h + (int64_t)sSelf[row] * ldh + 4 * c4);
         *reinterpret_cast<float4*>(sA + row * lda + 4 * c4) = v;
       }
     }
-    // ---- aggregate -> A[:, d:K) and agg: thread (row tid / TPR, float4
-    //      columns (tid % TPR) + TPR j); four slots' rows in flight per round
+    // ---- aggregate -> A[:, d:K) and agg (thread: row tid / 32, float4 columns
+    //      (tid % 32) + 32 j); four slots' rows in flight per round
     {
-      constexpr int TPR = kWfThreads / ROWS, NJ = Gm::NJ;
-      const int row = tid / TPR, c0 = tid % TPR, h4 = hid >> 2;
-      const int* sl = sLoc + row * kWfTMax;
-      const float* sw = sW + row * kWfTMax;
-      for (int j0 = 0; j0 < h4; j0 += TPR * NJ) {
-        float4 a[NJ];
+      const int row = tid >> 5, c0 = tid & 31, h4 = hid >> 2;
+      const int nj = (h4 + 31) / 32;
+      for (int j0 = 0; j0 < nj && !(PS_AGGWS_PROBE & 2); j0 += 4) {
+        float4 a[4];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (row < nrows) {
           int t = 0;
           for (; t + 4 <= T; t += 4) {
-            float4 x[4][NJ];
+            float4 x[4][4];
+            float w[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sl[t + u] * hid);
+              const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sLoc[row * kAw32TMax + t + u] * hid);
+              w[u] = sW[row * kAw32TMax + t + u];
 #pragma unroll
-              for (int j = 0; j < NJ; ++j) x[u][j] = qr[min(j0 + c0 + TPR * j, h4 - 1)];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float w = sw[t + u];
-#pragma unroll
-              for (int j = 0; j < NJ; ++j) {
-                a[j].x = fmaf(w, x[u][j].x, a[j].x);
-                a[j].y = fmaf(w, x[u][j].y, a[j].y);
-                a[j].z = fmaf(w, x[u][j].z, a[j].z);
-                a[j].w = fmaf(w, x[u][j].w, a[j].w);
+              for (int j = 0; j < 4; ++j) {
+                const int c = min(c0 + 32 * (j0 + j), h4 - 1);
+                x[u][j] = qr[c];
               }
             }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                a[j].x = fmaf(w[u], x[u][j].x, a[j].x);
+                a[j].y = fmaf(w[u], x[u][j].y, a[j].y);
+                a[j].z = fmaf(w[u], x[u][j].z, a[j].z);
+                a[j].w = fmaf(w[u], x[u][j].w, a[j].w);
+              }
           }
           for (; t < T; ++t) {
-            const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sl[t] * hid);
-            const float w = sw[t];
+            const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sLoc[row * kAw32TMax + t] * hid);
+            const float w = sW[row * kAw32TMax + t];
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const float4 x = qr[min(j0 + c0 + TPR * j, h4 - 1)];
+            for (int j = 0; j < 4; ++j) {
+              const int c = min(c0 + 32 * (j0 + j), h4 - 1);
+              const float4 x = qr[c];
               a[j].x = fmaf(w, x.x, a[j].x);
               a[j].y = fmaf(w, x.y, a[j].y);
               a[j].z = fmaf(w, x.z, a[j].z);
@@ -689,8 +650,8 @@ __global__ __launch_bounds__(kWfThreads) void agg_wf_kernel(
           }
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int c = j0 + c0 + TPR * j;
+        for (int j = 0; j < 4; ++j) {
+          const int c = c0 + 32 * (j0 + j);
           if (c < h4) {
             *reinterpret_cast<float4*>(sA + row * lda + d + 4 * c) = a[j];
             if (row < nrows) *reinterpret_cast<float4*>(agg + (r0 + row) * hid + 4 * c) = a[j];
@@ -699,154 +660,184 @@ __global__ __launch_bounds__(kWfThreads) void agg_wf_kernel(
       }
     }
     __syncthreads();
-    // ---- projection: wave w, steps s = w, w + 8, ..., all 128 columns
-    acc_t acc[Gm::NCG];
+    // ---- projection: wave (kq8 = w / 2, column groups 2 cp, 2 cp + 1)
+    const int kq8 = wave >> 1, cp = wave & 1;
+    const int l32 = lane & 31, hh = lane >> 5;
+    const int ksp = K >> 3, nst = ksp >> 4;
+    const float* arow = sA + l32 * lda + kq8 * ksp + 8 * hh;
+    f32x16 acc[2];
 #pragma unroll
-    for (int c = 0; c < Gm::NCG; ++c)
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int e = 0; e < NA; ++e) acc[c][e] = 0.f;
-    if (wave < S) {
-      bf16x8 bH[Gm::NCG], bM[Gm::NCG], bL[Gm::NCG];
-      load_b(wave, bH, bM, bL);
-      const float* arow = sA + lr * lda + 8 * kq;
-      for (int s = wave; s < S; s += kWfWaves) {
-        const int sn = s + kWfWaves < S ? s + kWfWaves : s;  // (the last step reloads itself: no branch)
-        bf16x8 nH[Gm::NCG], nM[Gm::NCG], nL[Gm::NCG];
-        load_b(sn, nH, nM, nL);
+      for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+    if constexpr (PL) {
+      const int sg0 = (kq8 * ksp) >> 4;
+      auto ldb = [&](int s, bf16x8 (&bb)[2][3]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const bf16x8* p =
+              reinterpret_cast<const bf16x8*>(planes + ((int64_t)((sg0 + s) * kWpCG + 2 * cp + c) * 3 * 64 + lane) * 8);
+          bb[c][0] = p[0];
+          bb[c][1] = p[64];
+          bb[c][2] = p[128];
+        }
+      };
+      bf16x8 bc[2][3], bn[2][3];
+      ldb(0, bc);
+      for (int s = 0; s < nst && !(PS_AGGWS_PROBE & 1); ++s) {
+        ldb(s + 1 < nst ? s + 1 : s, bn);  // (the last step reloads itself: no branch)
         bf16x8 aH, aM, aL;
-        const float* ap = arow + Gm::KS * s;
-        split3(*reinterpret_cast<const float4*>(ap), *reinterpret_cast<const float4*>(ap + 4), aH, aM, aL);
-#define PS_WF_ALL(X, Y)                                                                                   \
-  _Pragma("unroll") for (int c = 0; c < Gm::NCG; ++c) {                                                   \
-    if constexpr (ROWS == 32) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X, Y[c], acc[c], 0, 0, 0); \
-    else acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X, Y[c], acc[c], 0, 0, 0);                    \
-  }
-        PS_WF_ALL(aL, bH)
-        PS_WF_ALL(aH, bL)
-        PS_WF_ALL(aM, bM)
-        PS_WF_ALL(aM, bH)
-        PS_WF_ALL(aH, bM)
-        PS_WF_ALL(aH, bH)
-#undef PS_WF_ALL
+        split3(*reinterpret_cast<const float4*>(arow + 16 * s), *reinterpret_cast<const float4*>(arow + 16 * s + 4),
+               aH, aM, aL);
 #pragma unroll
-        for (int c = 0; c < Gm::NCG; ++c) {
-          bH[c] = nH[c];
-          bM[c] = nM[c];
-          bL[c] = nL[c];
+        for (int c = 0; c < 2; ++c) {
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bc[c][0], acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bc[c][2], acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bc[c][1], acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bc[c][0], acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bc[c][1], acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bc[c][0], acc[c], 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) bc[c][e] = bn[c][e];
+      }
+    } else {
+      const float* wrow = W + (int64_t)(2 * cp * 32 + l32) * K + kq8 * ksp + 8 * hh;  // column group 2 cp; +32 rows: 2 cp + 1
+      float4 bc[2][2], bn[2][2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        bc[c][0] = *reinterpret_cast<const float4*>(wrow + (int64_t)c * 32 * K);
+        bc[c][1] = *reinterpret_cast<const float4*>(wrow + (int64_t)c * 32 * K + 4);
+      }
+      for (int s = 0; s < nst; ++s) {
+        const int kn = 16 * (s + 1 < nst ? s + 1 : s);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          bn[c][0] = *reinterpret_cast<const float4*>(wrow + (int64_t)c * 32 * K + kn);
+          bn[c][1] = *reinterpret_cast<const float4*>(wrow + (int64_t)c * 32 * K + kn + 4);
+        }
+        bf16x8 aH, aM, aL;
+        split3(*reinterpret_cast<const float4*>(arow + 16 * s), *reinterpret_cast<const float4*>(arow + 16 * s + 4),
+               aH, aM, aL);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          bf16x8 bH, bM, bL;
+          split3(bc[c][0], bc[c][1], bH, bM, bL);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc[c], 0, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          bc[c][0] = bn[c][0];
+          bc[c][1] = bn[c][1];
         }
       }
     }
     __syncthreads();  // every wave is done reading the A tile
-    // ---- the waves' partial tiles -> LDS (over the A tile), summed in wave order
-    float* rw = red + wave * ROWS * kWfRed;
+    // ---- partial tiles -> LDS red[kq8][row][col], fixed-order sum, epilogue
+    float* red = sA;  // [8][32][128]
 #pragma unroll
-    for (int c = 0; c < Gm::NCG; ++c)
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int e = 0; e < NA; ++e) {
-        const int row = ROWS == 32 ? (e & 3) + 8 * (e >> 2) + 4 * kq : 4 * kq + e;
-        rw[row * kWfRed + Gm::CW * c + lane % Gm::CW] = acc[c][e];
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+        red[(kq8 * kAw32Rows + row) * kWpOut + (2 * cp + c) * 32 + l32] = acc[c][r];
       }
     __syncthreads();
     {
-      // thread: row tid / TPR, columns CPT (tid % TPR) .. + CPT - 1
-      constexpr int TPR = kWfThreads / ROWS, CPT = kWfOut / TPR, NQ = CPT / 4;
-      const int row = tid / TPR, c0 = CPT * (tid % TPR);
-      float4 sm[NQ];
+      const int row = tid >> 5, c4 = tid & 31;  // 4 columns 4 c4 .. 4 c4 + 3
+      float4 sm = *reinterpret_cast<const float4*>(red + row * kWpOut + 4 * c4);
 #pragma unroll
-      for (int qv = 0; qv < NQ; ++qv) sm[qv] = *reinterpret_cast<const float4*>(red + row * kWfRed + c0 + 4 * qv);
-      for (int w = 1; w < kWfWaves; ++w)
-#pragma unroll
-        for (int qv = 0; qv < NQ; ++qv) {
-          const float4 p = *reinterpret_cast<const float4*>(red + (w * ROWS + row) * kWfRed + c0 + 4 * qv);
-          sm[qv].x += p.x;
-          sm[qv].y += p.y;
-          sm[qv].z += p.z;
-          sm[qv].w += p.w;
-        }
-      float s2 = 0.f;
-#pragma unroll
-      for (int qv = 0; qv < NQ; ++qv) {
-        const float4 bv = *reinterpret_cast<const float4*>(bias + c0 + 4 * qv);
-        sm[qv].x = lrelu(sm[qv].x + bv.x);
-        sm[qv].y = lrelu(sm[qv].y + bv.y);
-        sm[qv].z = lrelu(sm[qv].z + bv.z);
-        sm[qv].w = lrelu(sm[qv].w + bv.w);
-        s2 += sm[qv].x * sm[qv].x + sm[qv].y * sm[qv].y + sm[qv].z * sm[qv].z + sm[qv].w * sm[qv].w;
+      for (int j = 1; j < 8; ++j) {
+        const float4 p = *reinterpret_cast<const float4*>(red + (j * kAw32Rows + row) * kWpOut + 4 * c4);
+        sm.x += p.x;
+        sm.y += p.y;
+        sm.z += p.z;
+        sm.w += p.w;
       }
+      const float4 bv = *reinterpret_cast<const float4*>(bias + 4 * c4);
+      const float v[4] = {lrelu(sm.x + bv.x), lrelu(sm.y + bv.y), lrelu(sm.z + bv.z), lrelu(sm.w + bv.w)};
+      float s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
 #pragma unroll
-      for (int o = 1; o < TPR; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+      for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
       const float nrm = sqrtf(s2);
+      const float4 yv = make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
       if (row < nrows) {
+        *reinterpret_cast<float4*>(y + (r0 + row) * kWpOut + 4 * c4) = yv;
+        if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
+      }
+      if (nx.q) {
+        // ---- the next layer's Q projection of these rows (AggNextQ), as in
+        //      agg_w32_kernel: the y tile to LDS (over red, once every thread
+        //      has read it) with each row's next-layer q row (-1: none)
+        float* sY = sA;  // [32][kAw32Lq]
+        int* sU = sLoc;  // [32]
+        __syncthreads();
+        *reinterpret_cast<float4*>(sY + row * kAw32Lq + 4 * c4) = yv;
+        if (c4 == 0) {
+          int u = -1;
+          if (row < nrows) {
+            const int64_t id = nx.S_mem[r0 + row];
+            if ((nx.bits[id >> 6] >> (id & 63)) & 1ull)
+              u = (int)(nx.pref[id >> 6] + __popcll(nx.bits[id >> 6] & ((1ull << (id & 63)) - 1ull)));
+          }
+          sU[row] = u;
+        }
+      }
+    }
+    if (nx.q) {
+      __syncthreads();
+      for (int cq = wave; cq < nx.hid / 32; cq += kAw32Threads / 64) {
+        const float* qrow = nx.Qw + (int64_t)(cq * 32 + l32) * kWpOut + 8 * hh;
+        f32x16 qa;
 #pragma unroll
-        for (int qv = 0; qv < NQ; ++qv)
-          *reinterpret_cast<float4*>(y + (r0 + row) * kWfOut + c0 + 4 * qv) =
-              make_float4(sm[qv].x / nrm, sm[qv].y / nrm, sm[qv].z / nrm, sm[qv].w / nrm);
-        if (tid % TPR == 0 && nrm_out) nrm_out[r0 + row] = nrm;
+        for (int r = 0; r < 16; ++r) qa[r] = 0.f;
+        const float* ap = sA + l32 * kAw32Lq + 8 * hh;
+#pragma unroll 2
+        for (int s = 0; s < 8; ++s) {
+          bf16x8 aH, aM, aL, bH, bM, bL;
+          split3(*reinterpret_cast<const float4*>(ap + 16 * s), *reinterpret_cast<const float4*>(ap + 16 * s + 4),
+                 aH, aM, aL);
+          split3(*reinterpret_cast<const float4*>(qrow + 16 * s), *reinterpret_cast<const float4*>(qrow + 16 * s + 4),
+                 bH, bM, bL);
+          qa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, qa, 0, 0, 0);
+          qa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, qa, 0, 0, 0);
+          qa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, qa, 0, 0, 0);
+          qa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, qa, 0, 0, 0);
+          qa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, qa, 0, 0, 0);
+          qa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, qa, 0, 0, 0);
+        }
+        const int col = cq * 32 + l32;
+        const float bq = nx.Qb[col];
+        float qv[16];
+        int us[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          us[r] = sLoc[(r & 3) + 8 * (r >> 2) + 4 * hh];
+          qv[r] = lrelu(qa[r] + bq);
+          asm volatile("" : "+v"(qv[r]), "+v"(us[r]));
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (us[r] >= 0) nx.q[(int64_t)us[r] * nx.hid + col] = qv[r];
       }
     }
     __syncthreads();  // LDS is reused by the next tile
   }
 }
 
-int agg_wf_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
-  // opt-in (PINSAGE_AGGW_FORM=1): measured even with the LDS-tile forms in the
-  // step (C2 layer 0 38.3 vs 37.1 us, C4 B 4096 237.6 vs 235.4 us) plus the W
-  // split launch on the chain; DESIGN.md §7
-  if (!getenv("PINSAGE_AGGW_FORM") || atoi(getenv("PINSAGE_AGGW_FORM")) != 1) return 0;
-  return out == kWfOut && d > 0 && hid > 0 && d % 32 == 0 && hid % 32 == 0 && T >= 1 && T <= kWfTMax &&
-         wf_lds_bytes<32>(d + hid) <= 160 * 1024;
-}
+int64_t agg_w_planes_bytes(int64_t d, int64_t hid) { return 3 * kWpOut * (d + hid) * 2; }
 
-int64_t agg_wf_planes_bytes(int64_t d, int64_t hid) { return 3 * kWfOut * (d + hid) * 2; }
-
-// the rows form of an expected row count (the planes' fragment order follows it)
-int agg_wf_rows(int64_t S_max) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
-  const int64_t min32 =
-      getenv("PINSAGE_AGGWF32_MIN_ROWS") ? atoll(getenv("PINSAGE_AGGWF32_MIN_ROWS")) : 16 * (int64_t)cus;
-  return S_max >= min32 ? 32 : 16;
-}
-
-int launch_split_wfrag(const float* W, int64_t ldw, int K, int rows, uint16_t* planes, hipStream_t st) {
-  PS_REQUIRE(K % 32 == 0 && (rows == 16 || rows == 32) && ldw >= K && ldw % 4 == 0, kErrArg,
-             "split_wfrag: K % 32 == 0, rows form 16 or 32");
-  const int64_t n = (int64_t)K * kWfOut / 8;
-  if (rows == 32)
-    hipLaunchKernelGGL(split_wfrag_kernel<32>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, ldw, K, planes);
-  else
-    hipLaunchKernelGGL(split_wfrag_kernel<16>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, ldw, K, planes);
-  PS_CHECK_LAUNCH();
-  return kOk;
-}
-
-static int launch_agg_wf(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
-                         const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
-                         int rows, const uint16_t* planes, const float* bias, float* y, float* nrm, float* agg,
-                         hipStream_t st) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
-  static bool prepared = false;
-  if (!prepared) {
-    PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_wf_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024));
-    PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_wf_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024));
-    prepared = true;
-  }
-  // ~3/4 of a tile per block over every CU (one block per CU)
-  const int64_t per = rows * 3 / 4;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(cus, (S_max + per - 1) / per));
-  if (rows == 32)
-    hipLaunchKernelGGL((agg_wf_kernel<32>), dim3(grid), dim3(kWfThreads), (unsigned)wf_lds_bytes<32>(d + hid), st, h,
-                       ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, planes, bias, y, nrm, agg);
-  else
-    hipLaunchKernelGGL((agg_wf_kernel<16>), dim3(grid), dim3(kWfThreads), (unsigned)wf_lds_bytes<16>(d + hid), st, h,
-                       ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, planes, bias, y, nrm, agg);
+int launch_split_wplanes(const float* W, int64_t ldw, int K, uint16_t* planes, hipStream_t st) {
+  PS_REQUIRE(K % 16 == 0 && ldw >= K && ldw % 4 == 0, kErrArg, "split_wplanes: K % 16 == 0, ldw >= K, ldw % 4 == 0");
+  const int64_t n = (int64_t)K * kWpOut / 8;
+  hipLaunchKernelGGL(split_wplanes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, ldw, K, planes);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -856,6 +847,14 @@ static int agg_w32_supported(int64_t d, int64_t hid, int64_t T) {
   const int64_t lds = (int64_t)kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
   return K % 128 == 0 && K + 4 >= 4 * kAw32Out && T <= kAw32TMax && lds <= 160 * 1024;
 }
+
+// the 32-row form (agg_w32s_kernel) also needs its LDS (the 8 partial tiles)
+static int agg_w32s_supported(int64_t d, int64_t hid, int64_t T) {
+  return agg_w32_supported(d, hid, T) && T >= 1 && ws_lds_bytes(d + hid) <= 160 * 1024;
+}
+
+// PINSAGE_AGGW_FORM=0: the 32-row tile as agg_w32_kernel (A/B reference)
+static bool aggw_form0() { return getenv("PINSAGE_AGGW_FORM") && atoi(getenv("PINSAGE_AGGW_FORM")) == 0; }
 
 int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
   const int64_t K = d + hid;
@@ -878,6 +877,11 @@ static int device_cus() {
   return cus;
 }
 
+int agg_w_uses_planes(int64_t d, int64_t hid, int64_t out, int64_t T, int64_t S_est) {
+  return out == kWpOut && S_est > 0 && S_est >= aggw_min_rows32(device_cus()) && agg_w32s_supported(d, hid, T) &&
+         !aggw_form0();
+}
+
 int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est) {
   const int cus = device_cus();
   return S_est > 0 && S_est >= aggw_min_rows32(cus) && agg_w32_supported(d, hid, T) &&
@@ -890,21 +894,10 @@ int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est) {
 int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, const float* q, int hid,
                  const int32_t* loc, const float* wloc, int T, const int* nS, int64_t n_static, int64_t S_max,
                  const float* W, const float* bias, float* y, float* nrm, float* agg, hipStream_t st,
-                 const AggNextQ* next, int* next_done, uint16_t* planes, int planes_rows,
+                 const AggNextQ* next, int* next_done, uint16_t* planes, int planes_ready,
                  const AggHead* head, int* head_done) {
   if (next_done) *next_done = 0;
   if (head_done) *head_done = 0;
-  if (planes && !(next && next->q) && agg_wf_supported(d, hid, kWfOut, T)) {
-    if (S_max <= 0) return kOk;
-    int rows = planes_rows;
-    if (rows == 0) {  // split W here (the engine splits once per forward, ahead)
-      rows = agg_wf_rows(S_max);
-      PS_TRY(launch_split_wfrag(W, d + hid, d + hid, rows, planes, st));
-    }
-    PS_REQUIRE(rows == 16 || rows == 32, kErrArg, "agg_w: planes_rows must be 0, 16 or 32");
-    return launch_agg_wf(h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, S_max, rows, planes, bias, y,
-                         nrm, agg, st);
-  }
   PS_REQUIRE(agg_w_supported(d, hid, kAwOut, T), kErrArg, "agg_w: unsupported shape");
   const int K = d + hid;
   const int lds = kAwRows * (K + 4) * 4 + 2 * kAwRows * kAwTMax * 4 + kAwRows * 4;
@@ -926,13 +919,6 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
   // PINSAGE_AGGW32_MIN_ROWS overrides the switch point (A/B).
   const int64_t min_rows32 = aggw_min_rows32(cus);
   if (S_max >= min_rows32 && agg_w32_supported(d, hid, T)) {
-    const int lds32 = kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
-    static bool prepared32 = false;
-    if (!prepared32) {
-      PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      prepared32 = true;
-    }
     // ~24 rows per block (a 32-row tile with headroom) over every CU
     const int64_t g32 = std::max<int64_t>(1, std::min<int64_t>(cus, (S_max + 23) / 24));
     AggNextQ nx;
@@ -943,8 +929,36 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
       nx = *next;
       if (next_done) *next_done = 1;
     }
-    hipLaunchKernelGGL(agg_w32_kernel, dim3((int)g32), dim3(kAw32Threads), lds32,
-                       st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, nx);
+    if (agg_w32s_supported(d, hid, T) && !aggw_form0()) {
+      const int lds_s = (int)ws_lds_bytes(K);
+      static bool prepared_s = false;
+      if (!prepared_s) {
+        PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32s_kernel<true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32s_kernel<false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        prepared_s = true;
+      }
+      if (planes) {
+        if (!planes_ready) PS_TRY(launch_split_wplanes(W, K, K, planes, st));
+        hipLaunchKernelGGL(agg_w32s_kernel<true>, dim3((int)g32), dim3(kAw32Threads), lds_s, st, h, ldh, d, self_src,
+                           q, hid, loc, wloc, T, nS, n_static, W, (const uint16_t*)planes, bias, y, nrm, agg, nx);
+      } else {
+        hipLaunchKernelGGL(agg_w32s_kernel<false>, dim3((int)g32), dim3(kAw32Threads), lds_s, st, h, ldh, d,
+                           self_src, q, hid, loc, wloc, T, nS, n_static, W, (const uint16_t*)nullptr, bias, y, nrm,
+                           agg, nx);
+      }
+    } else {
+      const int lds32 = kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
+      static bool prepared32 = false;
+      if (!prepared32) {
+        PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        prepared32 = true;
+      }
+      hipLaunchKernelGGL(agg_w32_kernel, dim3((int)g32), dim3(kAw32Threads), lds32,
+                         st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, nx);
+    }
   } else {
     AggHead hd;
     if (head && head->G1w && K >= 2 * kAwOut) {  // (y and H1 beside the output tile in the A tile's LDS)

@@ -623,17 +623,16 @@ int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32
                              const float* w, int64_t n_rows, int64_t T, const float* W,
                              const float* bias, int64_t out, uint16_t* W_planes, float* y,
                              float* norms, float* agg, void* stream) {
-  const bool wf = W_planes && agg_wf_supported(d, hid, out, T);
-  if (!(wf || agg_w_supported(d, hid, out, T)) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX || ldh < d ||
+  if (!agg_w_supported(d, hid, out, T) || n_rows < 0 || q_rows <= 0 || n_rows > INT32_MAX || ldh < d ||
       ldh % 4 != 0) {
-    set_error("conv_agg_project: out_dim must be 128, 1 <= T <= 64, and d, hid multiples of 32 (with W_planes) "
-              "or d + hid a multiple of 64 and d, hid multiples of 4");
+    set_error("conv_agg_project: out_dim must be 128, 1 <= T <= 64, d + hid a multiple of 64 and d, hid "
+              "multiples of 4");
     return kErrArg;
   }
   if (n_rows == 0) return kOk;
   // the engine's kernel (aggw.hip): the form by row count, rows from n_rows
-  // (W_planes: scratch of agg_wf_planes_bytes for the fragment form, which
-  // splits W into it first; null runs the LDS-tile forms)
+  // (W_planes: scratch of 3 x 128 x (d + hid) bf16 that lets the 32-row form
+  // run pipelined, W split into it first; null runs the unpipelined forms)
   return launch_agg_w(h, ldh, (int)d, self_src, q, (int)hid, loc, w, (int)T, nullptr, n_rows, n_rows, W, bias, y,
                       norms, agg, (hipStream_t)stream, nullptr, nullptr, W_planes, 0);
 }

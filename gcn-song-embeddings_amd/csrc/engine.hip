@@ -96,7 +96,7 @@ struct LayerBuf {
   size_t self_src = 0, q_src = 0, loc = 0, wloc = 0;
   size_t q = 0, agg = 0, y = 0, nrm = 0;
   size_t qsplit = 0;  // the Q weight's hi / mid / lo bf16 planes (split-bf16 Q projection)
-  size_t wplanes = 0;  // the W weight's fragment-order bf16 planes (aggw.hip fragment form)
+  size_t wplanes = 0;  // the W weight's fragment-order bf16 planes (aggw.hip pipelined form)
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
          occ2 = 0, occ2b = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
@@ -433,7 +433,7 @@ static void layout(Engine& E) {
     lb.wloc = carve(cur, FS * T * 4);
     lb.q = carve(cur, FN * c.hid * 4);
     lb.qsplit = carve(cur, 3 * c.hid * lb.d * 2);
-    lb.wplanes = carve(cur, agg_wf_planes_bytes(lb.d, c.hid));
+    lb.wplanes = carve(cur, agg_w_planes_bytes(lb.d, c.hid));
     lb.agg = carve(cur, FS * c.hid * 4);
     lb.y = carve(cur, FS * c.out * 4);
     lb.nrm = carve(cur, FS * 4);
@@ -600,23 +600,23 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
   const int Lc = (int)c.n_layers, T = (int)c.T;
   auto cnt = [&](const SetBuf& s) { return at<int>(ws, s.count); };
   LayerBuf& top = E.L[(size_t)Lc - 1];
-  // W of every layer split once into the aggregation kernel's fragment-order
-  // bf16 planes (the rows form picked by the expected frontier size)
-  std::vector<int> wf_rows((size_t)Lc, 0), next_q((size_t)Lc, 0);
+  // W of every layer whose aggregation + W kernel runs pipelined split once
+  // into its fragment-order bf16 planes
+  std::vector<int> wp((size_t)Lc, 0), next_q((size_t)Lc, 0);
   for (int l = 0; E.fused_aggw && E.fused_next_q && l + 1 < Lc; ++l) {
     const LayerBuf& lb = E.L[(size_t)l];
     const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
     next_q[(size_t)l] = E.fused_next_q > 0 || agg_w_next_q_pays(lb.d, c.hid, T, S_est);
   }
-  if (E.fused_aggw == 1) {
+  if (E.fused_aggw) {
     Timed ts(E, "fwd.wsplit", st);
     for (int l = 0; l < Lc; ++l) {
       LayerBuf& lb = E.L[(size_t)l];
-      if (next_q[(size_t)l] || !agg_wf_supported(lb.d, c.hid, c.out, T)) continue;
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
-      wf_rows[(size_t)l] = agg_wf_rows(S_est);
-      PS_TRY(launch_split_wfrag(E.params + lb.pWw, lb.d + c.hid, (int)(lb.d + c.hid), wf_rows[(size_t)l],
-                                at<uint16_t>(ws, lb.wplanes), st));
+      if (!agg_w_supported(lb.d, c.hid, c.out, T) || !agg_w_uses_planes(lb.d, c.hid, c.out, T, S_est)) continue;
+      wp[(size_t)l] = 1;
+      PS_TRY(launch_split_wplanes(E.params + lb.pWw, lb.d + c.hid, (int)(lb.d + c.hid), at<uint16_t>(ws, lb.wplanes),
+                                  st));
     }
   }
   int q_done = 0;  // this layer's q rows came out of the layer below's kernel (AggNextQ)
@@ -665,7 +665,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
       PS_TRY(dep(E, st, E.fork.stream));
       PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
     }
-    if (E.fused_aggw && (wf_rows[(size_t)l] || agg_w_supported(lb.d, c.hid, c.out, T))) {
+    if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {
       // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
       Timed taw(E, lname("fwd.aggw", l), st);
       const int64_t S_est = lb.S.hint > 0 ? std::min(lb.S.hint, lb.S.cap) : lb.S.cap;
@@ -692,7 +692,7 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
                           (int)c.hid, at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), T, cnt(lb.S), 0,
                           S_est, E.params + lb.pWw, E.params + lb.pWb, at<float>(ws, lb.y),
                           at<float>(ws, lb.nrm), at<float>(ws, lb.agg), st, nx.q ? &nx : nullptr, &q_done,
-                          wf_rows[(size_t)l] ? at<uint16_t>(ws, lb.wplanes) : nullptr, wf_rows[(size_t)l],
+                          wp[(size_t)l] ? at<uint16_t>(ws, lb.wplanes) : nullptr, wp[(size_t)l],
                           hd.G1w ? &hd : nullptr, &head_done));
       continue;
     }

@@ -228,10 +228,12 @@ int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const 
  * the engine's kernel: the aggregate formed in registers and written out once,
  * the projection on split-bf16 MFMA.  h f32 [.][ldh], q f32 [q_rows][hid],
  * loc int32 / w f32 [n_rows][T], W f32 [out][d+hid], y f32 [n_rows][out],
- * agg f32 [n_rows][hid].  out == 128, 1 <= T <= 64.  W_planes (device
- * scratch of 3 * out * (d + hid) uint16): W is split into it (fragment-order
- * bf16 planes) and the fragment form runs -- d and hid multiples of 32; null
- * runs the LDS-tile form -- d + hid a multiple of 64, d and hid multiples of 4. */
+ * agg f32 [n_rows][hid].  out == 128, 1 <= T <= 64, d + hid a multiple of 64,
+ * d and hid multiples of 4.  W_planes (nullable device scratch of
+ * 3 * out * (d + hid) uint16): where the 32-row tile runs (>= 16 rows per CU,
+ * d + hid a multiple of 128, d a multiple of 32) W is split into it
+ * (fragment-order bf16 planes) and the tile's gather runs pipelined against its
+ * projection (the same y bitwise); null runs it unpipelined. */
 int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32_t* self_src,
                              const float* q, int64_t hid, int64_t q_rows, const int32_t* loc,
                              const float* w, int64_t n_rows, int64_t T, const float* W,

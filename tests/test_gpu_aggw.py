@@ -24,7 +24,7 @@ def _vp(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def _run(h, d, self_src, q, loc, w, W, bias):
+def _run(h, d, self_src, q, loc, w, W, bias, planes=True):
     import _native as nat
     n_rows, T = loc.shape
     hid = q.shape[1]
@@ -32,7 +32,7 @@ def _run(h, d, self_src, q, loc, w, W, bias):
     y = torch.full((n_rows, out), float("nan"), device="cuda")
     nrm = torch.full((n_rows,), float("nan"), device="cuda")
     agg = torch.full((n_rows, hid), float("nan"), device="cuda")
-    planes = torch.empty(3 * out * (d + hid), dtype=torch.int16, device="cuda")
+    planes = torch.empty(3 * out * (d + hid), dtype=torch.int16, device="cuda") if planes else None
     rc = nat.lib().pinsage_conv_agg_project(
         _vp(h), h.shape[1], d, _vp(self_src), _vp(q), hid, q.shape[0], _vp(loc), _vp(w), n_rows, T, _vp(W),
         _vp(bias), out, _vp(planes), _vp(y), _vp(nrm), _vp(agg),
@@ -67,16 +67,14 @@ CASES = [  # n_rows, d, ldh, hid, T, U (q rows), n_h (h rows)
 ]
 
 
-@pytest.fixture(params=["wf32", "wf16", "lds32", "lds16"])
+@pytest.fixture(params=["s32", "ref32", "lds16"])
 def form(request, monkeypatch):
-    """the kernel form behind pinsage_conv_agg_project: the fragment form
-    (agg_wf_kernel, W split into fragment-order planes; the default) or the
-    LDS-tile forms (PINSAGE_AGGW_FORM=0), each with 32- or 16-row tiles"""
-    kind, rows = request.param[:-2], request.param[-2:]
-    monkeypatch.setenv("PINSAGE_AGGW_FORM", "1" if kind == "wf" else "0")
-    big = "0" if rows == "32" else "1000000000"
-    monkeypatch.setenv("PINSAGE_AGGWF32_MIN_ROWS", big)
-    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", big)
+    """the kernel form behind pinsage_conv_agg_project: the 32-row tile
+    (agg_w32s_kernel: each A fragment split once per two column groups, W read
+    from its fragment-order bf16 planes; the default from 16 rows per CU), the
+    32-row reference tile (agg_w32_kernel, PINSAGE_AGGW_FORM=0) or the 16-row tile"""
+    monkeypatch.setenv("PINSAGE_AGGW_FORM", "0" if request.param == "ref32" else "1")
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0" if request.param.endswith("32") else "1000000000")
     return request.param
 
 
@@ -123,6 +121,29 @@ def test_agg_project_agg_is_the_slot_order_fma_chain(form):
     nat.check(rc, "weighted_agg")
     torch.cuda.synchronize()
     assert torch.equal(agg, ref)
+
+
+@pytest.mark.parametrize("n_rows,d,hid,T,U", [(5704, 512, 512, 10, 10550), (8570, 128, 512, 10, 23190),
+                                              (777, 256, 512, 25, 3000), (300, 256, 512, 50, 2000),
+                                              (45, 128, 512, 3, 40), (100, 128, 384, 7, 90)])
+def test_planes_tile_is_bitwise_the_register_split_tile(n_rows, d, hid, T, U, monkeypatch):
+    """agg_w32s_kernel with W read from its fragment-order planes (written once
+    by split_wplanes_kernel) equals the same tile splitting W in registers
+    (W_planes null): the planes hold split3's pieces, the products and their
+    order are the same -- y, norms and agg bitwise equal."""
+    g = torch.Generator().manual_seed(n_rows + d)
+    h = torch.randn(900, d, generator=g).cuda()
+    q = torch.nn.functional.leaky_relu(torch.randn(U, hid, generator=g), 0.01).cuda()
+    loc = torch.randint(0, U, (n_rows, T), generator=g, dtype=torch.int32).cuda()
+    w = torch.rand(n_rows, T, generator=g).cuda()
+    self_src = torch.randint(0, 900, (n_rows,), generator=g, dtype=torch.int32).cuda()
+    W = torch.randn(128, d + hid, generator=g).cuda() * 0.05
+    bias = torch.rand(128, generator=g).cuda()
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
+    out = [_run(h, d, self_src, q, loc, w, W, bias, planes=pl) for pl in (True, False)]
+    for a, b in zip(*out):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
 
 
 def test_agg_project_rejects_unsupported_shapes():

@@ -41,3 +41,19 @@ def test_torchrun_two_ranks_gloo(scaling):
     assert res["scaling"] == scaling
     per_gpu = res["config"]["batch_per_gpu"]
     assert res["config"]["global_batch"] == (2 * per_gpu if scaling == "weak" else 512)
+
+
+def test_gpus_two_without_launcher_starts_the_ranks():
+    """`bench.py --gpus 2` run directly (no torch.distributed.run) starts the
+    two ranks itself and still prints one whole-job JSON line with n_gpus 2."""
+    env = dict(os.environ, PINSAGE_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["value"] > 0

@@ -382,3 +382,14 @@ def test_torch_operator_library_registers_every_op():
     import pytest
     with pytest.raises(NotImplementedError, match="CPU"):  # HIP dispatch only: fails loudly
         torch.ops.pinsage.linear(x, None, W, None, True)
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    """bench.py started by a launcher with WORLD_SIZE != --gpus exits non-zero
+    before touching the GPU (launch_ranks)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in (r.stderr + r.stdout)
