@@ -220,6 +220,7 @@ struct Engine {
   // backward side streams: [0] transposes (CSR) of the neighbour slots, [1]
   // weight gradients; forked from / joined to the caller's stream with events
   hipStream_t side[2] = {nullptr, nullptr};
+  int side_dev = 0;  // the device side[] and ev were created on (the retired pool's key)
   std::vector<hipEvent_t> ev;
   int ev_next = 0;
   // PINSAGE_DEFER_SIDE bit 0: in the backward, a launch forked onto a side
@@ -246,16 +247,18 @@ struct Engine {
 // Python finaliser inside torch.cuda.graph), and releasing HIP streams /
 // events there invalidates that capture (global capture mode).  An engine
 // destroy therefore makes no HIP call at all.
+// The pool is keyed by the device the streams and events were created on (an
+// engine on another device must not inherit them).
 static std::mutex g_retired_mu;
-static std::vector<hipStream_t> g_retired_streams;
-static std::vector<hipEvent_t> g_retired_events;
+static std::map<int, std::vector<hipStream_t>> g_retired_streams;
+static std::map<int, std::vector<hipEvent_t>> g_retired_events;
 static std::atomic<int64_t> g_live_engines{0};
 
 Engine::~Engine() {
   std::lock_guard<std::mutex> lk(g_retired_mu);
   for (auto& s : side)
-    if (s) g_retired_streams.push_back(s);
-  for (auto& e : ev) g_retired_events.push_back(e);
+    if (s) g_retired_streams[side_dev].push_back(s);
+  for (auto& e : ev) g_retired_events[side_dev].push_back(e);
   // (timing events are bench-only: pinsage_engine_timing(e, 0) releases them)
   g_live_engines--;
 }
@@ -266,20 +269,23 @@ constexpr int kEvents = 32;
 static int ensure_streams(Engine& E) {
   if (E.side[0]) return kOk;
   PS_TRY(csr_prepare());
+  PS_CHECK_HIP(hipGetDevice(&E.side_dev));
   std::lock_guard<std::mutex> lk(g_retired_mu);
+  auto& rs = g_retired_streams[E.side_dev];
+  auto& re = g_retired_events[E.side_dev];
   for (auto& s : E.side) {
-    if (!g_retired_streams.empty()) {
-      s = g_retired_streams.back();
-      g_retired_streams.pop_back();
+    if (!rs.empty()) {
+      s = rs.back();
+      rs.pop_back();
     } else {
       PS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     }
   }
   E.ev.resize(kEvents);
   for (auto& e : E.ev) {
-    if (!g_retired_events.empty()) {
-      e = g_retired_events.back();
-      g_retired_events.pop_back();
+    if (!re.empty()) {
+      e = re.back();
+      re.pop_back();
     } else {
       PS_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }

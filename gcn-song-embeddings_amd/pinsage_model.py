@@ -998,6 +998,7 @@ class _EngineRunner:
                 fx[xo:xo + n_x[c]] = feats[d.ids_x]
                 parts.append(torch.arange(xo, xo + n_x[c], dtype=torch.int64, device=self.dev))
             xo += n_x[c]
+        self._fly_mark_virtual(base_x, sum(n_x))
         ids = torch.cat(parts)
         out = _EngineFn.apply(self, fx, None, ids, tabs, *self.params())
         outs, o0 = [], 0
@@ -1014,20 +1015,25 @@ class _EngineRunner:
 
     def _fly_feats(self, feats, C, n_items, n_valid, n_x=0):
         """Feature rows of fly_calls' node ids: call c's copy of the table at
-        c * n_items (made once per feature tensor); rows from C * n_items are
-        the virtual nodes', written per call group.  A call that writes virtual
-        rows while an earlier call's backward is still pending on the cached
-        buffer (its backward reads those rows) gets its own copy."""
+        c * n_items (made once per feature tensor); rows C * n_items .. + n_x
+        are the virtual nodes', written per call group (_fly_mark_virtual).
+        Every engine call over this buffer keeps a copy of its own virtual rows
+        and puts them back before its backward if another call has overwritten
+        them since (pending and retained-graph backwards)."""
         key = (id(feats), feats.data_ptr(), getattr(feats, "_version", 0), C, int(self.engine.cfg.n_items))
         if getattr(self, "_fly_feat_key", None) != key:
             fx = torch.empty((int(self.engine.cfg.n_items), feats.shape[1]), dtype=feats.dtype, device=self.dev)
             for c in range(C):
                 fx[c * n_items:c * n_items + n_valid] = feats[:n_valid]
             self._fly_feat, self._fly_feat_key = fx, key
-            self._fly_pending = set()
-        if n_x and self._fly_pending:
-            return self._fly_feat.clone()
         return self._fly_feat
+
+    def _fly_mark_virtual(self, base_x, n_x):
+        """The virtual rows [base_x, base_x + n_x) of the shared buffer were just
+        written: a new version (the next engine call records it with a copy)."""
+        self._fly_ver = getattr(self, "_fly_ver", 0) + 1
+        self._fly_cur = self._fly_ver
+        self._fly_x = (base_x, n_x)
 
     def _fly_calls_merged(self, initial_h, feats, ids_c, n_items, n_valid):
         """fly_calls with the calls' walks merged per layer (_fly_tables_merged)."""
@@ -1044,6 +1050,7 @@ class _EngineRunner:
         if n_x:
             fx[base_x:base_x + n_x] = feats[ids_x]
             ids = torch.cat([uniq, torch.arange(base_x, base_x + n_x, dtype=torch.int64, device=self.dev)])
+        self._fly_mark_virtual(base_x, n_x)
         out = _EngineFn.apply(self, fx, None, ids, tabs, *self.params())
         n_u = int(uniq.shape[0])
         out_u = out[:n_u]
@@ -1109,13 +1116,12 @@ class _EngineFn(torch.autograd.Function):
         # pool when the autograd node is freed (after the last backward a
         # retained graph may still run), never earlier
         weakref.finalize(ctx, e.release_workspace, ws)
-        pend = getattr(runner, "_fly_pending", None)
-        if pend is not None and feats is getattr(runner, "_fly_feat", None):
-            # this call's backward reads the shared on-the-fly feature buffer
-            tok = object()
-            pend.add(tok)
-            ctx.fly_tok = tok
-            weakref.finalize(ctx, pend.discard, tok)
+        fxr = getattr(runner, "_fly_x", None)
+        if fxr is not None and fxr[1] and feats is getattr(runner, "_fly_feat", None):
+            # this call's virtual-node rows of the shared on-the-fly feature
+            # buffer (its backward reads them; a later call may overwrite them)
+            b0, nx = fxr
+            ctx.fly_x = (b0, nx, feats[b0:b0 + nx].clone(), runner._fly_cur)
         return out
 
     @staticmethod
@@ -1123,6 +1129,12 @@ class _EngineFn(torch.autograd.Function):
         runner, e, ws = ctx.runner, ctx.engine, ctx.ws
         grads = torch.zeros(e.n_params, dtype=torch.float32, device=runner.dev)
         runner.bind(ctx.feats, ctx.table, grads=grads, tabs=ctx.tabs)
+        fx = getattr(ctx, "fly_x", None)
+        if fx is not None and getattr(runner, "_fly_cur", None) != fx[3]:
+            # another call wrote its virtual rows since this forward: put this
+            # call's back (a retained graph's later backward)
+            ctx.feats[fx[0]:fx[0] + fx[1]] = fx[2]
+            runner._fly_cur = fx[3]
         dout = dout.contiguous().to(torch.float32)
         if ctx.n_bwd:  # a retained graph's next backward: re-zero what the last one accumulated into
             nat.check(nat.lib().pinsage_engine_reset_backward(e.h, nat.ptr(ws), nat.stream_ptr()),
@@ -1131,9 +1143,6 @@ class _EngineFn(torch.autograd.Function):
                                                            nat.stream_ptr()), "set_output_grad")
         nat.check(nat.lib().pinsage_engine_backward(e.h, nat.ptr(ws), nat.stream_ptr()), "backward")
         ctx.n_bwd += 1
-        tok = getattr(ctx, "fly_tok", None)
-        if tok is not None:
-            runner.__dict__.get("_fly_pending", set()).discard(tok)
         out = []
         off = 0
         for p in runner.params():

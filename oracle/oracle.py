@@ -260,15 +260,29 @@ def _put(h, rows_idx, rows):
     return _PutLast.apply(h.detach(), rows_idx, padded)
 
 
+# Test infrastructure only: when a list, every projection of model_forward
+# appends (weight key, bias key or None, its input, its output) so a parity
+# test can weigh a gradient's error by the magnitude of the terms it sums
+# (parity_util.cond_grads).
+_TAPS = None
+
+
+def _linear(p, wk, bk, x):
+    y = F.linear(x, p[wk], p[bk] if bk else None)
+    if _TAPS is not None:
+        _TAPS.append((wk, bk, x.detach(), y))
+    return y
+
+
 def conv_layer(p, i, h, nodes, nb, w, in_dim):
     """One ConvLayer (pinsage_model.py:189-212): f64 weighted mean, fp32 projections."""
     Fn, T = nb.shape
     self_h = h[nodes, :in_dim]
     nbr = h[nb.reshape(-1), :in_dim].reshape(Fn, T, in_dim)
-    q = F.leaky_relu(F.linear(nbr, p[f"conv_layers.{i}.Q.weight"], p[f"conv_layers.{i}.Q.bias"]))
+    q = F.leaky_relu(_linear(p, f"conv_layers.{i}.Q.weight", f"conv_layers.{i}.Q.bias", nbr))
     agg = (w[:, :, None] * q).sum(1) / w.sum(1, keepdim=True)
-    z = F.leaky_relu(F.linear(torch.cat([self_h, agg], 1).float(), p[f"conv_layers.{i}.W.weight"],
-                              p[f"conv_layers.{i}.W.bias"]))
+    z = F.leaky_relu(_linear(p, f"conv_layers.{i}.W.weight", f"conv_layers.{i}.W.bias",
+                             torch.cat([self_h, agg], 1).float()))
     return z / z.norm(dim=1, keepdim=True)
 
 
@@ -297,7 +311,7 @@ def model_forward(p, feats, nodeset, n_layers, T, w_table, nb_table, out_dim, la
         ns_t, w_t, nb_t = (torch.from_numpy(np.ascontiguousarray(a)) for a in (ns, w, nb))
         y = conv_layer(p, i, h, ns_t, nb_t, w_t, in_dims[i])
         h = _put(h, ns_t, y)
-    z = F.linear(F.leaky_relu(F.linear(y, p["G1.weight"], p["G1.bias"])), p["G2.weight"])
+    z = _linear(p, "G2.weight", None, F.leaky_relu(_linear(p, "G1.weight", "G1.bias", y)))
     idx = torch.from_numpy(np.asarray(nodeset, np.int64))
     h = _put(h, idx, z)
     return h[idx, :out_dim]

@@ -82,18 +82,19 @@ def test_train_step_c5_shape_reference_init(tmpdir_cwd):
     backward through three row normalisations of nearly parallel rows is
     ill-conditioned in its linearisation point, so gradients evaluated at the
     GPU's forward and at the oracle's (rows equal to 3e-7) differ by up to
-    ~1e-4 even under one shared cotangent (part B measured 3e-5 .. 1.04e-4
-    across kernel schedules), more with the oracle's own hinge cotangent
-    (part A, ~2e-4).  The forward rows and hinge arguments are held to 1e-4 /
-    1e-6, part B to 2e-4, part A to 1e-3; the kernels themselves are pinned at
-    1e-4 for this shape by test_fixed_cotangent_reference_init[50-3]
-    (random cotangent: well conditioned)."""
+    ~1e-4 norm-relative even under one shared cotangent (part B measured
+    3e-5 .. 1.04e-4 across kernel schedules), more with the oracle's own hinge
+    cotangent (part A, ~2e-4).  The forward rows and hinge arguments are held
+    to 1e-4 / 1e-6, part B componentwise (parity_util.cond_rel) to 1e-4,
+    part A to 1e-3; the kernels themselves are pinned at 1e-4 for this shape
+    by test_fixed_cotangent_reference_init[50-3] (random cotangent: well
+    conditioned)."""
     n = 4000
     g, feats, pos, w, nb = _graph_problem(tmpdir_cwd, n, 1000, 50000, 256, seed=21, hops=300)
     tr = make_trainer(g, n, feats.cuda(), pos, 3, 50, 64, margin=1e-5, seed=7)
     torch.manual_seed(8)
     batch, _ = tr.next_batch()
-    res = check_train_step(tr, feats, w.numpy(), nb.numpy(), batch, strict_a=False, tol_b=2e-4)
+    res = check_train_step(tr, feats, w.numpy(), nb.numpy(), batch, strict_a=False)
     assert res["grad_rel_A_max"] <= 1e-3, res
 
 
@@ -225,3 +226,37 @@ def test_full_size_precompute_and_frontier(cfg):
     for (gs, gw, gn), (rs, rw_, rn_) in zip(got, ref):
         assert np.array_equal(gs.cpu().numpy(), rs)
         assert np.array_equal(gn.cpu().numpy(), rn_) and np.array_equal(gw.cpu().numpy(), rw_)
+
+
+def test_autograd_call_above_the_position_csr_limit():
+    """the deterministic summation of a repeated id's per-position
+    output gradients (conv.hip pos_csr_kernel, one block) covers calls of up to
+    16384 ids (fused steps up to 5461 triples); above that the writers fall
+    back to float atomics -- order-dependent, still correct.  A 20000-id call
+    (every id repeated ~7 times) under a fixed cotangent: forward rows and every
+    gradient within 1e-4 of the oracle -- componentwise: the random cotangents
+    of thousands of rows cancel in every gradient (norm-relative they measured
+    3-7e-4 at 3000 to 20000 ids, below and above the limit alike) -- and two
+    runs within fp32 rounding."""
+    import graph
+    import pinsage_model as pm
+    import synthetic
+    n = 3000
+    pg = synthetic.make_playlist_graph(n, 750, 40000, seed=7)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices)
+    feats = torch.from_numpy(synthetic.make_features(n, 128, seed=8))
+    pm.set_rng_mode("philox")
+    try:
+        torch.manual_seed(0)
+        w, nb = pm.precompute_neighborhoods_topt(g, n, 200, 0.85, 100, None)
+    finally:
+        pm.set_rng_mode("mt19937")
+    ids = np.random.default_rng(5).integers(0, n, 20000)
+    torch.manual_seed(2)
+    m = pm.PinSageModel(g, n, 2, (128, 512, 128), 200, 0.85, 10, (w, nb))
+    fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), 2, 10, seed=3, cond=True)
+    g1 = [p.grad.clone() for p in m.parameters()]
+    fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), 2, 10, seed=3, cond=True)
+    for a, p in zip(g1, m.parameters()):
+        assert ((a - p.grad).norm() / a.norm()).item() <= 1e-6

@@ -101,10 +101,10 @@ def test_dashboard_train_pinsage_flow_c1():
             w, nb = pinsage.nbhds
             # B = 32 with ~half the triples active: the head's gradients are short
             # signed sums (cancelling q / pos / neg cotangents), so part A (oracle
-            # forward) is held to 1e-3 and part B (shared cotangent) to 3e-4; forward
-            # rows, hinge arguments and loss at 1e-4 / 1e-6 (parity_util)
+            # forward) is held to 1e-3; part B (shared cotangent, componentwise),
+            # forward rows, hinge arguments and loss at 1e-4 / 1e-6 (parity_util)
             for rec in records:
-                res = check_record(rec, features, w.numpy(), nb.numpy(), strict_a=False, tol_b=3e-4)
+                res = check_record(rec, features, w.numpy(), nb.numpy(), strict_a=False)
                 assert res["grad_rel_A_max"] <= 1e-3, res
             # --- state.pt written every batch, lr decayed per epoch
             prog = torch.load(os.path.join("runs", "pinsage_openl3_ft", "state.pt"), weights_only=True)

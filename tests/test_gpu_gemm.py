@@ -330,3 +330,50 @@ def test_warp_specialised_gemm_argument_checks():
         N = args.get("N", 128)
         with pytest.raises(RuntimeError, match="cfg 5"):
             _gemm(64, N, K, args.get("ak", 1), 1, A, None, B, C, cfg=5)
+
+
+@pytest.mark.parametrize("site", ["q0", "q1", "dyw", "wgrad_q0", "wgrad_w1"])
+def test_tuner_candidates_are_bitwise_equal(site):
+    """the step's in-context tuner picks, per site, among tile
+    configs 0-3 and 5 without stream-K (pinsage_training._tune_choices); the
+    default step's bitwise reproducibility rests on every candidate summing
+    each output element in the same k order.  At the C2 step's site shapes --
+    gathered A with bias + LeakyReLU (the Q projections), N-major B (dY W), and
+    the weight gradients' split-K slabs with gathered k-rows at the size
+    model's split counts -- every candidate's output is bitwise equal."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    outs = []
+    if site in ("q0", "q1"):
+        M, N, K = (10541, 512, 512) if site == "q0" else (2600, 512, 128)
+        rows = 3 * M
+        A = torch.randn(rows, K, device="cuda", generator=g)
+        a_idx = torch.randint(0, rows, (M,), device="cuda", generator=g, dtype=torch.int32)
+        B = torch.randn(N, K, device="cuda", generator=g) * 0.05
+        bias = torch.randn(N, device="cuda", generator=g)
+        for cfg in (0, 1, 2, 3, 5):
+            C = torch.full((M, N), float("nan"), device="cuda")
+            _gemm(M, N, K, 1, 1, A, a_idx, B, C, bias=bias, act=1, cfg=cfg, sk=0)
+            outs.append(C)
+    elif site == "dyw":
+        M, N, K = 5709, 640, 128
+        A = torch.randn(M, K, device="cuda", generator=g)
+        B = torch.randn(K, N, device="cuda", generator=g) * 0.05
+        for cfg in (0, 1, 2, 3):
+            C = torch.full((M, N), float("nan"), device="cuda")
+            _gemm(M, N, K, 1, 0, A, None, B, C, cfg=cfg, sk=0)
+            outs.append(C)
+    else:
+        # (the engine's size model, choose_wgrad: C2 layer-0 Q weight 32 splits, layer-1 W weight 11)
+        (M, N, K), S = ((512, 512, 10544), 32) if site == "wgrad_q0" else ((128, 640, 1452), 11)
+        A = torch.randn(K, M, device="cuda", generator=g)
+        rows = 3 * K
+        B = torch.randn(rows, N, device="cuda", generator=g)
+        b_idx = torch.randint(0, rows, (K,), device="cuda", generator=g, dtype=torch.int32)
+        for cfg in (0, 1, 2):
+            C = torch.full((S, M, N), float("nan"), device="cuda")
+            _gemm(M, N, K, 0, 0, A, None, B, C, epi=3, splits=S, cfg=cfg, b_idx=b_idx)
+            outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)

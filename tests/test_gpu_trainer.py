@@ -141,10 +141,10 @@ def test_train_after_large_forward_matches_oracle():
                 batch, _ = tr.next_batch()
                 # B = 32, ~14 active triples: the head's gradients are short signed sums
                 # (cancelling q / pos / neg cotangents), so part A (oracle forward) is held
-                # to 1e-3 and part B (shared cotangent) to 3e-4; forward rows, hinge
+                # to 1e-3; part B (shared cotangent, componentwise) and forward rows, hinge
                 # arguments and loss stay at 1e-4 / 1e-6 (parity_util)
                 res = check_train_step(tr, feats, tr.nbhds[0].numpy(), tr.nbhds[1].numpy(), batch,
-                                       strict_a=False, tol_b=3e-4)
+                                       strict_a=False)
                 assert res["grad_rel_A_max"] <= 1e-3, res
                 if it == 0:
                     e = tr.embed()  # all N ids: > 3 * batch_size, a larger engine
@@ -275,5 +275,84 @@ def test_engine_finalised_inside_a_capture():
             batch, _ = tr2.next_batch()
             loss, _, _ = tr2.train_batch(batch)
             assert np.isfinite(float(loss))
+        finally:
+            os.chdir(cwd)
+
+
+def test_native_stepper_matches_python_step_path(monkeypatch):
+    """the captured step's host side as one native call
+    (pinsage_stepper_step, PINSAGE_NATIVE_STEP=1, the default) and in Python
+    (=0) give bitwise-equal losses and parameters over steps that use the
+    look-ahead frontier (equal ahead hits); after capture an out-of-range
+    batch id raises IndexError on the native path and the trainer still takes
+    a valid step afterwards."""
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            monkeypatch.setenv("PINSAGE_AUTOTUNE", "0")
+            pt.PinSage(g, N, feats, pos, log=False, load_save=False)  # (precompute the table once)
+
+            def run(mode):
+                monkeypatch.setenv("PINSAGE_NATIVE_STEP", mode)
+                torch.manual_seed(1)
+                tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+                tr.batch_size = 64
+                torch.manual_seed(2)
+                losses = []
+                for _ in range(8):
+                    batch, _ = tr.next_batch()
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                flat = torch.cat([p.detach().flatten() for p in tr.model.parameters()]).cpu()
+                return tr, losses, flat, tr._fused.ahead_hits
+
+            tr1, l1, p1, h1 = run("1")
+            assert tr1._fused.stepper is not None  # the native path ran
+            tr0, l0, p0, h0 = run("0")
+            assert tr0._fused.stepper is None
+            assert l1 == l0, (l1, l0)
+            assert torch.equal(p1, p0)
+            assert h1 == h0 and h1 > 0, (h1, h0)
+            bad = torch.tensor([[1, 2, 3]] * 63 + [[N + 5, 2, 3]], dtype=torch.int64)
+            with pytest.raises(IndexError):
+                tr1.train_batch(bad)
+            batch, _ = tr1.next_batch()
+            loss = float(tr1.train_batch(batch)[0])
+            torch.cuda.synchronize()
+            assert np.isfinite(loss)
+        finally:
+            os.chdir(cwd)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_engine_on_second_device_after_first_device_engine_destroyed():
+    """streams and events of destroyed engines are pooled per
+    device; an engine built on cuda:1 after one on cuda:0 was destroyed runs
+    its forward and backward on cuda:1 streams."""
+    import gc
+    import pinsage_training as pt
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g, feats, pos = _problem(tmp)
+            torch.manual_seed(1)
+            tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+            out = tr.model(tr.features, torch.tensor([1, 2, 3, 40]))
+            out.sum().backward()
+            torch.cuda.synchronize()
+            del tr, out
+            gc.collect()
+            with torch.cuda.device(1):
+                torch.manual_seed(1)
+                tr = pt.PinSage(g, N, feats.to("cuda:1"), pos, log=False, load_save=False)
+                out = tr.model(tr.features, torch.tensor([1, 2, 3, 40]))
+                out.sum().backward()
+                torch.cuda.synchronize()
+                assert out.device.index == 1
+                assert all(torch.isfinite(p.grad).all() for p in tr.model.parameters())
         finally:
             os.chdir(cwd)
