@@ -253,273 +253,23 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
 
 typedef float aw_f32x16 __attribute__((ext_vector_type(16)));
 
-// The 32-row variant (one 1024-thread workgroup per CU, K split four ways
-// over the waves, v_mfma_f32_32x32x2_f32): reads W once per 32 rows instead
-// of per 16, which wins at K = d + hid = 1024 (C2/C3 layer 0: 41.6 vs 54.9 us
-// at C2); the 16-row kernel above wins at K = 640 (C2 layer 1: 22.5 vs 29.9 us).
+// The 32-row form: one 1024-thread workgroup per CU, W read once per 32 rows
+// (wins at K = d + hid = 1024: C2/C3 layer 0; the 16-row kernel above wins at
+// K = 640, C2 layer 1).
 constexpr int kAw32Rows = 32;     // rows per workgroup
 constexpr int kAw32Out = 128;     // out_dim (4 column groups of 32)
 constexpr int kAw32Threads = 1024;
 constexpr int kAw32TMax = 64;     // fanout held in LDS per row
 constexpr int kAw32Lq = kAw32Out + 4;  // LDS row of the y tile the next-layer Q projection reads
-
-// LDS: A tile [32][K + 4] floats (row stride = 4 mod 64 banks: b128 fragment
-// reads of 16 consecutive rows hit distinct banks), then the tile's slot lists.
 __device__ __forceinline__ int aw32_lda(int K) { return K + 4; }
 
-__global__ __launch_bounds__(kAw32Threads) void agg_w32_kernel(
-    const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
-    const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
-    const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
-    const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y,
-    float* __restrict__ nrm_out, float* __restrict__ agg, AggNextQ nx) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int K = d + hid, lda = aw32_lda(K);
-  float* sA = lds;                                          // [32][lda]
-  int* sLoc = reinterpret_cast<int*>(lds + kAw32Rows * lda);  // [32][T]
-  float* sW = reinterpret_cast<float*>(sLoc + kAw32Rows * kAw32TMax);  // [32][T]
-  int* sSelf = reinterpret_cast<int*>(sW + kAw32Rows * kAw32TMax);     // [32]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // rows dealt in contiguous ranges: block b of G owns [F b / G, F (b+1) / G)
-  // in near-equal tiles of <= 32 rows, so G ~ F / 24 blocks fill the CUs
-  const int64_t F = nS ? (int64_t)*nS : n_static;
-  const int64_t G = gridDim.x, b = blockIdx.x;
-  const int64_t rb = F * b / G, len = F * (b + 1) / G - rb;
-  const int ntile = (int)((len + kAw32Rows - 1) / kAw32Rows);
-  for (int tile = 0; tile < ntile; ++tile) {
-    const int64_t r0 = rb + len * tile / ntile;
-    const int nrows = (int)(rb + len * (tile + 1) / ntile - r0);
-    // ---- slot lists and self-row indices of the tile
-    for (int i = tid; i < kAw32Rows * T; i += kAw32Threads) {
-      const int row = i / T, t = i - row * T;
-      const bool ok = row < nrows;
-      sLoc[row * kAw32TMax + t] = ok ? loc[(r0 + row) * T + t] : 0;
-      sW[row * kAw32TMax + t] = ok ? wloc[(r0 + row) * T + t] : 0.f;
-    }
-    if (tid < kAw32Rows) sSelf[tid] = tid < nrows ? self_src[r0 + tid] : 0;
-    __syncthreads();
-    // ---- self rows -> A[:, 0:d)
-    {
-      const int d4 = d >> 2;
-      for (int i = tid; i < kAw32Rows * d4; i += kAw32Threads) {
-        const int row = i / d4, c4 = i - row * d4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row < nrows) v = *reinterpret_cast<const float4*>(h + (int64_t)sSelf[row] * ldh + 4 * c4);
-        *reinterpret_cast<float4*>(sA + row * lda + 4 * c4) = v;
-      }
-    }
-    // ---- aggregate -> A[:, d:K) and agg (thread: row tid / 32, float4 columns
-    //      (tid % 32) + 32 j); four slots' rows in flight per round
-    {
-      const int row = tid >> 5, c0 = tid & 31, h4 = hid >> 2;
-      const int nj = (h4 + 31) / 32;
-      for (int j0 = 0; j0 < nj; j0 += 4) {
-        float4 a[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row < nrows) {
-          int t = 0;
-          for (; t + 4 <= T; t += 4) {
-            float4 x[4][4];
-            float w[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sLoc[row * kAw32TMax + t + u] * hid);
-              w[u] = sW[row * kAw32TMax + t + u];
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const int c = min(c0 + 32 * (j0 + j), h4 - 1);
-                x[u][j] = qr[c];
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                a[j].x = fmaf(w[u], x[u][j].x, a[j].x);
-                a[j].y = fmaf(w[u], x[u][j].y, a[j].y);
-                a[j].z = fmaf(w[u], x[u][j].z, a[j].z);
-                a[j].w = fmaf(w[u], x[u][j].w, a[j].w);
-              }
-          }
-          for (; t < T; ++t) {
-            const float4* qr = reinterpret_cast<const float4*>(q + (int64_t)sLoc[row * kAw32TMax + t] * hid);
-            const float w = sW[row * kAw32TMax + t];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int c = min(c0 + 32 * (j0 + j), h4 - 1);
-              const float4 x = qr[c];
-              a[j].x = fmaf(w, x.x, a[j].x);
-              a[j].y = fmaf(w, x.y, a[j].y);
-              a[j].z = fmaf(w, x.z, a[j].z);
-              a[j].w = fmaf(w, x.w, a[j].w);
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = c0 + 32 * (j0 + j);
-          if (c < h4) {
-            *reinterpret_cast<float4*>(sA + row * lda + d + 4 * c) = a[j];
-            if (row < nrows) *reinterpret_cast<float4*>(agg + (r0 + row) * hid + 4 * c) = a[j];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ---- projection: wave (kq, cg), k quarter kq, columns 32 cg ..; split-bf16
-    // products (v_mfma_f32_32x32x16_bf16, six per 16-k step: A and W split into
-    // bf16 hi / mid / lo in registers, bf16split.h), 2.67x the fp32 MFMA rate:
-    // at fp32 MFMA the projection of a 32-row tile (8.4 MFLOP) held a CU ~14 us
-    const int cg = wave & 3, kq = wave >> 2;
-    const int l32 = lane & 31, hh = lane >> 5;
-    const int kspan = K >> 2, kb = kq * kspan;
-    const float* wrow = W + (int64_t)(cg * 32 + l32) * K + kb + 8 * hh;
-    const float* arow = sA + l32 * lda + kb + 8 * hh;
-    aw_f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    // chunks of two 16-k steps (32 k); W fragments of chunk c+1 load while c runs
-    const int nch = kspan / 32;
-    float4 bcur[4], bnxt[4];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bcur[2 * s2] = *reinterpret_cast<const float4*>(wrow + 16 * s2);
-      bcur[2 * s2 + 1] = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 4);
-    }
-    for (int ch = 0; ch < nch; ++ch) {
-      const int k0 = 32 * ch;
-      const int kn = ch + 1 < nch ? k0 + 32 : k0;  // (the last chunk reloads itself: no branch)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bnxt[2 * s2] = *reinterpret_cast<const float4*>(wrow + kn + 16 * s2);
-        bnxt[2 * s2 + 1] = *reinterpret_cast<const float4*>(wrow + kn + 16 * s2 + 4);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const float* ap = arow + k0 + 16 * s2;
-        bf16x8 aH, aM, aL, bH, bM, bL;
-        split3(*reinterpret_cast<const float4*>(ap), *reinterpret_cast<const float4*>(ap + 4), aH, aM, aL);
-        split3(bcur[2 * s2], bcur[2 * s2 + 1], bH, bM, bL);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) bcur[s2] = bnxt[s2];
-    }
-    __syncthreads();  // every wave is done reading the A tile
-    // ---- partial tiles -> LDS red[kq][row][col], fixed-order sum, epilogue
-    float* red = sA;  // [4][32][128]
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
-      red[(kq * kAw32Rows + row) * kAw32Out + cg * 32 + l32] = acc[r];
-    }
-    __syncthreads();
-    {
-      const int row = tid >> 5, c4 = tid & 31;  // 4 columns 4 c4 .. 4 c4 + 3
-      float v[4];
-      float s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int col = 4 * c4 + e;
-        float x = red[(0 * kAw32Rows + row) * kAw32Out + col];
-        x += red[(1 * kAw32Rows + row) * kAw32Out + col];
-        x += red[(2 * kAw32Rows + row) * kAw32Out + col];
-        x += red[(3 * kAw32Rows + row) * kAw32Out + col];
-        x = lrelu(x + bias[col]);
-        v[e] = x;
-        s2 += x * x;
-      }
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) s2 += __shfl_xor(s2, o, 64);
-      const float nrm = sqrtf(s2);
-      const float4 yv = make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm);
-      if (row < nrows) {
-        *reinterpret_cast<float4*>(y + (r0 + row) * kAw32Out + 4 * c4) = yv;
-        if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
-      }
-      if (nx.q) {
-        // ---- the next layer's Q projection of these rows (AggNextQ): the y
-        //      tile goes to LDS (over red, once every thread has read it) with
-        //      each row's next-layer q row (-1: not a neighbour there)
-        float* sY = sA;  // [32][kAw32Lq]
-        int* sU = sLoc;  // [32]
-        __syncthreads();
-        *reinterpret_cast<float4*>(sY + row * kAw32Lq + 4 * c4) = yv;
-        if (c4 == 0) {
-          int u = -1;
-          if (row < nrows) {
-            const int64_t id = nx.S_mem[r0 + row];
-            if ((nx.bits[id >> 6] >> (id & 63)) & 1ull)
-              u = (int)(nx.pref[id >> 6] + __popcll(nx.bits[id >> 6] & ((1ull << (id & 63)) - 1ull)));
-          }
-          sU[row] = u;
-        }
-      }
-    }
-    if (nx.q) {
-      __syncthreads();
-      // wave w: output columns 32 cg .. for cg = w, w + 16, ...; K = 128 in
-      // eight 16-k steps, the same k assignment, product order and epilogue
-      // (bias, lrelu) as the GEMM's split-bf16 tile (gemm.hip), so q matches
-      // the next layer's own Q GEMM
-      const int l32 = lane & 31, hh = lane >> 5;
-      for (int cg = wave; cg < nx.hid / 32; cg += kAw32Threads / 64) {
-        const float* qrow = nx.Qw + (int64_t)(cg * 32 + l32) * kAw32Out + 8 * hh;
-        aw_f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        const float* ap = sA + l32 * kAw32Lq + 8 * hh;
-        // (Q fragments straight from L2, two steps per unrolled pair: a deeper
-        // explicit prefetch spilled ~90 VGPRs at this kernel's 128)
-#pragma unroll 2
-        for (int s = 0; s < 8; ++s) {
-          bf16x8 aH, aM, aL, bH, bM, bL;
-          split3(*reinterpret_cast<const float4*>(ap + 16 * s), *reinterpret_cast<const float4*>(ap + 16 * s + 4),
-                 aH, aM, aL);
-          split3(*reinterpret_cast<const float4*>(qrow + 16 * s), *reinterpret_cast<const float4*>(qrow + 16 * s + 4),
-                 bH, bM, bL);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL, bH, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bL, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bM, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aM, bH, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bM, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH, bH, acc, 0, 0, 0);
-        }
-        const int col = cg * 32 + l32;
-        const float bq = nx.Qb[col];
-        // values and destinations first, pinned in registers, then the stores
-        // alone: a use of the loaded bias among the guarded stores made the
-        // compiler wait for every earlier store before each one
-        float qv[16];
-        int us[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          us[r] = sLoc[(r & 3) + 8 * (r >> 2) + 4 * hh];
-          qv[r] = lrelu(acc[r] + bq);
-          asm volatile("" : "+v"(qv[r]), "+v"(us[r]));
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (us[r] >= 0) nx.q[(int64_t)us[r] * nx.hid + col] = qv[r];
-      }
-    }
-    __syncthreads();  // LDS is reused by the next tile
-  }
-}
-
 // ---------------------------------------------------------------- 32-row form, A split once per two column groups
-// The default 32-row tile (agg_w32_kernel above is the unfused-W reference
-// form, PINSAGE_AGGW_FORM=0).  The gather is agg_w32_kernel's (every thread's
-// loads in flight at once; agg bitwise agg_kernel's); the projection is cut
-// differently: wave w owns k eighth w / 2 and column groups 2 (w % 2), +1, so
-// each A fragment read from LDS is split into bf16 hi / mid / lo once for 12
-// MFMAs (agg_w32_kernel: once per 6, every fragment split by four waves), and W
+// The gather: every thread's loads in flight at once (thread: row tid / 32,
+// float4 columns (tid % 32) + 32 j, four slots' rows per round; agg bitwise
+// agg_kernel's).  The projection: wave w owns k eighth w / 2 and column groups
+// 2 (w % 2), +1, so each A fragment read from LDS is split into bf16 hi / mid /
+// lo once for 12 MFMAs (round 4's form: once per 6, every fragment split by
+// four waves, W split in every workgroup: C2 layer 0 36.3 -> 32.5 us), and W
 // comes pre-split from its fragment-order planes (split_wplanes_kernel, one
 // coalesced 1 KiB load per plane and fragment; the next 16-k step's fragments
 // load while the current step's products run).  Without planes (PL false) W is
@@ -853,9 +603,6 @@ static int agg_w32s_supported(int64_t d, int64_t hid, int64_t T) {
   return agg_w32_supported(d, hid, T) && T >= 1 && ws_lds_bytes(d + hid) <= 160 * 1024;
 }
 
-// PINSAGE_AGGW_FORM=0: the 32-row tile as agg_w32_kernel (A/B reference)
-static bool aggw_form0() { return getenv("PINSAGE_AGGW_FORM") && atoi(getenv("PINSAGE_AGGW_FORM")) == 0; }
-
 int agg_w_supported(int64_t d, int64_t hid, int64_t out, int64_t T) {
   const int64_t K = d + hid;
   const int64_t lds = (int64_t)kAwRows * (K + 4) * 4 + 2 * kAwRows * kAwTMax * 4 + kAwRows * 4;
@@ -878,13 +625,12 @@ static int device_cus() {
 }
 
 int agg_w_uses_planes(int64_t d, int64_t hid, int64_t out, int64_t T, int64_t S_est) {
-  return out == kWpOut && S_est > 0 && S_est >= aggw_min_rows32(device_cus()) && agg_w32s_supported(d, hid, T) &&
-         !aggw_form0();
+  return out == kWpOut && S_est > 0 && S_est >= aggw_min_rows32(device_cus()) && agg_w32s_supported(d, hid, T);
 }
 
 int agg_w_next_q_pays(int64_t d, int64_t hid, int64_t T, int64_t S_est) {
   const int cus = device_cus();
-  return S_est > 0 && S_est >= aggw_min_rows32(cus) && agg_w32_supported(d, hid, T) &&
+  return S_est > 0 && S_est >= aggw_min_rows32(cus) && agg_w32s_supported(d, hid, T) &&
          (S_est + kAw32Rows - 1) / kAw32Rows <= cus;
 }
 
@@ -918,7 +664,7 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
   // 50.2 vs 73.4 us; the layers 1 (1.5-2k rows, K 640) 21.5-21.8 vs 24.7-25.3 us.
   // PINSAGE_AGGW32_MIN_ROWS overrides the switch point (A/B).
   const int64_t min_rows32 = aggw_min_rows32(cus);
-  if (S_max >= min_rows32 && agg_w32_supported(d, hid, T)) {
+  if (S_max >= min_rows32 && agg_w32s_supported(d, hid, T)) {
     // ~24 rows per block (a 32-row tile with headroom) over every CU
     const int64_t g32 = std::max<int64_t>(1, std::min<int64_t>(cus, (S_max + 23) / 24));
     AggNextQ nx;
@@ -929,35 +675,23 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
       nx = *next;
       if (next_done) *next_done = 1;
     }
-    if (agg_w32s_supported(d, hid, T) && !aggw_form0()) {
-      const int lds_s = (int)ws_lds_bytes(K);
-      static bool prepared_s = false;
-      if (!prepared_s) {
-        PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32s_kernel<true>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32s_kernel<false>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        prepared_s = true;
-      }
-      if (planes) {
-        if (!planes_ready) PS_TRY(launch_split_wplanes(W, K, K, planes, st));
-        hipLaunchKernelGGL(agg_w32s_kernel<true>, dim3((int)g32), dim3(kAw32Threads), lds_s, st, h, ldh, d, self_src,
-                           q, hid, loc, wloc, T, nS, n_static, W, (const uint16_t*)planes, bias, y, nrm, agg, nx);
-      } else {
-        hipLaunchKernelGGL(agg_w32s_kernel<false>, dim3((int)g32), dim3(kAw32Threads), lds_s, st, h, ldh, d,
-                           self_src, q, hid, loc, wloc, T, nS, n_static, W, (const uint16_t*)nullptr, bias, y, nrm,
-                           agg, nx);
-      }
+    const int lds_s = (int)ws_lds_bytes(K);
+    static bool prepared_s = false;
+    if (!prepared_s) {
+      PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32s_kernel<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32s_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      prepared_s = true;
+    }
+    if (planes) {
+      if (!planes_ready) PS_TRY(launch_split_wplanes(W, K, K, planes, st));
+      hipLaunchKernelGGL(agg_w32s_kernel<true>, dim3((int)g32), dim3(kAw32Threads), lds_s, st, h, ldh, d, self_src,
+                         q, hid, loc, wloc, T, nS, n_static, W, (const uint16_t*)planes, bias, y, nrm, agg, nx);
     } else {
-      const int lds32 = kAw32Rows * (K + 4) * 4 + 2 * kAw32Rows * kAw32TMax * 4 + kAw32Rows * 4;
-      static bool prepared32 = false;
-      if (!prepared32) {
-        PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w32_kernel,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        prepared32 = true;
-      }
-      hipLaunchKernelGGL(agg_w32_kernel, dim3((int)g32), dim3(kAw32Threads), lds32,
-                         st, h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, nx);
+      hipLaunchKernelGGL(agg_w32s_kernel<false>, dim3((int)g32), dim3(kAw32Threads), lds_s, st, h, ldh, d,
+                         self_src, q, hid, loc, wloc, T, nS, n_static, W, (const uint16_t*)nullptr, bias, y, nrm,
+                         agg, nx);
     }
   } else {
     AggHead hd;

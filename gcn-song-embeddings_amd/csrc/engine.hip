@@ -95,7 +95,6 @@ struct LayerBuf {
   int64_t d = 0;    // input dim of the layer
   size_t self_src = 0, q_src = 0, loc = 0, wloc = 0;
   size_t q = 0, agg = 0, y = 0, nrm = 0;
-  size_t qsplit = 0;  // the Q weight's hi / mid / lo bf16 planes (split-bf16 Q projection)
   size_t wplanes = 0;  // the W weight's fragment-order bf16 planes (aggw.hip pipelined form)
   // backward
   size_t dY = 0, dp = 0, dagg = 0, dpq = 0, cnt = 0, bsum = 0, off = 0, cursor = 0, cbase = 0,
@@ -128,12 +127,6 @@ struct Engine {
   // the optimizer pass.  Measured at C2 in the one-launch step graph (bench.py):
   // 0.605-0.615 / - / 0.645-0.648 / 0.611-0.640 / 0.620-0.626 ms per step.
   int stream_mode = getenv("PINSAGE_BWD_STREAMS") ? atoi(getenv("PINSAGE_BWD_STREAMS")) : 0;
-  // weight-gradient GEMMs beside the chain use at most this many workgroups
-  // (PINSAGE_SIDE_GRID; 0 = no cap), leaving the other CUs to the chain
-  int side_grid = getenv("PINSAGE_SIDE_GRID") ? atoi(getenv("PINSAGE_SIDE_GRID")) : 0;
-  // workgroups the size model aims a side-stream weight gradient's split-K at
-  // (the chain's own: 512)
-  int side_wg_target = getenv("PINSAGE_SIDE_WG_TARGET") ? std::max(1, atoi(getenv("PINSAGE_SIDE_WG_TARGET"))) : 512;
   // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
   bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
   // the fused head backward sums repeated batch nodes' loss rows itself (no
@@ -151,9 +144,6 @@ struct Engine {
   // removed: register-pipelined split-bf16 (C2 layer 0 39.7 us),
   // warp-specialised on LDS-DMA (45.8) or on registers (41.4), against 36.5.
   int fused_aggw = getenv("PINSAGE_FUSED_AGGW") ? atoi(getenv("PINSAGE_FUSED_AGGW")) : 1;
-  // Q projections read their weight pre-split into bf16 planes (one small
-  // split launch per layer per forward; the GEMM then converts A only)
-  bool presplit_q = getenv("PINSAGE_PRESPLIT_Q") && atoi(getenv("PINSAGE_PRESPLIT_Q")) != 0;
   // The next layer's Q projection inside the 32-row aggregation + W kernel
   // (AggNextQ, aggw.h): one launch less per upper layer, at the price of the
   // products of every output row (not only the next layer's neighbours) and
@@ -438,7 +428,6 @@ static void layout(Engine& E) {
     lb.loc = carve(cur, FS * T * 4);
     lb.wloc = carve(cur, FS * T * 4);
     lb.q = carve(cur, FN * c.hid * 4);
-    lb.qsplit = carve(cur, 3 * c.hid * lb.d * 2);
     lb.wplanes = carve(cur, agg_w_planes_bytes(lb.d, c.hid));
     lb.agg = carve(cur, FS * c.hid * 4);
     lb.y = carve(cur, FS * c.out * 4);
@@ -648,18 +637,9 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     q.ldc = c.hid;
     q.bias = E.params + lb.pQb;
     q.act = true;
-    if (E.presplit_q && gemm_default_prec() == 1 && lb.d % 8 == 0) {
-      uint16_t* planes = at<uint16_t>(ws, lb.qsplit);
-      Timed ts(E, lname("fwd.q_split", l), st);
-      PS_TRY(launch_split_planes(E.params + lb.pQw, c.hid, lb.d, lb.d, planes, st));
-      q.b_split = planes;
-      q.ldb_split = lb.d;
-    }
     {
       Timed tt(E, lname("fwd.q_gemm", l), st);
-      // the plane-reading tile is pinned bitwise to the in-register split for
-      // whole-tile schedules only (tests/test_gpu_gemm.py): no stream-K with it
-      if (!q.b_split) with_sk(E, ws, q);
+      with_sk(E, ws, q);
       apply_choice(E, lname("fwd.q_gemm", l), q);
       PS_TRY(launch_gemm(q, st));
       E.sk_used[lname("fwd.q_gemm", l)] = gemm_last_stream_k();
@@ -825,8 +805,10 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
   float* const slab = at<float>(ws, main ? E.slab_main : E.slab);
   float* const bslab = at<float>(ws, main ? E.bslab_main : E.bslab);
   int cfg = 0, S = 1;
-  choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S,
-               beside ? E.side_wg_target : 512);
+  // (a side-stream target of 256 workgroups measured faster at C2 and slower
+  // at C4, 128 slower, and a grid cap on side launches even or slower: one
+  // target for both)
+  choose_wgrad(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max, &cfg, &S);
   {
     auto it = E.choice.find(site);
     if (it != E.choice.end()) {
@@ -836,7 +818,6 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
   }
   GemmParams p;
   p.cfg = cfg;
-  if (beside) p.grid_cap = E.side_grid;
   p.M = w.M;
   p.N = w.N;
   p.K_dev = w.K_dev;

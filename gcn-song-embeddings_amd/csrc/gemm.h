@@ -70,8 +70,6 @@ struct GemmParams {
   float* sk_slab = nullptr;
   int* sk_cnt = nullptr;
   int64_t sk_cnt_len = 0;
-  int grid_cap = 0;               // > 0: at most this many workgroups (a launch beside
-                                  // the critical chain leaves the other CUs to it)
   int stream_k = -1;              // -1 choose by size, 0 off, 1 on (when allowed)
   int sk_min_units = 4;           // k-steps per block at least
   // product arithmetic: 0 = v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains);

@@ -975,10 +975,11 @@ bool gemm_ws_supported(const GemmParams& p) {
          p.ldb % 4 == 0;
 }
 
-// PINSAGE_WS_VARIANT (A/B): 0 = 32-k slots, 3 k-blocks ahead, one workgroup
-// per CU (default); 1 = 16-k slots, 2 ahead, two per CU; 2 = 32-k slots, 1 ahead
-template <int BK, int AHEAD, int WPC>
-static int launch_ws_variant(const GemmParams& p, int Mmax, hipStream_t st) {
+// gemm_ws_kernel's launch: 32-k slots, 3 k-blocks ahead, one workgroup per CU
+// (A/B'd against 16-k slots two ahead at two per CU and 32-k slots one ahead:
+// slower, removed)
+static int launch_gemm_ws(const GemmParams& p, int Mmax, hipStream_t st) {
+  constexpr int BK = 32, AHEAD = 3, WPC = 1;
   static bool prepared = false;
   const int lds = kWsSlots * WsGeom<BK>::Slot;
   if (!prepared) {
@@ -994,13 +995,6 @@ static int launch_ws_variant(const GemmParams& p, int Mmax, hipStream_t st) {
   hipLaunchKernelGGL((gemm_ws_kernel<BK, AHEAD, WPC>), dim3(grid), dim3(512), lds, st, p);
   PS_CHECK_LAUNCH();
   return kOk;
-}
-
-static int launch_gemm_ws(const GemmParams& p, int Mmax, hipStream_t st) {
-  static const int variant = getenv("PINSAGE_WS_VARIANT") ? atoi(getenv("PINSAGE_WS_VARIANT")) : 0;
-  if (variant == 1) return launch_ws_variant<16, 2, 2>(p, Mmax, st);
-  if (variant == 2) return launch_ws_variant<32, 1, 1>(p, Mmax, st);
-  return launch_ws_variant<32, 3, 1>(p, Mmax, st);
 }
 
 // rows per tile of each cfg (5: gemm_ws_kernel's 64-row tiles)
@@ -1230,7 +1224,6 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
     const int G = splits > 1 ? splits : tiles_m, W = splits > 1 ? tiles_m * tiles_n : tiles_n;
     const int64_t iters = 8LL * ((G + 7) / 8) * W;
     grid = (int)(iters < 1024 ? iters : 1024);
-    if (p.grid_cap > 0 && grid > p.grid_cap) grid = p.grid_cap;
     grid = (grid + 7) / 8 * 8;
   }
   dim3 g(grid);

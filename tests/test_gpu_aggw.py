@@ -67,14 +67,13 @@ CASES = [  # n_rows, d, ldh, hid, T, U (q rows), n_h (h rows)
 ]
 
 
-@pytest.fixture(params=["s32", "ref32", "lds16"])
+@pytest.fixture(params=["s32", "s32reg", "lds16"])
 def form(request, monkeypatch):
     """the kernel form behind pinsage_conv_agg_project: the 32-row tile
     (agg_w32s_kernel: each A fragment split once per two column groups, W read
     from its fragment-order bf16 planes; the default from 16 rows per CU), the
-    32-row reference tile (agg_w32_kernel, PINSAGE_AGGW_FORM=0) or the 16-row tile"""
-    monkeypatch.setenv("PINSAGE_AGGW_FORM", "0" if request.param == "ref32" else "1")
-    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0" if request.param.endswith("32") else "1000000000")
+    same tile splitting W in registers (no planes), or the 16-row tile"""
+    monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0" if request.param.startswith("s32") else "1000000000")
     return request.param
 
 
@@ -93,7 +92,7 @@ def test_agg_project_matches_f64(n_rows, d, ldh, hid, T, U, n_h, form):
     W = (torch.rand(128, d + hid, generator=g) * 2 - 1) * bound
     bias = torch.full((128,), 0.3)
     loc, w, self_src, W, bias = loc.cuda(), w.cuda(), self_src.cuda(), W.cuda(), bias.cuda()
-    y, nrm, agg = _run(h, d, self_src, q, loc, w, W, bias)
+    y, nrm, agg = _run(h, d, self_src, q, loc, w, W, bias, planes=form != "s32reg")
     ry, rn, ragg = _ref(h, d, self_src, q, loc, w, W, bias)
     assert torch.isfinite(y).all() and torch.isfinite(agg).all()
     assert _rowrel(agg, ragg) <= 1e-6
@@ -114,7 +113,7 @@ def test_agg_project_agg_is_the_slot_order_fma_chain(form):
     self_src = torch.randint(0, 700, (n_rows,), generator=g, dtype=torch.int32).cuda()
     W = torch.randn(128, d + hid, generator=g).cuda() * 0.05
     bias = torch.zeros(128).cuda()
-    _, _, agg = _run(h, d, self_src, q, loc, w, W, bias)
+    _, _, agg = _run(h, d, self_src, q, loc, w, W, bias, planes=form != "s32reg")
     ref = torch.empty(n_rows, hid, device="cuda")
     rc = nat.lib().pinsage_weighted_agg(_vp(q), hid, _vp(loc), _vp(w), n_rows, T, _vp(ref),
                                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))

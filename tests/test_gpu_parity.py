@@ -654,66 +654,6 @@ def test_csr_transpose_ranges_match_atomic_path():
                 os.environ["PINSAGE_CSR_RANGES"] = old
 
 
-def test_presplit_q_weights_train_like_in_register_split():
-    """PINSAGE_PRESPLIT_Q=1 (Q projections read their weight as pre-split bf16
-    planes, re-split every forward from the current parameters) trains like
-    the default in-register split over several Adam steps: same losses and
-    parameters within rounding (the GEMM products are bitwise equal, see
-    test_gpu_gemm.py; the CSR fill order uses atomics), with the Q projections
-    pinned to a tile that reads the planes and the tuner off (PINSAGE_AUTOTUNE=0:
-    its timing-picked split-K counts change the weight gradients' summation
-    order between the two runs, and Adam turns those last-bit differences in
-    near-zero gradients into lr-sized steps: 1.4e-4 apart once on the GPU box)."""
-    import graph
-    import pinsage_training as pt
-    import synthetic
-    pg = synthetic.make_playlist_graph(6000, 1500, 40000, seed=41)
-    indptr, indices = pg.csr()
-    feats = torch.from_numpy(synthetic.make_features(6000, 256, seed=42))
-    pos = torch.from_numpy(synthetic.make_positives(pg, 30000, seed=43))
-    with tempfile.TemporaryDirectory() as tmp:
-        cwd = os.getcwd()
-        os.chdir(tmp)
-        old = {k: os.environ.get(k) for k in ("PINSAGE_PRESPLIT_Q", "PINSAGE_GEMM_CHOICES", "PINSAGE_AUTOTUNE")}
-        try:
-            os.environ["PINSAGE_AUTOTUNE"] = "0"
-            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp,
-                                        nbhds_path=os.path.join(tmp, "nb.pt"))
-            pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
-            # the Q projections pinned to cfg 3 (a tile that runs the plane form)
-            import json
-            choices = os.path.join(tmp, "choices.json")
-            with open(choices, "w") as f:
-                json.dump({"fwd.q_gemm.l0": {"cfg": [3, 0, 0]}, "fwd.q_gemm.l1": {"cfg": [3, 0, 0]}}, f)
-            os.environ["PINSAGE_GEMM_CHOICES"] = choices
-
-            def run(presplit):
-                os.environ["PINSAGE_PRESPLIT_Q"] = presplit
-                torch.manual_seed(5)
-                tr = pt.PinSage(g, 6000, feats, pos, log=False, load_save=False)
-                tr.batch_size = 256
-                torch.manual_seed(6)
-                losses = []
-                for _ in range(5):
-                    batch, _ = tr.next_batch()
-                    losses.append(float(tr.train_batch(batch)[0]))
-                torch.cuda.synchronize()
-                return losses, torch.cat([p.detach().flatten() for p in tr.model.parameters()])
-
-            l0, p0 = run("0")
-            l1, p1 = run("1")
-            for a, b in zip(l0, l1):
-                assert abs(a - b) <= 1e-4 * abs(a) + 1e-7, (l0, l1)
-            assert ((p0 - p1).norm() / p0.norm()).item() < 1e-4
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-            os.chdir(cwd)
-
-
 def test_default_step_is_bitwise_reproducible():
     """two fresh trainers with the default in-context GEMM
     tuner ON and the same seeds end 3 fused steps with bitwise-equal
