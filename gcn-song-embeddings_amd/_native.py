@@ -71,6 +71,12 @@ _SIGS = {
     "pinsage_ppr_topk_segments": (ctypes.c_int, [vp, vp, i64, vp, i64, vp, vp, vp, i64, f32, i64, u32, vp,
                                                  i64, vp, vp, vp, vp, i64, vp]),
     "pinsage_visit_dense": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, vp]),
+    "pinsage_fly_workspace_bytes": (i64, [i64, i64, i64, i64, i64]),
+    "pinsage_fly_init_workspace": (ctypes.c_int, [vp, i64, i64, i64, i64, i64, vp]),
+    "pinsage_fly_sample": (ctypes.c_int, [vp, vp, i64, vp, i64, i64, i64, i64, i64, f32, vp, vp, i64, vp, vp, vp,
+                                          i64, vp, vp, vp, i64, vp, i64, i64, vp, i64, vp, vp]),
+    "pinsage_engine_set_fly": (ctypes.c_int, [vp, i64, vp, vp, i64, i64]),
+    "pinsage_fly_publish_err": (ctypes.c_int, [vp, vp, i64, i64, vp, i64, vp]),
     "pinsage_frontier_workspace": (i64, [i64]),
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),
     "pinsage_frontier_local_idx": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),

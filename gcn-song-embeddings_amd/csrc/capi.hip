@@ -26,10 +26,16 @@ int launch_visit_topk(const int32_t*, const int64_t*, int64_t, int64_t, int64_t,
                       double*, int64_t*, float*, int32_t*, int64_t, hipStream_t);
 int launch_visit_dense(const int32_t*, const int64_t*, int64_t, int64_t, int64_t, double*,
                        hipStream_t);
+int64_t fly_workspace_bytes(int64_t, int64_t, int64_t, int64_t, int64_t);
+int fly_init_workspace(void*, int64_t, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+int fly_publish_err(const int*, void*, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);
+int fly_sample(const int64_t*, const int32_t*, int64_t, const int64_t*, int64_t, int64_t, int64_t, int64_t, int64_t,
+               float, const uint64_t*, void*, int64_t, int32_t* const*, float* const*, int32_t**, int64_t, int64_t*,
+               int*, int64_t*, int64_t, const float*, int64_t, int64_t, float*, int64_t, int*, hipStream_t);
 int launch_walk_runs(const int64_t*, const int32_t*, const int64_t*, int64_t, int, float,
                      const uint32_t*, uint64_t, uint32_t, int64_t, uint2*, int*, int*, hipStream_t);
 int launch_heap_topk(const uint2*, const int*, int64_t, int, int, double*, int64_t*, float*, int32_t*,
-                     int, hipStream_t);
+                     int, hipStream_t, const int* n_src_dev = nullptr);
 int64_t bitset_words(int64_t universe);
 int64_t bitset_blocks(int64_t universe);
 int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
@@ -616,6 +622,38 @@ int pinsage_knn_cosine(const float* emb, int64_t n, int64_t d, int64_t ld, const
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,
                          int64_t n_rows, int64_t T, float* agg, void* stream) {
   return launch_agg(q, (int)hid, loc, w, (int)T, nullptr, n_rows, agg, (hipStream_t)stream);
+}
+
+int64_t pinsage_fly_workspace_bytes(int64_t n, int64_t B, int64_t n_layers, int64_t T, int64_t n_hops) {
+  if (n <= 0 || B <= 0 || n_layers < 1 || n_layers > 8 || T < 1 || n_hops < 1) return -1;
+  return fly_workspace_bytes(n, B, n_layers, T, n_hops);
+}
+
+int pinsage_fly_init_workspace(void* ws, int64_t n, int64_t B, int64_t n_layers, int64_t T, int64_t n_hops,
+                               void* stream) {
+  PS_REQUIRE(ws && n > 0 && B > 0 && n_layers >= 1 && n_layers <= 8 && T >= 1 && n_hops >= 1, kErrArg,
+             "fly_init_workspace: bad argument");
+  return fly_init_workspace(ws, n, B, n_layers, T, n_hops, (hipStream_t)stream);
+}
+
+int pinsage_fly_sample(const int64_t* indptr, const int32_t* indices, int64_t n_all, const int64_t* batch,
+                       int64_t B, int64_t n, int64_t n_layers, int64_t T, int64_t n_hops, float alpha,
+                       const uint64_t* seeds, void* ws, int64_t ws_bytes, int32_t* const* nbt, float* const* wnt,
+                       int32_t** tab_ptrs, int64_t rows_cap, int64_t* pos_ids, int* n_x, int64_t* ids_xo,
+                       int64_t x_cap, const float* feats, int64_t ld_f, int64_t d, float* fx, int64_t ld_x,
+                       int* err, void* stream) {
+  PS_REQUIRE(indptr && indices && batch && seeds && ws && nbt && wnt && tab_ptrs && pos_ids && n_x && ids_xo && err,
+             kErrArg, "fly_sample: null argument");
+  for (int64_t l = 0; l < n_layers; ++l) PS_REQUIRE(nbt[l] && wnt[l], kErrArg, "fly_sample: null table");
+  PS_REQUIRE(!fx || (feats && d > 0 && ld_f >= d && ld_x >= d), kErrArg, "fly_sample: feature rows");
+  return fly_sample(indptr, indices, n_all, batch, B, n, n_layers, T, n_hops, alpha, seeds, ws, ws_bytes, nbt, wnt,
+                    tab_ptrs, rows_cap, pos_ids, n_x, ids_xo, x_cap, feats, ld_f, d, fx, ld_x, err,
+                    (hipStream_t)stream);
+}
+
+int pinsage_fly_publish_err(const int* err, void* ring, int64_t slot_bytes, int64_t R, const int64_t* ctr,
+                            int64_t err_off, void* stream) {
+  return fly_publish_err(err, ring, slot_bytes, R, ctr, err_off, (hipStream_t)stream);
 }
 
 int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32_t* self_src,

@@ -1967,6 +1967,49 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   return kOk;
 }
 
+// The on-the-fly step's virtual nodes (fly.hip): an id repeated inside a call
+// computed once per occurrence, every occurrence's conv output getting the
+// id's summed cotangent (index_put's backward, pinsage_model.py:257-265).  The
+// loss left each call's summed rows in G at the id's rank r with Kc = the
+// occurrence count (the table step's K x, all occurrences being one row);
+// here the real row keeps K = 1 and virtual node j (rank of x0 + j in the top
+// set) gets the same G row with K = 1.  One wave per virtual node.
+__global__ void fly_fix_kernel(float* __restrict__ G, int* __restrict__ Kc, int64_t S_max, int d,
+                               const unsigned long long* __restrict__ bits, const uint32_t* __restrict__ prefix,
+                               const int* __restrict__ n_x, const int64_t* __restrict__ xids, int64_t x0,
+                               int64_t unit) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nx = *n_x;
+  for (int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; j < nx; j += nw) {
+    const int64_t id = xids[j], xv = x0 + j;
+    const int c = (int)(id / unit);
+    const int64_t rr = prefix[id >> 6] + __popcll(bits[id >> 6] & ((1ull << (id & 63)) - 1ull));
+    const int64_t rx = prefix[xv >> 6] + __popcll(bits[xv >> 6] & ((1ull << (xv & 63)) - 1ull));
+    const float* src = G + ((int64_t)c * S_max + rr) * d;
+    float* dst = G + ((int64_t)c * S_max + rx) * d;
+    for (int k = lane; k < d; k += 64) dst[k] = src[k];
+    if (lane == 0) {
+      Kc[c * S_max + rx] = 1;
+      Kc[c * S_max + rr] = 1;
+    }
+  }
+}
+
+int launch_fly_fix(float* G, int* Kc, int64_t S_max, int d, const unsigned long long* bits, const uint32_t* prefix,
+                   const int* n_x, const int64_t* xids, int64_t x0, int64_t unit, int64_t x_cap, const int* nS,
+                   float* dZ, bool combine_dz, hipStream_t st) {
+  hipLaunchKernelGGL(fly_fix_kernel, dim3(grid_for(x_cap * 64, 256)), dim3(256), 0, st, G, Kc, S_max, d, bits, prefix,
+                     n_x, xids, x0, unit);
+  PS_CHECK_LAUNCH();
+  if (combine_dz) {
+    hipLaunchKernelGGL(dz_combine_kernel, dim3(grid_for(S_max * d, 1024, 256)), dim3(1024), 0, st, G, Kc, S_max, nS,
+                       d, dZ);
+    PS_CHECK_LAUNCH();
+  }
+  return kOk;
+}
+
 int launch_loss_monitor(const float* part, int nparts, const float* colpart, int d, int B, float* scal,
                         hipStream_t st) {
   hipLaunchKernelGGL(loss_monitor_kernel, dim3(1), dim3(1024), 0, st, part, nparts, colpart, d, B, scal);

@@ -38,7 +38,10 @@ int launch_mark_table(unsigned long long*, const int32_t*, const int*, int64_t, 
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int launch_top_set(unsigned long long*, int64_t, unsigned long long*, const int64_t*, int64_t,
-                   int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
+                   int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t, int64_t x0 = 0,
+                   const int* x_n = nullptr);
+int launch_fly_fix(float*, int*, int64_t, int, const unsigned long long*, const uint32_t*, const int*, const int64_t*,
+                   int64_t, int64_t, int64_t, const int*, float*, bool, hipStream_t);
 int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const int*, int64_t,
                       const unsigned long long*, const uint32_t*, const unsigned long long*,
                       const uint32_t*, const int32_t*, const float*, int64_t, int, int32_t*,
@@ -228,6 +231,12 @@ struct Engine {
   // the optimizer pass) 0.454-0.467.
   int defer_side = getenv("PINSAGE_DEFER_SIDE") ? atoi(getenv("PINSAGE_DEFER_SIDE")) : 3;
   std::vector<std::function<int()>> pend;  // deferred side launches, in order
+  // the on-the-fly step (pinsage_engine_set_fly, fly.hip): the virtual nodes
+  // x0 .. x0 + *fly_nx - 1 join the top set, and the loss hands each the
+  // summed G row of its real node fly_xids[j] (call fly_xids[j] / fly_unit)
+  int64_t fly_x0 = 0, fly_unit = 1, fly_xcap = 0;
+  const int* fly_nx = nullptr;
+  const int64_t* fly_xids = nullptr;
   ~Engine();
 };
 
@@ -538,7 +547,7 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
   // faulted; synchronised ones did not).
   PS_TRY(launch_top_set(at<unsigned long long>(ws, E.bits_begin),
                         (int64_t)(E.bits_end - E.bits_begin) / 8, bits(top.S), ids, n_pos, n, bsum,
-                        pref(top.S), mem(top.S), cnt(top.S), st));
+                        pref(top.S), mem(top.S), cnt(top.S), st, E.fly_x0, E.fly_nx));
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
     const int32_t* nb_l = lb.nb_tab ? lb.nb_tab : E.nb;
@@ -1405,14 +1414,22 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
   hipStream_t st = (hipStream_t)stream;
   {
     Timed t(*E, "loss", st);
-    E->reps_in_gp = E->fused_head && E->head_rep_sum;
+    // (on the fly the repeated ranks are summed in the loss launch: the
+    // virtual nodes copy the summed rows)
+    const bool fly = E->fly_nx != nullptr;
+    E->reps_in_gp = E->fused_head && E->head_rep_sum && !fly;
     PS_TRY(launch_loss(at<float>(ws, E->Z), (int)c.out, at<int32_t>(ws, E->pos_rank), (int)batch_size,
                        margin, with_monitors ? E->feats : nullptr, E->ld_f, (int)c.d_in,
                        at<int64_t>(ws, E->ids), at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap,
                        at<int>(ws, top.S.count), at<float>(ws, E->dZ), at<float>(ws, E->part),
                        at<float>(ws, E->varpart), at<float>(ws, E->scal), at<float>(ws, E->hinge),
-                       !E->fused_head, !E->fused_head || !E->head_rep_sum, at<int>(ws, E->rank_off),
+                       !E->fused_head && !fly, !E->fused_head || !E->head_rep_sum || fly, at<int>(ws, E->rank_off),
                        at<int32_t>(ws, E->pos_sorted), at<float>(ws, E->Gp), st));
+    if (fly)
+      PS_TRY(launch_fly_fix(at<float>(ws, E->G), at<int>(ws, E->Kc), top.S.cap, (int)c.out,
+                            at<unsigned long long>(ws, top.S.bits), at<uint32_t>(ws, top.S.prefix), E->fly_nx,
+                            E->fly_xids, E->fly_x0, E->fly_unit, E->fly_xcap, at<int>(ws, top.S.count),
+                            at<float>(ws, E->dZ), !E->fused_head, st));
   }
   // the monitors (loss, node-feature loss, variance scalars) beside the
   // backward, on side stream 0, joined at the backward's end (with
@@ -1430,6 +1447,21 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
     return launch_loss_monitor(part, nb4, varpart, out, B, scal, s0);
   };
   return fork_side(*E, st, s0, (E->defer_side & 2) != 0, mon);
+}
+
+int pinsage_engine_set_fly(pinsage_engine* e, int64_t x0, const int* n_x, const int64_t* xids, int64_t unit,
+                           int64_t x_cap) {
+  if (!e || (n_x && (!xids || unit <= 0 || x0 < 0 || x_cap < 0))) {
+    set_error("engine_set_fly: bad argument");
+    return kErrArg;
+  }
+  Engine* E = reinterpret_cast<Engine*>(e);
+  E->fly_x0 = n_x ? x0 : 0;
+  E->fly_nx = n_x;
+  E->fly_xids = n_x ? xids : nullptr;
+  E->fly_unit = n_x ? unit : 1;
+  E->fly_xcap = n_x ? x_cap : 0;
+  return kOk;
 }
 
 int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,

@@ -280,10 +280,13 @@ __global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
 // (zero_words u64 words from zero), mark the batch ids into the top set and
 // finalise it -- one block, replacing a memset, a mark and a finalise launch.
 // Ids outside [0, limit) are skipped (callers validate them).
+// x_n (nullable): the ids x0 .. x0 + *x_n - 1 join the set too (the on-the-fly
+// step's virtual nodes, fly.hip).
 __global__ __launch_bounds__(1024) void bits_top_set_kernel(
     unsigned long long* __restrict__ zero, int64_t zero_words, unsigned long long* bits,
     const int64_t* __restrict__ ids, int64_t n, int64_t limit, int64_t nwords,
-    uint32_t* __restrict__ prefix, int32_t* __restrict__ members, int* __restrict__ count_out) {
+    uint32_t* __restrict__ prefix, int32_t* __restrict__ members, int* __restrict__ count_out, int64_t x0,
+    const int* __restrict__ x_n) {
   for (int64_t w = threadIdx.x; w < zero_words; w += 1024) zero[w] = 0ull;
   __threadfence();
   __syncthreads();
@@ -291,9 +294,23 @@ __global__ __launch_bounds__(1024) void bits_top_set_kernel(
     const int64_t v = ids[i];
     if (v >= 0 && v < limit) atomicOr(bits + (v >> 6), 1ull << (v & 63));
   }
+  if (x_n) {
+    const int64_t nx = *x_n;
+    for (int64_t v = x0 + threadIdx.x; v < x0 + nx; v += 1024)
+      if (v >= 0 && v < limit) atomicOr(bits + (v >> 6), 1ull << (v & 63));
+  }
   __threadfence();
   __syncthreads();
   finalize_block<true>(bits, bits, nullptr, nwords, prefix, members, count_out);
+}
+
+// mark the id range x0 .. x0 + *x_n - 1
+__global__ void bits_mark_range_kernel(unsigned long long* __restrict__ bits, int64_t x0,
+                                       const int* __restrict__ x_n, int64_t limit) {
+  const int64_t nx = *x_n;
+  for (int64_t v = x0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < x0 + nx;
+       v += (int64_t)gridDim.x * blockDim.x)
+    if (v >= 0 && v < limit) atomicOr(bits + (v >> 6), 1ull << (v & 63));
 }
 
 // zero n u64 words (a kernel, not a memset: keeps captured step graphs
@@ -392,11 +409,12 @@ int launch_set_finalize(unsigned long long* dst, const unsigned long long* a,
 // finalise that set (the top frontier of a step)
 int launch_top_set(unsigned long long* zero, int64_t zero_words, unsigned long long* bits,
                    const int64_t* ids, int64_t n, int64_t universe, uint32_t* block_sums,
-                   uint32_t* prefix, int32_t* members, int* count, hipStream_t st) {
+                   uint32_t* prefix, int32_t* members, int* count, hipStream_t st, int64_t x0,
+                   const int* x_n) {
   const int64_t nw = bitset_words(universe);
   if (nw <= kSmallWords) {
     hipLaunchKernelGGL(bits_top_set_kernel, dim3(1), dim3(1024), 0, st, zero, zero_words, bits, ids,
-                       n, universe, nw, prefix, members, count);
+                       n, universe, nw, prefix, members, count, x0, x_n);
     PS_CHECK_LAUNCH();
     return kOk;
   }
@@ -404,6 +422,10 @@ int launch_top_set(unsigned long long* zero, int64_t zero_words, unsigned long l
                      zero_words);
   PS_CHECK_LAUNCH();
   PS_TRY(launch_mark_i64(bits, ids, n, universe, nullptr, st));
+  if (x_n) {
+    hipLaunchKernelGGL(bits_mark_range_kernel, dim3(16), dim3(256), 0, st, bits, x0, x_n, universe);
+    PS_CHECK_LAUNCH();
+  }
   return launch_set_finalize(bits, bits, nullptr, universe, block_sums, prefix, members, count, st);
 }
 

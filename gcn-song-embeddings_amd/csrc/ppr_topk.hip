@@ -45,21 +45,17 @@ __device__ __forceinline__ uint4 philox10_(uint64_t key, uint4 c) {
   return c;
 }
 
+// One source's walk (one wave, LDS keys[2P]): source index s (its runs' slot),
+// graph node src, Philox key seed and stream position pos (kMT: raw words).
 template <bool kMT>
-__global__ __launch_bounds__(64) void walk_runs_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const int64_t* __restrict__ sources, int64_t n_src, int n_hops, float alpha,
-    const uint32_t* __restrict__ raw, uint64_t seed, uint32_t offset, int64_t src_base, int P,
-    uint2* __restrict__ runs, int* __restrict__ n_runs, int* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // [P] keys, [P] run starts
+__device__ __forceinline__ void walk_runs_body(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t s, int64_t src,
+    int n_hops, float alpha, const uint32_t* __restrict__ raw, uint64_t seed, uint32_t offset, uint64_t pos,
+    int P, uint2* __restrict__ runs, int* __restrict__ n_runs, int* __restrict__ err, uint32_t* keys) {
   const int lane = threadIdx.x;
-  const int64_t s = blockIdx.x;
-  if (s >= n_src) return;
-  const int64_t src = sources[s];
   const int64_t sb = indptr[src];
   const int64_t sd = indptr[src + 1] - sb;
   const uint32_t* rw = kMT ? raw + s * 3 * (int64_t)n_hops : nullptr;
-  const uint64_t pos = (uint64_t)(src_base + s);
   int64_t carry_item = src;  // item of the previous round's last hop
   bool carry_rst = true;     // hop -1 "restarted": hop 0 starts at the source
   bool bad = false;
@@ -173,6 +169,40 @@ __global__ __launch_bounds__(64) void walk_runs_kernel(
   if (lane == 0) n_runs[s] = nr;
 }
 
+template <bool kMT>
+__global__ __launch_bounds__(64) void walk_runs_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const int64_t* __restrict__ sources, int64_t n_src, int n_hops, float alpha,
+    const uint32_t* __restrict__ raw, uint64_t seed, uint32_t offset, int64_t src_base, int P,
+    uint2* __restrict__ runs, int* __restrict__ n_runs, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t keys[];  // [P] keys, [P] run starts
+  const int64_t s = blockIdx.x;
+  if (s >= n_src) return;
+  walk_runs_body<kMT>(indptr, indices, s, sources[s], n_hops, alpha, raw, seed, offset, (uint64_t)(src_base + s),
+                      P, runs, n_runs, err, keys);
+}
+
+// The on-the-fly sampler's walks (fly.hip): sources are C calls' nodes at
+// c * id_unit + id, sorted by call, the calls' segment starts and Philox keys
+// on the device (seg[0..C], seeds[c * key_stride]); source s of segment c is
+// the (s - seg[c])-th of its call (the per-call path's numbering).  The grid
+// covers a capacity; sources past *n_src_dev (or seg[C]) return.
+template <typename Src>
+__global__ __launch_bounds__(64) void walk_runs_seg_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, const Src* __restrict__ sources,
+    const int* __restrict__ seg, int C, const uint64_t* __restrict__ seeds, int key_stride, int64_t id_unit,
+    int n_hops, float alpha, uint32_t offset, int P, uint2* __restrict__ runs, int* __restrict__ n_runs,
+    int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+  const int64_t s = blockIdx.x;
+  if (s >= (int64_t)seg[C]) return;
+  int c = 0;
+  while (c + 1 < C && s >= (int64_t)seg[c + 1]) ++c;
+  const int64_t src = (int64_t)sources[s] - (int64_t)c * id_unit;
+  walk_runs_body<false>(indptr, indices, s, src, n_hops, alpha, nullptr, seeds[(int64_t)c * key_stride], offset,
+                        (uint64_t)(s - seg[c]), P, runs, n_runs, err, keys);
+}
+
 // ---------------------------------------------------------------- lane-per-source heap replay
 // libstdc++ __adjust_heap / __push_heap / __make_heap / __pop_heap /
 // __heap_select / __sort_heap over 32-bit entries ordered by count (bits 16..31).
@@ -207,10 +237,11 @@ __device__ __forceinline__ void h_adjust(uint32_t* f, int hole, int len, uint32_
 __global__ __launch_bounds__(64) void heap_topk_kernel(
     const uint2* __restrict__ runs, const int* __restrict__ n_runs, int64_t n_src, int n_hops, int k,
     int kp, int G, double* __restrict__ out_w, int64_t* __restrict__ out_nb, float* __restrict__ out_wn,
-    int32_t* __restrict__ out_nb32, int T_norm) {
+    int32_t* __restrict__ out_nb32, int T_norm, const int* __restrict__ n_src_dev) {
   extern __shared__ __attribute__((aligned(16))) uint32_t heaps[];  // [G][kp]
   __shared__ double rowsum[64];
   const int lane = threadIdx.x;
+  if (n_src_dev) n_src = min(n_src, (int64_t)*n_src_dev);  // (a capacity grid: the count on the device)
   const int64_t s0 = (int64_t)blockIdx.x * G;
   const int64_t s = s0 + lane;
   uint32_t* f = heaps + lane * kp;
@@ -314,7 +345,7 @@ int launch_walk_runs(const int64_t* indptr, const int32_t* indices, const int64_
 
 int launch_heap_topk(const uint2* runs, const int* n_runs, int64_t n_src, int n_hops, int k,
                      double* out_w, int64_t* out_nb, float* out_wn, int32_t* out_nb32, int T_norm,
-                     hipStream_t st) {
+                     hipStream_t st, const int* n_src_dev) {
   if (n_src <= 0) return kOk;
   const int kp = k | 1;
   // sources per block: 64 (one per lane) while the heaps fit 64 KB of LDS,
@@ -328,9 +359,35 @@ int launch_heap_topk(const uint2* runs, const int* n_runs, int64_t n_src, int n_
   const int lds = G * kp * 4;
   PS_REQUIRE(lds <= 64 * 1024, kErrArg, "ppr_topk: k too large for the LDS heaps");
   hipLaunchKernelGGL(heap_topk_kernel, dim3((unsigned)ceil_div(n_src, G)), dim3(64), lds, st, runs,
-                     n_runs, n_src, n_hops, k, kp, G, out_w, out_nb, out_wn, out_nb32, T_norm);
+                     n_runs, n_src, n_hops, k, kp, G, out_w, out_nb, out_wn, out_nb32, T_norm, n_src_dev);
   PS_CHECK_LAUNCH();
   return kOk;
+}
+
+// n_src_cap sources at most, the count in seg[C] (sources int64 or int32)
+template <typename Src>
+static int launch_walk_runs_seg_t(const int64_t* indptr, const int32_t* indices, const Src* sources,
+                                  int64_t n_src_cap, const int* seg, int C, const uint64_t* seeds, int key_stride,
+                                  int64_t id_unit, int n_hops, float alpha, uint32_t offset, uint2* runs,
+                                  int* n_runs, int* err, hipStream_t st) {
+  if (n_src_cap <= 0) return kOk;
+  int P;
+  const int lds = ppr_walk_lds_bytes(n_hops, &P);
+  PS_REQUIRE(lds <= 64 * 1024, kErrArg, "ppr_topk: n_hops too large");
+  hipLaunchKernelGGL(walk_runs_seg_kernel<Src>, dim3((unsigned)n_src_cap), dim3(64), lds, st, indptr, indices,
+                     sources, seg, C, seeds, key_stride, id_unit, n_hops, alpha, offset, P, runs, n_runs, err);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+int launch_walk_runs_seg(const int64_t* indptr, const int32_t* indices, const int64_t* sources64,
+                         const int32_t* sources32, int64_t n_src_cap, const int* seg, int C, const uint64_t* seeds,
+                         int key_stride, int64_t id_unit, int n_hops, float alpha, uint32_t offset, uint2* runs,
+                         int* n_runs, int* err, hipStream_t st) {
+  if (sources64)
+    return launch_walk_runs_seg_t(indptr, indices, sources64, n_src_cap, seg, C, seeds, key_stride, id_unit, n_hops,
+                                  alpha, offset, runs, n_runs, err, st);
+  return launch_walk_runs_seg_t(indptr, indices, sources32, n_src_cap, seg, C, seeds, key_stride, id_unit, n_hops,
+                                alpha, offset, runs, n_runs, err, st);
 }
 
 }  // namespace ps

@@ -571,6 +571,87 @@ def _fly_tables_merged(g, n_items, ids_c, n_layers, n_hops, alpha, T):
     return tabs, uniq, inv, ids_xo % n, inv[pos_x]
 
 
+def _fly_seed_words(n_layers, C=_FLY_CALLS):
+    """The Philox keys of C calls' walks, drawn from torch's generator as C
+    sequential calls draw them (call c, layer l: the (c L + l)-th pair of
+    words; _fly_tables_merged), as an int64 array [C * L] (bit patterns)."""
+    with nat.torch_rng() as mt:
+        d = [int(x) for x in mt.draws(2 * C * n_layers)]
+    keys = [(d[2 * (c * n_layers + l)] << 32) | d[2 * (c * n_layers + l) + 1]
+            for c in range(C) for l in range(n_layers)]
+    return np.array(keys, dtype=np.uint64).view(np.int64)
+
+
+class _FlyDevice:
+    """Buffers of the device on-the-fly sampler (pinsage_fly_sample, fly.hip)
+    for a train step's C = 3 calls of B ids each: per-layer tables [3 n + x_cap]
+    [T] (engine layer order), the engine positions, the virtual nodes, the
+    tiled feature rows (call c's copy of the table at c n, virtual rows after
+    3 n) and the sampler's workspace.  sample() enqueues one step's sampling
+    with no host synchronisation; its tables equal _fly_tables_merged's."""
+
+    def __init__(self, model, B, feats, dev):
+        L = nat.lib()
+        self.model = model
+        self.n = int(model.n_items)
+        self.B = int(B)
+        self.L = int(model.n_layers)
+        self.T = int(model.T)
+        self.n_hops = int(model.n_hops)
+        self.alpha32 = float(np.float32(model.alpha))
+        self.x_cap = _FLY_CALLS * self.B
+        self.rows = _FLY_CALLS * self.n + self.x_cap
+        gc = _as_csr(model.g)
+        self.n_all = gc.number_of_nodes()
+        self.indptr, self.indices = gc.device_csr(dev)
+        self.tabs = [(torch.empty((self.rows, self.T), dtype=torch.int32, device=dev),
+                      torch.empty((self.rows, self.T), dtype=torch.float32, device=dev)) for _ in range(self.L)]
+        self.tab_ptrs = torch.tensor([nb.data_ptr() for nb, _ in self.tabs] + [wn.data_ptr() for _, wn in self.tabs],
+                                     dtype=torch.int64, device=dev)
+        self._nbt = (ctypes.c_void_p * self.L)(*[nb.data_ptr() for nb, _ in self.tabs])
+        self._wnt = (ctypes.c_void_p * self.L)(*[wn.data_ptr() for _, wn in self.tabs])
+        need = L.pinsage_fly_workspace_bytes(self.n, self.B, self.L, self.T, self.n_hops)
+        if need < 0:
+            raise ValueError("fly sampler: bad sizes")
+        self.ws = torch.empty(int(need), dtype=torch.uint8, device=dev)
+        nat.check(L.pinsage_fly_init_workspace(nat.ptr(self.ws), self.n, self.B, self.L, self.T, self.n_hops,
+                                               nat.stream_ptr()), "fly_init_workspace")
+        self.pos_ids = torch.empty(_FLY_CALLS * self.B, dtype=torch.int64, device=dev)
+        self.n_x = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ids_xo = torch.zeros(self.x_cap, dtype=torch.int64, device=dev)
+        self.err = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.seeds = torch.zeros(_FLY_CALLS * self.L, dtype=torch.int64, device=dev)
+        self.batch_dev = torch.zeros((self.B, _FLY_CALLS), dtype=torch.int64, device=dev)
+        self.feats = feats
+        d = int(feats.shape[1])
+        self.fx = torch.empty((self.rows, d), dtype=torch.float32, device=dev)
+        n_valid = min(int(feats.shape[0]), self.n)
+        for c in range(_FLY_CALLS):
+            self.fx[c * self.n:c * self.n + n_valid] = feats[:n_valid]
+
+    def sample(self, batch_dev, pos_out=None):
+        """Enqueue the sampling of batch_dev (int64 [B][3] on the device) with
+        the keys in self.seeds; the engine positions go to pos_out (a device
+        int64 [3 B] view, e.g. the engine workspace's ids) or self.pos_ids."""
+        pos = self.pos_ids if pos_out is None else pos_out
+        nat.check(nat.lib().pinsage_fly_sample(
+            nat.ptr(self.indptr), nat.ptr(self.indices), self.n_all, nat.ptr(batch_dev), self.B, self.n, self.L,
+            self.T, self.n_hops, self.alpha32, nat.ptr(self.seeds), nat.ptr(self.ws), self.ws.numel(), self._nbt,
+            self._wnt, nat.ptr(self.tab_ptrs), self.rows, nat.ptr(pos), nat.ptr(self.n_x),
+            nat.ptr(self.ids_xo), self.x_cap, nat.ptr(self.feats), self.feats.stride(0), int(self.feats.shape[1]),
+            nat.ptr(self.fx), self.fx.stride(0), nat.ptr(self.err), nat.stream_ptr()), "fly_sample")
+
+    def check_err(self):
+        """Raise what the reference raises if the last sampled step met a
+        zero-degree node or drew an id >= n (synchronises)."""
+        e = self.err.tolist()
+        if e[0] != 0x7f7f7f7f:
+            raise RuntimeError("walk: zero-degree node met (the reference's torch.randint(0) raises here)")
+        if e[1]:
+            raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
+                             "zero-weight tail: the reference's h[nb] raises IndexError)")
+
+
 class _DeviceTable:
     """Device mirror of a precomputed (weights, nodes) table: first T columns,
     nodes int32, weights f32 normalised by their f64 row sum."""

@@ -959,6 +959,171 @@ class _FusedStep:
         return out[0], out[1], out[3]
 
 
+class _FusedFlyStep(_FusedStep):
+    """The train step of an on-the-fly model (relevant_nodes_per_layer,
+    pinsage_model.py:142-154; Philox draws) as ONE captured graph: stage the
+    batch, Adam coefficients and the calls' walk keys from the host ring slot
+    the device counter picks; sample every layer of the three calls on the
+    device (pinsage_fly_sample: walks, top-T, next nodesets, virtual nodes for
+    ids repeated inside a call -- the tables of _fly_tables_merged, bitwise);
+    frontier, layers, loss (virtual nodes get their id's summed output
+    gradient: pinsage_engine_set_fly), backward + Adam, publish.  The host's
+    part of a step: the batch (native sampler), the 2 C L key words from
+    torch's generator (where the per-call path draws them), one graph launch.
+
+    A zero-degree node met by a walk, or a drawn id >= n_items, is reported
+    through the ring slot and raised when the host next waits for that slot
+    (up to HOST_RING steps late; the per-call path raises at the draw)."""
+
+    def __init__(self, trainer):
+        super().__init__(trainer)
+        self.ahead = False
+        self.ahead_mode = "0"
+        self.autotune = False
+        self.fd = None
+
+    def ensure(self, B):
+        super().ensure(B)
+        m = self.tr.model
+        feats = self.runner.features(self.tr.features)
+        fkey = (id(feats), feats.data_ptr())
+        if self.fd is None or self.fd.B != B or getattr(self, "_fkey", None) != fkey:
+            self.fd = pm_fly_device(m, B, feats, self.dev)
+            self._fkey = fkey
+            self.graphs = None
+            self._fly_ring = None
+        if getattr(self, "_fly_ring", None) is not self.ring:  # (super().ensure may have rebuilt it)
+            self.graphs = None
+            L = int(m.n_layers)
+            mp = int(self.runner.engine.cfg.max_pos)
+            # slot: [ids | Adam coefficients | walk keys | error words]
+            self.slot_ids, self.slot_coef = 0, mp * 8
+            self.slot_seeds = self.slot_coef + 16
+            self.slot_err = self.slot_seeds + 3 * L * 8
+            self.slot_bytes = self.slot_err + 8
+            self.ring = torch.zeros((self.HOST_RING, self.slot_bytes), dtype=torch.uint8).pin_memory()
+            self.ring_ev = [None] * self.HOST_RING
+            for k in range(self.HOST_RING):
+                self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32)[0] = 0x7f7f7f7f
+            self._fly_ring = self.ring
+
+    def _slot_write_ids(self, k, off, batch, B):
+        ids = self.ring[k, off:off + 3 * B * 8].view(torch.int64)
+        ids.copy_(torch.as_tensor(batch).reshape(-1).to(torch.int64))
+        n_valid = min(int(self.tr.model.n_items), int(self.fd.feats.shape[0]))
+        if int(ids.min()) < 0 or int(ids.max()) >= n_valid:
+            raise IndexError(f"node ids out of range for {n_valid} items")
+
+    def _check_slot(self, k):
+        e = self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32).tolist()
+        self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32)[0] = 0x7f7f7f7f
+        self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32)[1] = 0
+        if e[0] != 0x7f7f7f7f:
+            raise RuntimeError("walk: zero-degree node met (the reference's torch.randint(0) raises here)")
+        if e[1]:
+            raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
+                             "zero-weight tail: the reference's h[nb] raises IndexError)")
+
+    def _fly_seq(self, B):
+        """One step's device work (the captured graph's contents)."""
+        L = nat.lib()
+        e = self.runner.engine
+        fd = self.fd
+        st = nat.stream_ptr()
+        ws = self.wss[0]
+        coef = ctypes.c_void_p(self.stage_view[0].data_ptr() + 3 * B * 8)
+        nat.check(L.pinsage_step_stage(nat.ptr(self.ring), self.slot_bytes, self.HOST_RING, nat.ptr(self.ctr),
+                                       self.slot_ids, 3 * B * 8, nat.ptr(fd.batch_dev), self.slot_coef, coef, st),
+                  "step_stage")
+        nat.check(L.pinsage_step_stage(nat.ptr(self.ring), self.slot_bytes, self.HOST_RING, nat.ptr(self.ctr),
+                                       self.slot_seeds, fd.seeds.numel() * 8, nat.ptr(fd.seeds), 0, None, st),
+                  "step_stage")
+        fd.sample(fd.batch_dev, pos_out=self.ids_view[0])
+        nat.check(L.pinsage_engine_frontier(e.h, nat.ptr(ws), nat.ptr(self.ids_view[0]), 3 * B, st), "frontier")
+        nat.check(L.pinsage_engine_forward_layers(e.h, nat.ptr(ws), st), "forward_layers")
+        nat.check(L.pinsage_engine_loss(e.h, nat.ptr(ws), B, float(self.tr.margin), 1, st), "loss")
+        if not self._tuned:  # once: frontier sizes of a real batch pick the GEMM tiles
+            e.tune(ws)
+            self._tuned = True
+        self._backward(0, True)
+        nat.check(L.pinsage_fly_publish_err(nat.ptr(fd.err), nat.ptr(self.ring), self.slot_bytes, self.HOST_RING,
+                                            nat.ptr(self.ctr), self.slot_err, st), "fly_publish_err")
+        self._publish(0)
+
+    def _bind_fly(self, on):
+        r = self.runner
+        e = r.engine
+        fd = self.fd
+        if on:
+            r.bind(fd.fx, None, grads=self.grads, adam_m=self.m, adam_v=self.v, tabs=fd.tabs)
+            r.set_layer_tables(fd.tabs)
+            nat.check(nat.lib().pinsage_engine_set_fly(e.h, 3 * fd.n, nat.ptr(fd.n_x), nat.ptr(fd.ids_xo), fd.n,
+                                                       fd.x_cap), "engine_set_fly")
+        else:
+            r.set_layer_tables(None)
+            nat.lib().pinsage_engine_set_fly(e.h, 0, None, None, 1, 0)
+
+    def _call(self, batch):
+        batch = torch.as_tensor(batch)
+        B = int(batch.shape[0])
+        self.ensure(B)
+        self.B_cur = B
+        k = self.nstep % self.HOST_RING
+        if self.ring_ev[k] is not None:  # the step that used this slot is done
+            tw = time.perf_counter()
+            self.ring_ev[k].synchronize()
+            self.wait_s += time.perf_counter() - tw
+            self._check_slot(k)
+        self._slot_write_ids(k, self.slot_ids, batch, B)
+        self._slot_write_coef(k)
+        L = int(self.tr.model.n_layers)
+        self.ring[k, self.slot_seeds:self.slot_seeds + 3 * L * 8].view(torch.int64).copy_(
+            torch.from_numpy(pm_fly_seed_words(L)))
+        sig = (B, id(self.fd), id(self.runner.engine))
+        if self.graphs is not None and (self.graph_sig != sig or not self.use_graph):
+            self.graphs = None
+        if self.graphs is not None:
+            self.graphs.replay()
+        else:
+            self._bind_fly(True)
+            try:
+                if self._tuned and self.use_graph:  # hints set: capture, then replay for this step
+                    was = gc.isenabled()
+                    gc.collect()
+                    gc.disable()
+                    try:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g):
+                            self._fly_seq(B)
+                    finally:
+                        if was:
+                            gc.enable()
+                    self.graphs = g
+                    self.graph_sig = sig
+                    g.replay()
+                else:
+                    self._fly_seq(B)
+            finally:
+                self._bind_fly(False)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.ring_ev[k] = ev
+        out = self.out_ring[self.nstep % self.OUT_RING]
+        self.nstep += 1
+        self.host_step += 1
+        return out[0], out[1], out[3]
+
+
+def pm_fly_device(model, B, feats, dev):
+    import pinsage_model as pm
+    return pm._FlyDevice(model, B, feats, dev)
+
+
+def pm_fly_seed_words(L):
+    import pinsage_model as pm
+    return pm._fly_seed_words(L)
+
+
 class PinSage:
     """The PinSage trainer (pinsage_training.py:108-295): same attributes,
     defaults and file formats; hyperparameters are bound at construction
@@ -1073,6 +1238,27 @@ class PinSage:
             self._fused = _FusedStep(self)
         return self._fused(batch)
 
+    def _fly_fused_ok(self, batch):
+        """Whether the on-the-fly step runs as the captured device step
+        (_FusedFlyStep): Philox draws with the merged calls, no model hooks,
+        one process, the fused sampler's regime; PINSAGE_FLY_FUSED=0 keeps the
+        host-orchestrated path."""
+        import pinsage_model as pm
+        from torch.nn.modules import module as _nnm
+        model = self.model
+        if (os.environ.get("PINSAGE_FLY_FUSED", "1") == "0" or pm.get_rng_mode() == "mt19937"
+                or os.environ.get("PINSAGE_FLY_MERGE", "1") == "0" or self._dp()[1] > 1):
+            return False
+        if (model._forward_pre_hooks or model._forward_hooks or model._forward_hooks_with_kwargs
+                or model._forward_hooks_always_called or model._backward_hooks or model._backward_pre_hooks
+                or _nnm._global_forward_hooks or _nnm._global_forward_pre_hooks or _nnm._global_backward_hooks
+                or _nnm._global_backward_pre_hooks):
+            return False
+        n_all = pm._as_csr(model.g).number_of_nodes()
+        T, h = int(model.T), int(model.n_hops)
+        return (torch.as_tensor(batch).dim() == 2 and int(torch.as_tensor(batch).shape[0]) >= 2 and T * 64 <= n_all
+                and h <= 8192 and h + T < 65536)
+
     def _train_batch_fly(self, batch):
         """The reference's train_batch (pinsage_training.py:181-215) step for
         step when the model samples on the fly (relevant_nodes_per_layer,
@@ -1081,6 +1267,10 @@ class PinSage:
         generator as the reference does -- max_margin_loss, the engine's HIP
         backward per call (autograd), torch's Adam."""
         batch = torch.as_tensor(batch)
+        if self._fly_fused_ok(batch):
+            if getattr(self, "_fused_fly", None) is None:
+                self._fused_fly = _FusedFlyStep(self)
+            return self._fused_fly(batch)
         model = self.model
         from torch.nn.modules import module as _nnm
         if (model._forward_pre_hooks or model._forward_hooks_with_kwargs or model._forward_hooks_always_called

@@ -151,6 +151,37 @@ int pinsage_ppr_topk_segments(const int64_t* indptr, const int32_t* indices, int
                               float alpha, int64_t k, uint32_t offset, void* ws, int64_t ws_bytes,
                               double* w_out, int64_t* nb_out, float* wn_out, int32_t* nb32_out,
                               int64_t t_norm, void* stream);
+/* ------------------------------------------------------------------ on-the-fly step (device)
+ * relevant_nodes_per_layer (pinsage_model.py:142-154) for a train step's three
+ * model calls (pinsage_training.py:183-185), all sizes on the device (no host
+ * synchronisation: the on-the-fly step is captured whole).  Philox draws: call
+ * c, fly layer k (0 = top) walks with key seeds[c * n_layers + k] and numbers
+ * its sources from 0, as pinsage_ppr_topk_segments.  batch int64 [B][3]; call
+ * c's node v is c * n + v in every table and position; tables nbt / wnt
+ * (host arrays of n_layers device pointers, engine layer order: 0 = bottom)
+ * [rows_cap >= 3 n + x_cap][T], rows of every layer's nodes written; virtual
+ * nodes 3 n + j (j < *n_x <= x_cap, x_cap >= 3 B) are the earlier occurrences
+ * of ids repeated inside a call (the last occurrence owns the id's row).
+ * tab_ptrs: device array of 2 n_layers pointers (the nbt, then the wnt of
+ * every engine layer).  pos_ids [3 B]: the engine's positions (3 i + c);
+ * ids_xo [x_cap]: virtual node j's real node; fx (nullable) [3 n + x_cap][ld_x]:
+ * the virtual rows j get feats[ids_xo[j] % n].  err[0] != 0x7f7f7f7f: a walk
+ * met a zero-degree node; err[1] != 0: a drawn id >= n (the reference raises).
+ * ws: pinsage_fly_workspace_bytes, initialised once by pinsage_fly_init_workspace. */
+int64_t pinsage_fly_workspace_bytes(int64_t n, int64_t B, int64_t n_layers, int64_t T, int64_t n_hops);
+int pinsage_fly_init_workspace(void* ws, int64_t n, int64_t B, int64_t n_layers, int64_t T, int64_t n_hops,
+                               void* stream);
+int pinsage_fly_sample(const int64_t* indptr, const int32_t* indices, int64_t n_all, const int64_t* batch,
+                       int64_t B, int64_t n, int64_t n_layers, int64_t T, int64_t n_hops, float alpha,
+                       const uint64_t* seeds, void* ws, int64_t ws_bytes, int32_t* const* nbt, float* const* wnt,
+                       int32_t** tab_ptrs, int64_t rows_cap, int64_t* pos_ids, int* n_x, int64_t* ids_xo,
+                       int64_t x_cap, const float* feats, int64_t ld_f, int64_t d, float* fx, int64_t ld_x,
+                       int* err, void* stream);
+/* The sampler's two error words into the host ring slot (*ctr % R) at err_off
+ * (the captured on-the-fly step reports them there; the host reads them when
+ * it next waits for that slot). */
+int pinsage_fly_publish_err(const int* err, void* ring, int64_t slot_bytes, int64_t R, const int64_t* ctr,
+                            int64_t err_off, void* stream);
 /* sample_neighborhood (pinsage_model.py:88-101): dense f64 [n_src][n_all]. */
 int pinsage_visit_dense(const int32_t* trace, const int64_t* sources, int64_t n_src,
                         int64_t n_hops, int64_t n_all, double* dense, void* stream);
@@ -470,6 +501,13 @@ int pinsage_engine_set_hints(pinsage_engine* e, const int64_t* S, const int64_t*
 int pinsage_engine_site_stream_k(const pinsage_engine* e, const char* site);
 int pinsage_engine_set_layer_table(pinsage_engine* e, int64_t layer, const int32_t* nb,
                                    const float* wn, int64_t ld);
+/* The on-the-fly step's virtual nodes (pinsage_fly_sample): ids x0 .. x0 +
+ * *n_x - 1 join every frontier's top set, and pinsage_engine_loss hands
+ * virtual node j the summed output gradient of its real node xids[j] (call
+ * xids[j] / unit), each occurrence's conv output with multiplicity 1
+ * (index_put's backward, pinsage_model.py:257-265).  n_x = null: off. */
+int pinsage_engine_set_fly(pinsage_engine* e, int64_t x0, const int* n_x, const int64_t* xids, int64_t unit,
+                           int64_t x_cap);
 /* Per-site GEMM choice (a tuner measures the sites in context and fixes them):
  * site names as the timing sites -- fwd.q_gemm.lN, fwd.w_gemm.lN, bwd.dcat.lN,
  * bwd.dh.lN (block tile config cfg 0..3, stream_k 0/1), bwd.w_wgrad.lN,
