@@ -413,8 +413,9 @@ def main():
         gemm_choices = tr._fused.tuned_choices if tr._fused is not None else None
         # per-kernel timing pass (HIP events on the launch stream), separate from the timed
         # loop; runs the same kernels eagerly (events are not recorded inside the graph)
-        if tr._fused is not None:
-            tr._fused.use_graph = False
+        fused_any = tr._fused if tr._fused is not None else getattr(tr, "_fused_fly", None)
+        if fused_any is not None:
+            fused_any.use_graph = False
         eng = tr.model.runner().engine
         nat.lib().pinsage_engine_timing(eng.h, 1)
         n_t = 1 if micro else max(5, min(20, args.steps))
@@ -431,7 +432,7 @@ def main():
             off = eng.off
             # micro-batched: the frontier of the last slice's outputs-only forward
             rn = tr.model.runner()
-            ws = tr._fused.ws if tr._fused is not None else (rn._ws if rn._ws is not None else rn.last_ws)
+            ws = fused_any.ws if fused_any is not None else (rn._ws if rn._ws is not None else rn.last_ws)
             cN0 = int(eng.view(ws, int(off.count_N[0]), torch.int32, 1).item())
             cS0 = int(eng.view(ws, int(off.count_S[0]), torch.int32, 1).item())
             cN1 = (int(eng.view(ws, int(off.count_N[1]), torch.int32, 1).item())
