@@ -1055,7 +1055,8 @@ __device__ __forceinline__ unsigned long long match_digit(int dig, bool valid) {
   return m;
 }
 __global__ __launch_bounds__(1024) void pos_csr_kernel(const int32_t* __restrict__ pos_rank, int n,
-                                                       int* __restrict__ rank_off, int32_t* __restrict__ pos_sorted) {
+                                                       const int* __restrict__ nS, int* __restrict__ rank_off,
+                                                       int32_t* __restrict__ pos_sorted) {
   extern __shared__ unsigned pk[];
   if (n > kPosCsrMax) {
     if (threadIdx.x == 0) rank_off[0] = -1;
@@ -1115,16 +1116,21 @@ __global__ __launch_bounds__(1024) void pos_csr_kernel(const int32_t* __restrict
     src = dst;
     dst = t;
   }
+  // every rank 0..nS gets an offset, the ranks without a position too (the
+  // on-the-fly step's virtual nodes: top-set ranks no batch position names)
   for (int i = tid; i < n; i += blockDim.x) {
     const unsigned v = src[i];
     const int r = (int)(v >> 16);
     pos_sorted[i] = (int32_t)(v & 0xffffu);
-    if (i == 0 || (int)(src[i - 1] >> 16) != r) rank_off[r] = i;
-    if (i == n - 1) rank_off[r + 1] = n;
+    const int rp = i == 0 ? -1 : (int)(src[i - 1] >> 16);
+    for (int q = rp + 1; q <= r; ++q) rank_off[q] = i;
   }
+  const int qe = max(*nS, (int)(src[n - 1] >> 16) + 1);
+  for (int q = (int)(src[n - 1] >> 16) + 1 + tid; q <= qe; q += blockDim.x) rank_off[q] = n;
 }
 
-int launch_pos_csr(const int32_t* pos_rank, int64_t n, int* rank_off, int32_t* pos_sorted, hipStream_t st) {
+int launch_pos_csr(const int32_t* pos_rank, int64_t n, const int* nS, int* rank_off, int32_t* pos_sorted,
+                   hipStream_t st) {
   static bool prepared = false;
   if (!prepared) {
     PS_CHECK_HIP(hipFuncSetAttribute((const void*)pos_csr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1133,7 +1139,7 @@ int launch_pos_csr(const int32_t* pos_rank, int64_t n, int* rank_off, int32_t* p
   }
   if (n <= 0) return kOk;
   hipLaunchKernelGGL(pos_csr_kernel, dim3(1), dim3(1024), n <= kPosCsrMax ? (unsigned)kPosCsrLds : 0u, st, pos_rank,
-                     (int)std::min<int64_t>(n, INT32_MAX), rank_off, pos_sorted);
+                     (int)std::min<int64_t>(n, INT32_MAX), nS, rank_off, pos_sorted);
   PS_CHECK_LAUNCH();
   return kOk;
 }

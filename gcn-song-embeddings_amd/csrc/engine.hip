@@ -61,7 +61,7 @@ int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const i
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
                 const int64_t*, float*, int*, int64_t, const int*, float*, float*, float*, float*,
                 float*, bool, bool, const int*, const int32_t*, float*, hipStream_t);
-int launch_pos_csr(const int32_t*, int64_t, int*, int32_t*, hipStream_t);
+int launch_pos_csr(const int32_t*, int64_t, const int*, int*, int32_t*, hipStream_t);
 int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
 int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
                 hipStream_t);
@@ -575,7 +575,7 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
                              pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank),
                              prev ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr, (int)c.out,
                              prev ? cnt(*prev) : nullptr, st));
-    if (is_top) PS_TRY(launch_pos_csr(at<int32_t>(ws, E.pos_rank), n_pos, at<int>(ws, E.rank_off),
+    if (is_top) PS_TRY(launch_pos_csr(at<int32_t>(ws, E.pos_rank), n_pos, cnt(top.S), at<int>(ws, E.rank_off),
                                       at<int32_t>(ws, E.pos_sorted), st));
   }
   // the transposes of the neighbour slots (CSR of slot occurrences by q row,

@@ -103,7 +103,10 @@ def test_fused_fly_step_trains_like_the_per_call_path(L, T, monkeypatch):
     four steps with ids repeated inside and across calls: the same generator
     state after every step, losses within 1e-5 and parameters within 1e-5
     (rounding: the loss and Adam are summed in a different order), and the
-    graph path is the one that ran."""
+    graph path is the one that ran.  The caching allocator is first handed a
+    block of random words, so workspace the step reads before writing (the
+    position CSR's offsets of the virtual ranks, which no position names)
+    shows up here instead of depending on what an earlier test left."""
     import pinsage_model as pm
     import pinsage_training as pt
     pm.set_rng_mode("philox")
@@ -117,6 +120,9 @@ def test_fused_fly_step_trains_like_the_per_call_path(L, T, monkeypatch):
 
                 def run(fused):
                     monkeypatch.setenv("PINSAGE_FLY_FUSED", fused)
+                    torch.cuda.empty_cache()
+                    junk = torch.randint(0, 1 << 20, (64 << 20,), dtype=torch.int32, device="cuda")
+                    del junk  # (the block stays cached: the workspaces are carved from it)
                     torch.manual_seed(1)
                     tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
                     torch.manual_seed(2)
