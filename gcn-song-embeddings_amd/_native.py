@@ -96,6 +96,9 @@ _SIGS = {
     "pinsage_split_planes": (ctypes.c_int, [vp, i64, i64, i64, vp, vp]),
     "pinsage_linear_split_b": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, vp, i64, ctypes.c_int,
                                               vp, i64, ctypes.c_int, vp]),
+    "pinsage_split_ilv": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, vp]),
+    "pinsage_linear_ilv": (ctypes.c_int, [vp, i64, vp, i64, vp, i64, i64, vp, vp, i64, vp, i64, ctypes.c_int, vp,
+                                          i64, vp]),
     "pinsage_step_stage": (ctypes.c_int, [vp, i64, i64, vp, i64, i64, vp, i64, vp, vp]),
     "pinsage_step_publish": (ctypes.c_int, [vp, i64, vp, i64, vp, vp]),
     "pinsage_stream_hold": (ctypes.c_int, [i64, vp]),

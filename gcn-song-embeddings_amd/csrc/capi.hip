@@ -574,6 +574,44 @@ int pinsage_split_planes(const float* W, int64_t rows, int64_t cols, int64_t ldw
   return launch_split_planes(W, rows, cols, ldw, out, (hipStream_t)stream);
 }
 
+int pinsage_split_ilv(const float* src, int64_t ld, int64_t rows, int64_t K, uint16_t* out, int64_t ldo,
+                      void* stream) {
+  if (K <= 0 || K > INT32_MAX) {
+    set_error("split_ilv: bad argument");
+    return kErrArg;
+  }
+  return launch_split_ilv(src, ld, rows, (int)K, out, ldo, (hipStream_t)stream);
+}
+
+int pinsage_linear_ilv(const uint16_t* A_ilv, int64_t lda_ilv, const int32_t* a_idx, int64_t M, const int* M_dev,
+                       int64_t M_max, int64_t K, const float* W, const uint16_t* W_ilv, int64_t ldw_ilv,
+                       const float* bias, int64_t N, int act, float* C, int64_t ldc, void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX || M_max < 0 ||
+      M_max > INT32_MAX || (M_dev && M_max == 0)) {
+    set_error("linear_ilv: bad argument");
+    return kErrArg;
+  }
+  GemmParams p;
+  p.M = (int)M;
+  p.M_dev = M_dev;
+  p.M_max = (int)M_max;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.a_ilv = A_ilv;
+  p.lda_ilv = lda_ilv;
+  p.a_idx = a_idx;
+  p.b = W;
+  p.ldb = K;
+  p.b_ilv = W_ilv;
+  p.ldb_ilv = W_ilv ? ldw_ilv : 0;
+  p.c = C;
+  p.ldc = ldc;
+  p.bias = bias;
+  p.act = act != 0;
+  p.prec = 1;
+  return launch_gemm(p, (hipStream_t)stream);
+}
+
 int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, int64_t M, int64_t K,
                            const float* W, const uint16_t* W_planes, int64_t ldws,
                            const float* bias, int64_t N, int act, float* C, int64_t ldc, int cfg,

@@ -85,7 +85,19 @@ struct GemmParams {
   // the 1.5x larger B image); ignored elsewhere.  K and ldb_split % 8 == 0.
   const uint16_t* b_split = nullptr;
   int64_t ldb_split = 0;
+  // split-bf16, K-major A and B read from interleaved plane tables
+  // (launch_split_ilv; row strides lda_ilv / ldb_ilv in bf16 elements, >= 3K),
+  // A's rows gathered by a_idx; replace a and b.  Static K % 16 == 0, store
+  // epilogue; runs cfg 0's 128 x 128 tiles.
+  const uint16_t* a_ilv = nullptr;
+  const uint16_t* b_ilv = nullptr;
+  int64_t lda_ilv = 0, ldb_ilv = 0;
 };
+
+// Interleaved plane table of src[rows][K] (GemmParams::a_ilv / b_ilv): row r
+// at out + r * ldo (ldo >= 3K bf16 elements, % 8 == 0), K/16 stages of the
+// six 16-B chunks hi0 hi1 mid0 mid1 lo0 lo1 (8 k each).  K % 16 == 0.
+int launch_split_ilv(const float* src, int64_t ld, int64_t rows, int K, uint16_t* out, int64_t ldo, hipStream_t st);
 
 // hi / mid / lo bf16 planes of a row-major fp32 matrix w[rows][cols] (row
 // stride ldw floats): out[p][r][c], plane stride rows*cols (cols % 8 == 0)

@@ -119,6 +119,43 @@ struct KSplitOp {
   }
 };
 
+// Interleaved-plane operand (GemmParams::a_ilv / b_ilv, launch_split_ilv):
+// each row of the table is K/16 stages of 96 B -- the hi / mid / lo bf16 of
+// its 16 k as six 16-B chunks, chunk w = plane * 2 + half -- so one row's
+// stage is a single contiguous piece however the rows are gathered.  LDS
+// image: row r's six chunks at slots r*6 .., chunk w at slot (w + ((r >> 3) & 1))
+// % 6 (the rotation makes every ds_read_b128 lane group of a fragment
+// conflict-free at the 96-B row pitch).
+template <int R>
+struct IlvOp {
+  static constexpr int SZ = R * 24;          // floats per stage image
+  static constexpr int NI = R * 6 / 256;     // 16-B DMAs per thread per stage
+  static_assert(R * 6 % 256 == 0, "whole DMAs per thread");
+  __device__ static __forceinline__ float4 frag(const float* img, int row, int w) {
+    int sl = w + ((row >> 3) & 1);
+    sl = sl >= 6 ? sl - 6 : sl;
+    return *reinterpret_cast<const float4*>(img + (row * 6 + sl) * 4);
+  }
+  const char* rp[NI];
+  __device__ __forceinline__ void init(int tid, int r0, int rmax, const uint16_t* t, int64_t ld,
+                                       const int32_t* idx) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = j * 256 + tid, row = i / 6, sl = i - row * 6;
+      int w = sl - ((row >> 3) & 1);
+      w = w < 0 ? w + 6 : w;
+      const int g = r0 + row, rc = g < rmax ? g : rmax - 1;
+      rp[j] = reinterpret_cast<const char*>(t + (int64_t)(idx ? idx[rc] : rc) * ld) + w * 16;
+    }
+  }
+  __device__ __forceinline__ void issue(unsigned img, int wave, int k0, int, int) const {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      glds16(reinterpret_cast<const float*>(rp[j] + (k0 / 16) * 96), img + (unsigned)(j * 256 + wave * 64) * 16u);
+  }
+  __device__ __forceinline__ void zero_tail(float*, int, int, int) const {}  // (K % 16 == 0)
+};
+
 // MN-major operand: global [k][col] (k rows optionally gathered; columns >= c1
 // from a second matrix), LDS image linear [BK][R].
 template <int R, int BK>
@@ -217,14 +254,18 @@ __device__ __forceinline__ void quad_transpose16(float (&v)[16], int lane) {
 // tile loop is inlined once and the code is ~40 % smaller, which a launch
 // pays for in instruction fetch before its first MFMA.
 template <bool AK, bool BKM, int WM, int WN, int TM, int TN, int BK, int NSMAX = 4, int WPC = 2,
-          bool BF = false, bool PB = false, bool SK = true>
+          bool BF = false, bool PB = false, bool SK = true, int IL = 0>
 __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
   static_assert(!BF || BK % 16 == 0, "split-bf16 products: 16-k steps");
   static_assert(!PB || (BF && BKM), "pre-split B: split-bf16 products, K-major B");
+  // IL 1: A and B from interleaved tables; 2: A from one, B fp32 split in registers
+  static_assert(!IL || (BF && AK && BKM && !PB && !SK && BK == 16), "interleaved planes: split bf16, K-major A and B");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  using OpA = typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type;
-  using OpB = typename std::conditional<
+  using OpA = typename std::conditional<
+      IL != 0, IlvOp<BM>, typename std::conditional<AK, KOp<BM, BK>, MNOp<BM, BK>>::type>::type;
+  using OpBp = typename std::conditional<
       PB, KSplitOp<BN, BK>, typename std::conditional<BKM, KOp<BN, BK>, MNOp<BN, BK>>::type>::type;
+  using OpB = typename std::conditional<IL == 1, IlvOp<BN>, OpBp>::type;
   constexpr int SZA = OpA::SZ, SZB = OpB::SZ, SZS = SZA + SZB;
   constexpr int NG = OpA::NI + OpB::NI;  // DMAs per wave per stage
   constexpr bool GA = !AK, GB = !BKM;    // operands that may need gathered k-rows
@@ -279,9 +320,13 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
 
     OpA opa;
     OpB opb;
-    if constexpr (AK) opa.init(tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
+    if constexpr (IL) {
+      opa.init(tid, m0, M, p.a_ilv, p.lda_ilv, p.a_idx);
+      if constexpr (IL == 1) opb.init(tid, n0, N, p.b_ilv, p.ldb_ilv, nullptr);
+    } else if constexpr (AK) opa.init(tid, m0, M, p.a, p.lda, p.a_idx, p.a2, p.lda2, p.a2_idx);
     else opa.init(tid, m0, M, p.a, p.lda, idxA, -1, nullptr, 0, nullptr);
-    if constexpr (PB) opb.init(tid, n0, N, p.b_split, p.ldb_split, N);
+    if constexpr (IL == 1) {
+    } else if constexpr (PB) opb.init(tid, n0, N, p.b_split, p.ldb_split, N);
     else if constexpr (BKM) opb.init(tid, n0, N, p.b, p.ldb, nullptr, nullptr, 0, nullptr);
     else opb.init(tid, n0, N, p.b, p.ldb, idxB, p.N1, p.b2, p.ldb2, idxB2);
 
@@ -361,13 +406,23 @@ __global__ __launch_bounds__(256, WPC) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
             const int r = (wm * TM + i) * 32 + l32;
-            split3(OpA::frag(As, r, 16 * t + 8 * h), OpA::frag(As, r, 16 * t + 8 * h + 4), aH[i], aM[i],
-                   aL[i]);
+            if constexpr (IL) {  // interleaved planes: chunk plane * 2 + h of row r
+              aH[i] = __builtin_bit_cast(bf16x8, OpA::frag(As, r, h));
+              aM[i] = __builtin_bit_cast(bf16x8, OpA::frag(As, r, 2 + h));
+              aL[i] = __builtin_bit_cast(bf16x8, OpA::frag(As, r, 4 + h));
+            } else {
+              split3(OpA::frag(As, r, 16 * t + 8 * h), OpA::frag(As, r, 16 * t + 8 * h + 4), aH[i], aM[i],
+                     aL[i]);
+            }
           }
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int c = (wn * TN + j) * 32 + l32;
-            if constexpr (PB) {  // the planes' 8 k of this lane: one chunk each
+            if constexpr (IL == 1) {
+              bH[j] = __builtin_bit_cast(bf16x8, OpB::frag(Bs, c, h));
+              bM[j] = __builtin_bit_cast(bf16x8, OpB::frag(Bs, c, 2 + h));
+              bL[j] = __builtin_bit_cast(bf16x8, OpB::frag(Bs, c, 4 + h));
+            } else if constexpr (PB) {  // the planes' 8 k of this lane: one chunk each
               using P = typename OpB::P;
               bH[j] = __builtin_bit_cast(bf16x8, P::frag(Bs, c, 8 * t + 4 * h));
               bM[j] = __builtin_bit_cast(bf16x8, P::frag(Bs + P::SZ, c, 8 * t + 4 * h));
@@ -1085,6 +1140,38 @@ int launch_split_planes(const float* w, int64_t rows, int64_t cols, int64_t ldw,
   return kOk;
 }
 
+// one thread per (row, 8 k): the interleaved table row (IlvOp): stage
+// k / 16, chunks plane * 2 + (k % 16) / 8
+__global__ __launch_bounds__(256) void split_ilv_kernel(const float* __restrict__ src, int64_t ld, int64_t rows,
+                                                        int K, uint16_t* __restrict__ out, int64_t ldo) {
+  const int k8 = K / 8;
+  const int64_t n = rows * k8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / k8;
+    const int kc = (int)(i - r * k8);
+    const float4 a = *reinterpret_cast<const float4*>(src + r * ld + 8 * kc);
+    const float4 b = *reinterpret_cast<const float4*>(src + r * ld + 8 * kc + 4);
+    bf16x8 H, Md, L;
+    split3(a, b, H, Md, L);
+    uint16_t* o = out + r * ldo + (kc >> 1) * 48 + (kc & 1) * 8;
+    *reinterpret_cast<bf16x8*>(o) = H;
+    *reinterpret_cast<bf16x8*>(o + 16) = Md;
+    *reinterpret_cast<bf16x8*>(o + 32) = L;
+  }
+}
+
+int launch_split_ilv(const float* src, int64_t ld, int64_t rows, int K, uint16_t* out, int64_t ldo, hipStream_t st) {
+  PS_REQUIRE(K > 0 && K % 16 == 0 && ld % 4 == 0 && ld >= K && ldo % 8 == 0 && ldo >= 3LL * K &&
+                 (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0 && rows >= 0,
+             kErrArg, "split_ilv: K a multiple of 16, ld of 4, ldo of 8 and >= 3K, 16-B aligned pointers");
+  const int64_t n = rows * (K / 8);
+  if (n == 0) return kOk;
+  hipLaunchKernelGGL(split_ilv_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 16384)), dim3(256), 0, st,
+                     src, ld, rows, K, out, ldo);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 template <bool AK, bool BKM>
 static void launch_cfg(int cfg, dim3 g, hipStream_t st, const GemmParams& p) {
   if constexpr (BKM) {
@@ -1168,6 +1255,26 @@ int launch_gemm(const GemmParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.sk_min_units >= 1, kErrArg, "gemm: sk_min_units must be positive");
   PS_REQUIRE(p.cfg != 4 || (p.a_kmajor && p.b_kmajor), kErrArg,
              "gemm: cfg 4 (four workgroups per CU) needs K-major A and B");
+  if (p.a_ilv || p.b_ilv) {  // interleaved plane tables: cfg 0's 128 x 128 tiles, gathered A rows
+    PS_REQUIRE(p.a_ilv && p.a_kmajor && p.b_kmajor && !p.K_dev && p.K % 16 == 0 && p.K1 < 0 &&
+                   (p.epi == kEpiStore || p.epi == kEpiAccum) && !p.c2 && p.lda_ilv % 8 == 0 &&
+                   p.lda_ilv >= 3LL * p.K && (uintptr_t)p.a_ilv % 16 == 0 &&
+                   (p.b_ilv ? p.ldb_ilv % 8 == 0 && p.ldb_ilv >= 3LL * p.K && (uintptr_t)p.b_ilv % 16 == 0
+                            : p.b != nullptr),
+               kErrArg, "gemm: interleaved planes need A's table, static K % 16 == 0 and a store epilogue");
+    g_last_sk = 0;
+    const int tiles_m = (Mmax + 127) / 128, tiles_n = (p.N + 127) / 128;
+    const int64_t iters = 8LL * ((tiles_m + 7) / 8) * tiles_n;
+    const int grid = (int)((std::min<int64_t>(iters, 1024) + 7) / 8 * 8);
+    if (p.b_ilv)
+      hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 2, 2, 16, 4, 2, true, false, false, 1>), dim3(grid),
+                         dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((gemm_f32_kernel<true, true, 2, 2, 2, 2, 16, 4, 2, true, false, false, 2>), dim3(grid),
+                         dim3(256), 0, st, p);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
   if (p.cfg == 5) {  // the warp-specialised split-bf16 kernel (K-major A and B, store epilogue)
     if (gemm_ws_supported(p) && (p.prec == 1 || (p.prec < 0 && gemm_default_prec() == 1))) {
       g_last_sk = 0;

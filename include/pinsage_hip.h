@@ -246,6 +246,22 @@ int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, in
                            const float* W, const uint16_t* W_planes, int64_t ldws,
                            const float* bias, int64_t N, int act, float* C, int64_t ldc, int cfg,
                            void* stream);
+/* Interleaved split-bf16 table of src[rows][K] (K % 16 == 0, ld % 4 == 0):
+ * row r at out + r * ldo (bf16 elements, ldo % 8 == 0, ldo >= 3K) holds K/16
+ * stages of six 16-B chunks -- hi, mid, lo bf16 of the stage's 16 values, 8
+ * per chunk -- the exact split the GEMM does in registers.  The input feature
+ * table is split once (features do not change during training), W_Q per step. */
+int pinsage_split_ilv(const float* src, int64_t ld, int64_t rows, int64_t K, uint16_t* out, int64_t ldo,
+                      void* stream);
+/* C[m][0..N) = act(A[a_idx[m]] . W[n] + bias[n]) from an interleaved table of
+ * A (rows gathered by a_idx) and W [N][K] either as its interleaved table
+ * (W_ilv, pinsage_split_ilv) or, W_ilv null, fp32 split in registers: bitwise
+ * pinsage_linear's split-bf16 product on the same 128 x 128 tiles, every
+ * gathered row's 16-k stage one contiguous 96-B read.  M static or *M_dev <=
+ * M_max.  The layer-0 Q projection (pinsage_model.py:201). */
+int pinsage_linear_ilv(const uint16_t* A_ilv, int64_t lda_ilv, const int32_t* a_idx, int64_t M, const int* M_dev,
+                       int64_t M_max, int64_t K, const float* W, const uint16_t* W_ilv, int64_t ldw_ilv,
+                       const float* bias, int64_t N, int act, float* C, int64_t ldc, void* stream);
 /* agg[f] = sum_t w[f][t] * q[loc[f][t]]  (weights already normalised;
  * pinsage_model.py:202). */
 int pinsage_weighted_agg(const float* q, int64_t hid, const int32_t* loc, const float* w,

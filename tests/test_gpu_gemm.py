@@ -296,6 +296,62 @@ def test_presplit_b_argument_checks():
                                       _vp(C), 128, 3, stream) != 0  # K % 8
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 128, 16), (37, 128, 144), (200, 256, 528), (3000, 512, 512),
+                                   (10541, 512, 512), (24369, 512, 128), (500, 200, 272), (77, 72, 48)])
+def test_interleaved_tables_bitwise(M, N, K):
+    """The Q projection from interleaved split-bf16 tables (pinsage_split_ilv
+    of the whole row table, split once, and of W -- or W fp32 split in
+    registers; pinsage_linear_ilv gathers the rows): bitwise the in-register split-bf16 GEMM of cfg 0 (the same
+    128 x 128 tiles, products and k order), with M static and as a device-side
+    count below M_max (the engine's form), within 2e-6 of float64; the table
+    holds the RN-even split of torch's bf16 cast; bad arguments are refused."""
+    import _native as nat
+    lib = nat.lib()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    old = lib.pinsage_gemm_get_prec()
+    try:
+        assert lib.pinsage_gemm_set_prec(1) == 0
+        pool = M + 7
+        A = torch.randn(pool, K + 4, device="cuda", generator=g)  # (row stride K + 4: the first K columns)
+        A *= torch.exp2(torch.randint(-20, 20, (pool, 1), device="cuda", generator=g).float())
+        W = torch.randn(N, K, device="cuda", generator=g) * 0.05
+        bias = torch.randn(N, device="cuda", generator=g)
+        a_idx = torch.randint(0, pool, (M,), device="cuda", generator=g, dtype=torch.int32)
+        C0 = torch.full((M, N), float("nan"), device="cuda")
+        _gemm(M, N, K, 1, 1, A, a_idx, W, C0, bias=bias, act=1, cfg=0, sk=0)
+        lda = 3 * K + 8  # a padded table row
+        at = torch.full((pool, lda), 0x7fff, dtype=torch.int16, device="cuda")
+        wt = torch.empty(N, 3 * K, dtype=torch.int16, device="cuda")
+        nat.check(lib.pinsage_split_ilv(_vp(A), K + 4, pool, K, _vp(at), lda, stream), "split A")
+        nat.check(lib.pinsage_split_ilv(_vp(W), K, N, K, _vp(wt), 3 * K, stream), "split W")
+        torch.cuda.synchronize()
+        # table row = K/16 stages x (hi0 hi1 mid0 mid1 lo0 lo1) chunks of 8
+        ref = _split_planes_ref(A[:, :K].contiguous()).view(3, pool, K // 16, 2, 8)
+        got = at[:, :3 * K].view(pool, K // 16, 3, 2, 8).permute(2, 0, 1, 3, 4)
+        assert torch.equal(got, ref)
+        m_dev = torch.tensor([M], dtype=torch.int32, device="cuda")
+        for dev_m, w_tab in [(False, True), (True, True), (True, False)]:  # W as a table or fp32
+            C1 = torch.full((M, N), float("nan"), device="cuda")
+            nat.check(lib.pinsage_linear_ilv(_vp(at), lda, _vp(a_idx), 0 if dev_m else M,
+                                             _vp(m_dev) if dev_m else None, M + 300, K, _vp(W),
+                                             _vp(wt) if w_tab else None, 3 * K, _vp(bias), N, 1, _vp(C1), N, stream),
+                      "linear_ilv")
+            torch.cuda.synchronize()
+            assert torch.isfinite(C1).all(), (M, N, K, dev_m, w_tab)
+            assert torch.equal(C0, C1), (M, N, K, dev_m, w_tab, (C0 - C1).abs().max().item())
+        assert _rel(C1, _ref(M, N, K, 1, 1, A[:, :K], a_idx, W, bias, 1)) < 2e-6
+        # K % 16, a row stride below 3K, negative sizes
+        assert lib.pinsage_split_ilv(_vp(A), K + 4, 8, K - 8, _vp(at), lda, stream) != 0
+        assert lib.pinsage_split_ilv(_vp(A), K + 4, 8, K, _vp(at), 3 * K - 8, stream) != 0
+        assert lib.pinsage_linear_ilv(_vp(at), lda, None, M, None, M, K - 8, _vp(W), _vp(wt), 3 * K, None, N, 0,
+                                      _vp(C1), N, stream) != 0
+        assert lib.pinsage_linear_ilv(_vp(at), lda, None, -1, None, M, K, _vp(W), _vp(wt), 3 * K, None, N, 0,
+                                      _vp(C1), N, stream) != 0
+    finally:
+        lib.pinsage_gemm_set_prec(old)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 128, 32), (63, 128, 128), (1000, 256, 512), (10541, 512, 512),
                                    (3000, 512, 128), (700, 128, 1024)])
 def test_warp_specialised_gemm_is_bitwise_cfg3(M, N, K):

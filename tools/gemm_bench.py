@@ -56,7 +56,18 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_
     args = (M, N, K, ak, bk, vp(A), A.shape[1], vp(a_idx), vp(B), B.shape[1], vp(b_idx), vp(C), N,
             vp(bias), int(bias_act), 3 if splits > 1 else 0, splits, cfg, sk, ctypes.c_void_p(stream.cuda_stream))
     call = lib.pinsage_gemm_ex
-    if presplit:  # B (K-major, [N][K]) read as pre-split bf16 planes: pinsage_linear_split_b
+    if presplit == "ilv":  # the A table and W as interleaved plane tables (pinsage_split_ilv), A's split once
+        assert ak and bk and splits == 1 and sk == 0
+        cs0 = ctypes.c_void_p(stream.cuda_stream)
+        at = torch.empty(A.shape[0], 3 * K, dtype=torch.int16, device=dev)
+        wt = torch.empty(N, 3 * K, dtype=torch.int16, device=dev)
+        nat.check(lib.pinsage_split_ilv(vp(A), A.shape[1], A.shape[0], K, vp(at), 3 * K, cs0), "split A")
+        nat.check(lib.pinsage_split_ilv(vp(B), B.shape[1], N, K, vp(wt), 3 * K, cs0), "split W")
+        args = (vp(at), 3 * K, vp(a_idx), M, None, M, K, vp(B), vp(wt), 3 * K, vp(bias), N, int(bias_act), vp(C), N,
+                cs0)
+        call = lib.pinsage_linear_ilv
+        ai = 2
+    elif presplit:  # B (K-major, [N][K]) read as pre-split bf16 planes: pinsage_linear_split_b
         assert ak and bk and splits == 1 and sk == 0, "pre-split B: K-major operands, no split-K/stream-K"
         planes = torch.empty(3, N, K, dtype=torch.int16, device=dev)
         nat.check(lib.pinsage_split_planes(vp(B), N, K, K, vp(planes), ctypes.c_void_p(stream.cuda_stream)),
@@ -75,7 +86,8 @@ def run(shape, cfg, sk, reps, lib, stream, pool=0, sets=1, bias_act=False, sort_
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(3):
         call(*args)
-    ai = 2 if presplit else 7  # position of a_idx
+    if presplit != "ilv":
+        ai = 2 if presplit else 7  # position of a_idx
     all_args = [tuple(vp(ix) if i == ai else a for i, a in enumerate(args)) for ix in idx_sets] \
         if idx_sets[0] is not None else [args]
     if graph:  # the reps captured once and replayed: device time without the host's launch rate
@@ -117,7 +129,8 @@ def main():
     ap.add_argument("--sorted", action="store_true", help="gathered rows in ascending order")
     ap.add_argument("--graph", action="store_true", help="time a hipGraph of the reps (no host launch rate)")
     ap.add_argument("--prec", default="1",
-                    help="product arithmetic(s): 0 fp32 MFMA, 1 split bf16, 2 split bf16 with pre-split B planes")
+                    help="product arithmetic(s): 0 fp32 MFMA, 1 split bf16, 2 split bf16 with pre-split B planes, "
+                         "3 interleaved plane tables of A (split once) and W (pinsage_linear_ilv)")
     a = ap.parse_args()
     lib = nat.lib()
     stream = torch.cuda.current_stream()
@@ -129,7 +142,7 @@ def main():
                 if sk == 1 and cfg == 0:
                     continue
                 us, tf, err = run(s, cfg, sk, a.reps, lib, stream, a.pool, a.sets, a.bias_act, a.sorted,
-                                  presplit=prec == 2, graph=a.graph)
+                                  presplit="ilv" if prec == 3 else prec == 2, graph=a.graph)
                 print(f"{s:24s} prec={prec} cfg={cfg:2d} sk={sk:2d} {us:9.2f} us {tf:7.1f} TF/s  relerr={err:.2e}",
                       flush=True)
 
