@@ -96,6 +96,8 @@ _SIGS = {
     "pinsage_split_planes": (ctypes.c_int, [vp, i64, i64, i64, vp, vp]),
     "pinsage_linear_split_b": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, vp, i64, ctypes.c_int,
                                               vp, i64, ctypes.c_int, vp]),
+    "pinsage_triplet_loss_scratch_bytes": (i64, [i64, i64]),
+    "pinsage_triplet_loss": (ctypes.c_int, [vp, i64, i64, ctypes.c_float, vp, vp, vp, vp]),
     "pinsage_split_ilv": (ctypes.c_int, [vp, i64, i64, i64, vp, i64, vp]),
     "pinsage_linear_ilv": (ctypes.c_int, [vp, i64, vp, i64, vp, i64, i64, vp, vp, i64, vp, i64, ctypes.c_int, vp,
                                           i64, vp]),

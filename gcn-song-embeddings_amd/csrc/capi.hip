@@ -41,6 +41,9 @@ int64_t bitset_blocks(int64_t universe);
 int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
 int launch_mark_table_i64(unsigned long long*, const int64_t*, int64_t, const int32_t*, int64_t,
                           int, int64_t, int*, hipStream_t);
+int64_t triplet_loss_scratch_bytes(int64_t B, int64_t d);
+int launch_triplet_loss(const float* Z, int B, int d, float margin, float* G, void* scratch, float* scal,
+                        hipStream_t st);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
@@ -572,6 +575,19 @@ int pinsage_gemm_get_prec(void) { return gemm_default_prec(); }
 int pinsage_split_planes(const float* W, int64_t rows, int64_t cols, int64_t ldw, uint16_t* out,
                          void* stream) {
   return launch_split_planes(W, rows, cols, ldw, out, (hipStream_t)stream);
+}
+
+int64_t pinsage_triplet_loss_scratch_bytes(int64_t B, int64_t d) {
+  return B <= 0 || d <= 0 ? -1 : triplet_loss_scratch_bytes(B, d);
+}
+
+int pinsage_triplet_loss(const float* Z, int64_t B, int64_t d, float margin, float* G, void* scratch, float* scal,
+                         void* stream) {
+  if (!Z || !G || !scratch || !scal || B <= 0 || B > (INT32_MAX / 9) || d <= 0 || d > 256) {
+    set_error("triplet_loss: bad argument");
+    return kErrArg;
+  }
+  return launch_triplet_loss(Z, (int)B, (int)d, margin, G, scratch, scal, (hipStream_t)stream);
 }
 
 int pinsage_split_ilv(const float* src, int64_t ld, int64_t rows, int64_t K, uint16_t* out, int64_t ldo,

@@ -11,6 +11,7 @@
 //                   (pinsage_training.py:200-212)
 //   adam            torch.optim.Adam step (pinsage_training.py:147,191)
 #include "common.h"
+#include "conv.h"
 
 #include <algorithm>
 #include <climits>
@@ -23,56 +24,44 @@ __device__ __forceinline__ int32_t rank_in(const unsigned long long* bits, const
   return (int32_t)(prefix[v >> 6] + __popcll(w & ((1ull << (v & 63)) - 1ull)));
 }
 
-// ---------------------------------------------------------------- layer prep
-// For f < *nS (rows of the layer's node set S_l, sorted ids):
-//   self_src[f]   = row of h_l holding node f (rank in S_{l-1}, or the id at l=0)
-//   loc[f*T+t]    = rank of nb[id][t] in N_l (row of the Q output)
-//   wloc[f*T+t]   = normalised importance weight
-// For u < *nN (rows of N_l):  q_src[u] = row of h_l holding that node.
-__global__ void layer_prep_kernel(const int32_t* __restrict__ S_mem, const int* __restrict__ nS,
-                                  const int32_t* __restrict__ N_mem, const int* __restrict__ nN,
-                                  const unsigned long long* __restrict__ N_bits,
-                                  const uint32_t* __restrict__ N_pref,
-                                  const unsigned long long* __restrict__ P_bits,
-                                  const uint32_t* __restrict__ P_pref,
-                                  const int32_t* __restrict__ nb, const float* __restrict__ wn,
-                                  int64_t ldT, int T, int32_t* __restrict__ self_src,
-                                  int32_t* __restrict__ q_src, int32_t* __restrict__ loc,
-                                  float* __restrict__ wloc,
-                                  const unsigned long long* __restrict__ S_bits,
-                                  const uint32_t* __restrict__ S_pref,
-                                  const int64_t* __restrict__ ids, int64_t n_ids,
-                                  int32_t* __restrict__ pos_rank, float* __restrict__ z, int z_n,
-                                  const int* __restrict__ z_rows) {
-  if (z) {  // zero the layer below's dY rows: the backward scatter-adds into them
-    const int64_t zn4 = (int64_t)(*z_rows) * z_n / 4;
-    float4* z4 = reinterpret_cast<float4*>(z);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zn4;
-         i += (int64_t)gridDim.x * blockDim.x)
-      z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+// ---------------------------------------------------------------- layer prep (conv.h)
+// every layer's tables in one launch (each layer's items follow the previous
+// layer's: the grid strides over their concatenation)
+__global__ void layer_prep_kernel(LayerPreps a) {
+  const int T = a.T;
+  const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+  for (int l = 0; l < a.n; ++l) {
+    const LayerPrep& p = a.L[l];
+    if (p.z) {  // zero the layer below's dY rows: the backward scatter-adds into them
+      const int64_t zn4 = (int64_t)(*p.z_rows) * p.z_n / 4;
+      float4* z4 = reinterpret_cast<float4*>(p.z);
+      for (int64_t i = g0; i < zn4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
-  const int64_t FS = (int64_t)(*nS), FN = (int64_t)(*nN);
-  const int64_t total = FS * T + FS + FN + n_ids;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    if (e < FS * T) {
-      const int64_t f = e / T, t = e - f * T;
-      const int64_t id = S_mem[f];
-      const int64_t u = nb[id * ldT + t];
-      loc[e] = rank_in(N_bits, N_pref, u);
-      wloc[e] = wn[id * ldT + t];
-    } else if (e < FS * T + FS) {
-      const int64_t f = e - FS * T;
-      const int64_t id = S_mem[f];
-      self_src[f] = P_bits ? rank_in(P_bits, P_pref, id) : (int32_t)id;
-    } else if (e < FS * T + FS + FN) {
-      const int64_t u = e - FS * T - FS;
-      const int64_t id = N_mem[u];
-      q_src[u] = P_bits ? rank_in(P_bits, P_pref, id) : (int32_t)id;
-    } else {
-      // batch position -> row of the top-layer set (duplicates share a row)
-      const int64_t i = e - FS * T - FS - FN;
-      pos_rank[i] = rank_in(S_bits, S_pref, ids[i]);
+  for (int l = 0; l < a.n; ++l) {
+    const LayerPrep& p = a.L[l];
+    const int64_t FS = (int64_t)(*p.nS), FN = (int64_t)(*p.nN);
+    const int64_t total = FS * T + FS + FN + p.n_ids;
+    for (int64_t e = g0; e < total; e += gs) {
+      if (e < FS * T) {
+        const int64_t f = e / T, t = e - f * T;
+        const int64_t id = p.S_mem[f];
+        const int64_t u = p.nb[id * p.ldT + t];
+        p.loc[e] = rank_in(p.N_bits, p.N_pref, u);
+        p.wloc[e] = p.wn[id * p.ldT + t];
+      } else if (e < FS * T + FS) {
+        const int64_t f = e - FS * T;
+        const int64_t id = p.S_mem[f];
+        p.self_src[f] = p.P_bits ? rank_in(p.P_bits, p.P_pref, id) : (int32_t)id;
+      } else if (e < FS * T + FS + FN) {
+        const int64_t u = e - FS * T - FS;
+        const int64_t id = p.N_mem[u];
+        p.q_src[u] = p.P_bits ? rank_in(p.P_bits, p.P_pref, id) : (int32_t)id;
+      } else {
+        // batch position -> row of the top-layer set (duplicates share a row)
+        const int64_t i = e - FS * T - FS - FN;
+        p.pos_rank[i] = rank_in(p.S_bits, p.S_pref, p.ids[i]);
+      }
     }
   }
 }
@@ -1762,19 +1751,19 @@ int launch_reduce_slabs_2d(const float* part, int S, int64_t stride, int M, int 
   PS_CHECK_LAUNCH();
   return kOk;
 }
-int launch_layer_prep(const int32_t* S_mem, const int* nS, int64_t S_max, const int32_t* N_mem,
-                      const int* nN, int64_t N_max, const unsigned long long* N_bits,
-                      const uint32_t* N_pref, const unsigned long long* P_bits,
-                      const uint32_t* P_pref, const int32_t* nb, const float* wn, int64_t ldT,
-                      int T, int32_t* self_src, int32_t* q_src, int32_t* loc, float* wloc,
-                      const unsigned long long* S_bits, const uint32_t* S_pref, const int64_t* ids,
-                      int64_t n_ids, int32_t* pos_rank, float* z, int z_n, const int* z_rows,
-                      hipStream_t st) {
-  PS_REQUIRE(!z || z_n % 4 == 0, kErrArg, "layer_prep: zeroed rows must be a multiple of 4 wide");
-  const int64_t tot = S_max * T + S_max + N_max + n_ids;
-  hipLaunchKernelGGL(layer_prep_kernel, dim3(grid_for(tot, 256)), dim3(256), 0, st, S_mem, nS, N_mem,
-                     nN, N_bits, N_pref, P_bits, P_pref, nb, wn, ldT, T, self_src, q_src, loc, wloc,
-                     S_bits, S_pref, ids, n_ids, pos_rank, z, z_n, z_rows);
+// one layer's tables: p.* as in LayerPrep, S_max / N_max the set capacities
+int launch_layer_preps(const LayerPrep* p, const int64_t* S_max, const int64_t* N_max, int n, int T, hipStream_t st) {
+  PS_REQUIRE(n >= 1 && n <= kMaxPrepLayers, kErrArg, "layer_prep: 1..4 layers per launch");
+  LayerPreps a;
+  a.n = n;
+  a.T = T;
+  int64_t tot = 0;
+  for (int l = 0; l < n; ++l) {
+    PS_REQUIRE(!p[l].z || p[l].z_n % 4 == 0, kErrArg, "layer_prep: zeroed rows must be a multiple of 4 wide");
+    a.L[l] = p[l];
+    tot = std::max(tot, S_max[l] * T + S_max[l] + N_max[l] + p[l].n_ids);
+  }
+  hipLaunchKernelGGL(layer_prep_kernel, dim3(grid_for(tot, 256)), dim3(256), 0, st, a);
   PS_CHECK_LAUNCH();
   return kOk;
 }
@@ -2014,6 +2003,56 @@ int launch_fly_fix(float* G, int* Kc, int64_t S_max, int d, const unsigned long 
     PS_CHECK_LAUNCH();
   }
   return kOk;
+}
+
+// The step's loss arithmetic on outputs given per position (the micro-batched
+// step, pinsage_training._train_batch_micro): Z [3][B][d] (call-major), every
+// position its own row (no repeated ranks, so the float atomics of det_put
+// each add into a zero: exact).  G [3][3B][d]: position (c, b)'s cotangent at
+// G[c][c*B + b].  scal: {loss, 0, sum |h_q|^2, variance} -- the same kernels
+// and reduction order as pinsage_engine_loss, so the same bits for the same
+// rows.  scratch: triplet_loss_scratch_bytes(B, d).
+__global__ void triplet_identity_kernel(int32_t* __restrict__ pos_rank, int B, int* __restrict__ rank_off) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * B; i += gridDim.x * blockDim.x)
+    pos_rank[i] = (i % 3) * B + i / 3;  // position 3b + c -> row c*B + b
+  if (blockIdx.x == 0 && threadIdx.x == 0) rank_off[0] = -1;  // no position CSR: det_put's atomics
+}
+
+int64_t triplet_loss_scratch_bytes(int64_t B, int64_t d) {
+  const int64_t nblk = (B + 3) / 4;
+  return align_up(3 * B * 4, 256) + align_up(9 * B * 4, 256) + align_up((nblk + 1) * 16, 256) +
+         align_up((nblk + 1) * 2 * d * 4, 256) + 256;
+}
+
+int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float margin, const float* feats, int64_t ld_f,
+                int d_in, const int64_t* batch, float* G, int* Kc, int64_t S_max, const int* nS, float* dZ, float* part,
+                float* colpart, float* scal, float* hinge, bool combine_dz, bool rep_sum, const int* rank_off,
+                const int32_t* pos_sorted, float* Gp, hipStream_t st);
+int launch_loss_monitor(const float* part, int nparts, const float* colpart, int d, int B, float* scal,
+                        hipStream_t st);
+
+int launch_triplet_loss(const float* Z, int B, int d, float margin, float* G, void* scratch, float* scal,
+                        hipStream_t st) {
+  PS_REQUIRE(B > 0 && d > 0 && d <= 256 && 1024 % d == 0, kErrArg, "triplet_loss: B > 0, d <= 256 dividing 1024");
+  const int64_t nblk = (B + 3) / 4;
+  char* p = static_cast<char*>(scratch);
+  int32_t* pos_rank = reinterpret_cast<int32_t*>(p);
+  p += align_up(3LL * B * 4, 256);
+  int* Kc = reinterpret_cast<int*>(p);
+  p += align_up(9LL * B * 4, 256);
+  float* part = reinterpret_cast<float*>(p);
+  p += align_up((nblk + 1) * 16, 256);
+  float* colpart = reinterpret_cast<float*>(p);
+  p += align_up((nblk + 1) * 2 * d * 4, 256);
+  int* rank_off = reinterpret_cast<int*>(p);
+  PS_CHECK_HIP(hipMemsetAsync(G, 0, (size_t)9 * B * d * 4, st));
+  PS_CHECK_HIP(hipMemsetAsync(Kc, 0, (size_t)9 * B * 4, st));
+  hipLaunchKernelGGL(triplet_identity_kernel, dim3((unsigned)std::min<int64_t>((3LL * B + 255) / 256, 1024)),
+                     dim3(256), 0, st, pos_rank, B, rank_off);
+  PS_CHECK_LAUNCH();
+  PS_TRY(launch_loss(Z, d, pos_rank, B, margin, nullptr, 0, 0, nullptr, G, Kc, 3LL * B, nullptr, nullptr, part,
+                     colpart, scal, nullptr, false, false, rank_off, nullptr, nullptr, st));
+  return launch_loss_monitor(part, (int)nblk, colpart, d, B, scal, st);
 }
 
 int launch_loss_monitor(const float* part, int nparts, const float* colpart, int d, int B, float* scal,

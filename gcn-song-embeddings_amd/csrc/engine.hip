@@ -25,6 +25,7 @@
 
 #include "aggw.h"
 #include "common.h"
+#include "conv.h"
 #include "gemm.h"
 
 namespace ps {
@@ -35,6 +36,10 @@ int64_t bitset_blocks(int64_t universe);
 int launch_mark_i64(unsigned long long*, const int64_t*, int64_t, int64_t, int*, hipStream_t);
 int launch_mark_table(unsigned long long*, const int32_t*, const int*, int64_t, const int32_t*,
                       int64_t, int, int64_t, hipStream_t);
+bool mark_finalize_fits(int64_t universe);
+int launch_mark_finalize(unsigned long long*, const int32_t*, const int*, int64_t, const int32_t*, int64_t, int,
+                         int64_t, int*, uint32_t*, int32_t*, int*, unsigned long long*, const unsigned long long*,
+                         uint32_t*, int32_t*, int*, hipStream_t);
 int launch_set_finalize(unsigned long long*, const unsigned long long*, const unsigned long long*,
                         int64_t, uint32_t*, uint32_t*, int32_t*, int*, hipStream_t);
 int launch_top_set(unsigned long long*, int64_t, unsigned long long*, const int64_t*, int64_t,
@@ -42,11 +47,7 @@ int launch_top_set(unsigned long long*, int64_t, unsigned long long*, const int6
                    const int* x_n = nullptr);
 int launch_fly_fix(float*, int*, int64_t, int, const unsigned long long*, const uint32_t*, const int*, const int64_t*,
                    int64_t, int64_t, int64_t, const int*, float*, bool, hipStream_t);
-int launch_layer_prep(const int32_t*, const int*, int64_t, const int32_t*, const int*, int64_t,
-                      const unsigned long long*, const uint32_t*, const unsigned long long*,
-                      const uint32_t*, const int32_t*, const float*, int64_t, int, int32_t*,
-                      int32_t*, int32_t*, float*, const unsigned long long*, const uint32_t*,
-                      const int64_t*, int64_t, int32_t*, float*, int, const int*, hipStream_t);
+
 int launch_agg(const float*, int, const int32_t*, const float*, int, const int*, int64_t, float*,
                hipStream_t);
 int launch_csr_build(const int32_t*, const float*, const int*, int64_t, int, const int*, int64_t, int*, int*,
@@ -188,6 +189,7 @@ struct Engine {
   int64_t pG1w = 0, pG1b = 0, pG2w = 0, n_params = 0;
   // workspace layout
   size_t bits_begin = 0, bits_end = 0;  // all bitmaps contiguous (one memset)
+  size_t tickets = 0;                    // (inside the bitmap region)
   size_t block_sums = 0, ids = 0, pos_rank = 0, H1 = 0, Z = 0, dZ = 0, dP1 = 0;
   size_t G = 0, Kc = 0, part = 0, scal = 0, slab = 0, bslab = 0, varpart = 0, hinge = 0;
   // the batch positions by top-set rank (pos_csr) and the deterministic
@@ -422,6 +424,9 @@ static void layout(Engine& E) {
     lb.S.bits = carve(cur, nw * 8);
     lb.N.bits = carve(cur, nw * 8);
   }
+  // the fused mark + finalise launches' tickets (zeroed with the bitmaps by
+  // every step's first kernel, reset by their last blocks)
+  E.tickets = carve(cur, std::max<int64_t>(Lc, 1) * 4);
   E.bits_end = carve(cur, 0);
   const int64_t scan_blocks = std::max<int64_t>(E.max_bsum_blocks, 1);
   E.block_sums = carve(cur, scan_blocks * 4);
@@ -552,6 +557,14 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
     LayerBuf& lb = E.L[(size_t)l];
     const int32_t* nb_l = lb.nb_tab ? lb.nb_tab : E.nb;
     const int64_t ld_l = lb.nb_tab ? lb.ld_tab : E.ldT;
+    if (mark_finalize_fits(n) && lb.S.cap > 0) {  // one launch: mark N_l, finalise N_l and S_{l-1}
+      LayerBuf* lo = l > 0 ? &E.L[(size_t)l - 1] : nullptr;
+      PS_TRY(launch_mark_finalize(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, nb_l, ld_l, T, n,
+                                  at<int>(ws, E.tickets) + l, pref(lb.N), mem(lb.N), cnt(lb.N),
+                                  lo ? bits(lo->S) : nullptr, bits(lb.S), lo ? pref(lo->S) : nullptr,
+                                  lo ? mem(lo->S) : nullptr, lo ? cnt(lo->S) : nullptr, st));
+      continue;
+    }
     PS_TRY(launch_mark_table(bits(lb.N), mem(lb.S), cnt(lb.S), lb.S.cap, nb_l, ld_l, T, n, st));
     PS_TRY(launch_set_finalize(bits(lb.N), bits(lb.N), nullptr, n, bsum, pref(lb.N), mem(lb.N),
                                cnt(lb.N), st));
@@ -561,22 +574,45 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
                                  cnt(lo.S), st));
     }
   }
-  // index tables of every layer, bottom-up
-  for (int l = 0; l < Lc; ++l) {
-    LayerBuf& lb = E.L[(size_t)l];
-    const SetBuf* prev = l > 0 ? &E.L[(size_t)l - 1].S : nullptr;
-    const bool is_top = l == Lc - 1;  // the top layer also ranks the batch positions
-    PS_TRY(launch_layer_prep(mem(lb.S), cnt(lb.S), lb.S.cap, mem(lb.N), cnt(lb.N), lb.N.cap,
-                             bits(lb.N), pref(lb.N), prev ? bits(*prev) : nullptr,
-                             prev ? pref(*prev) : nullptr, lb.nb_tab ? lb.nb_tab : E.nb,
-                             lb.nb_tab ? lb.wn_tab : E.wn, lb.nb_tab ? lb.ld_tab : E.ldT, T,
-                             at<int32_t>(ws, lb.self_src), at<int32_t>(ws, lb.q_src),
-                             at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), bits(top.S),
-                             pref(top.S), ids, is_top ? n_pos : 0, at<int32_t>(ws, E.pos_rank),
-                             prev ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr, (int)c.out,
-                             prev ? cnt(*prev) : nullptr, st));
-    if (is_top) PS_TRY(launch_pos_csr(at<int32_t>(ws, E.pos_rank), n_pos, cnt(top.S), at<int>(ws, E.rank_off),
-                                      at<int32_t>(ws, E.pos_sorted), st));
+  // index tables of every layer, one launch
+  {
+    LayerPrep pp[kMaxPrepLayers];
+    int64_t smax[kMaxPrepLayers], nmax[kMaxPrepLayers];
+    PS_REQUIRE(Lc <= kMaxPrepLayers, kErrArg, "engine: at most 4 layers");
+    for (int l = 0; l < Lc; ++l) {
+      LayerBuf& lb = E.L[(size_t)l];
+      const SetBuf* prev = l > 0 ? &E.L[(size_t)l - 1].S : nullptr;
+      const bool is_top = l == Lc - 1;  // the top layer also ranks the batch positions
+      LayerPrep& p = pp[l];
+      p.S_mem = mem(lb.S);
+      p.nS = cnt(lb.S);
+      p.N_mem = mem(lb.N);
+      p.nN = cnt(lb.N);
+      p.N_bits = bits(lb.N);
+      p.N_pref = pref(lb.N);
+      p.P_bits = prev ? bits(*prev) : nullptr;
+      p.P_pref = prev ? pref(*prev) : nullptr;
+      p.nb = lb.nb_tab ? lb.nb_tab : E.nb;
+      p.wn = lb.nb_tab ? lb.wn_tab : E.wn;
+      p.ldT = lb.nb_tab ? lb.ld_tab : E.ldT;
+      p.self_src = at<int32_t>(ws, lb.self_src);
+      p.q_src = at<int32_t>(ws, lb.q_src);
+      p.loc = at<int32_t>(ws, lb.loc);
+      p.wloc = at<float>(ws, lb.wloc);
+      p.S_bits = bits(top.S);
+      p.S_pref = pref(top.S);
+      p.ids = ids;
+      p.n_ids = is_top ? n_pos : 0;
+      p.pos_rank = at<int32_t>(ws, E.pos_rank);
+      p.z = prev ? at<float>(ws, E.L[(size_t)l - 1].dY) : nullptr;
+      p.z_n = (int)c.out;
+      p.z_rows = prev ? cnt(*prev) : nullptr;
+      smax[l] = lb.S.cap;
+      nmax[l] = lb.N.cap;
+    }
+    PS_TRY(launch_layer_preps(pp, smax, nmax, Lc, T, st));
+    PS_TRY(launch_pos_csr(at<int32_t>(ws, E.pos_rank), n_pos, cnt(top.S), at<int>(ws, E.rank_off),
+                          at<int32_t>(ws, E.pos_sorted), st));
   }
   // the transposes of the neighbour slots (CSR of slot occurrences by q row,
   // the aggregation backward's plan) depend only on the frontier: built here,

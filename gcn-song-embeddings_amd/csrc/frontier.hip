@@ -45,6 +45,82 @@ __global__ void bits_mark_i64_kernel(unsigned long long* __restrict__ bits,
   }
 }
 
+// Single-block finalisation for bitmaps of <= kSmallWords words (<= 1M ids):
+// OR, popcount, block scan, prefixes, compaction and count in one launch.
+constexpr int kSmallWords = 16384;
+// kCoherent: read the bitmap with device-coherent loads (it was written by
+// atomics of this same kernel, which bypass the CU's L1)
+template <bool kCoherent>
+__device__ __forceinline__ void finalize_block(unsigned long long* __restrict__ dst,
+                                               const unsigned long long* a,
+                                               const unsigned long long* __restrict__ b,
+                                               int64_t nwords, uint32_t* __restrict__ prefix,
+                                               int32_t* __restrict__ members,
+                                               int* __restrict__ count_out) {
+  __shared__ uint32_t wsum[16];
+  const int per = (int)((nwords + 1023) / 1024);
+  const int64_t w0 = (int64_t)threadIdx.x * per;
+  unsigned long long xs[16];
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    xs[q] = 0ull;
+    const int64_t w = w0 + q;
+    if (q < per && w < nwords) {
+      unsigned long long x =
+          kCoherent ? __hip_atomic_load(a + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a[w];
+      if (b) x |= b[w];
+      if (dst != a || b) dst[w] = x;
+      xs[q] = x;
+      c += __popcll(x);
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t p = inc - c;
+  for (int i = 0; i < wv; ++i) p += wsum[i];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t w = w0 + q;
+    if (q < per && w < nwords) {
+      prefix[w] = p;
+      unsigned long long m = xs[q];
+      uint32_t j = p;
+      while (m) {
+        const int bit = __ffsll((long long)m) - 1;
+        members[j++] = (int32_t)(w * 64 + bit);
+        m &= m - 1;
+      }
+      p += __popcll(xs[q]);
+    }
+  }
+  if (threadIdx.x == 1023) *count_out = (int)p;
+}
+
+// The finalisations a mark launch runs itself (its last block to finish, so
+// no separate single-block launch follows it): the marked set N (prefix,
+// members, count) and optionally S_lo = N | S_l.  ticket: a zeroed int (the
+// frontier's bitmap region, which the step's first kernel zeroes; the last
+// block also resets it).
+struct MarkFinalize {
+  int* ticket = nullptr;
+  uint32_t* prefN = nullptr;
+  int32_t* memN = nullptr;
+  int* cntN = nullptr;
+  unsigned long long* dstS = nullptr;  // null: N only
+  const unsigned long long* bS = nullptr;
+  uint32_t* prefS = nullptr;
+  int32_t* memS = nullptr;
+  int* cntS = nullptr;
+};
+
 // mark nb_table[members[f]][t] for f < *count, t < T (table row stride ld).
 // lds_words > 0: each block marks its contiguous slice into an LDS copy of the
 // bitmap and ORs the touched words into HBM once (popular ids repeat thousands
@@ -53,12 +129,12 @@ __global__ void bits_mark_i64_kernel(unsigned long long* __restrict__ bits,
 // the work into (window, slice) items, about two per workgroup; a block marks
 // the ids of its slice that fall in its window into LDS (the slice's table rows
 // are re-read once per window, from L2 / the Infinity Cache after the first).
-__global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long long* __restrict__ bits,
+__global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long long* bits,
                                                                const int32_t* __restrict__ members,
                                                                const int* __restrict__ count,
                                                                const int32_t* __restrict__ nb,
                                                                int64_t ld, int T, int lds_words,
-                                                               int64_t nwords, int range_words) {
+                                                               int64_t nwords, int range_words, MarkFinalize fz) {
   extern __shared__ unsigned long long lbits[];
   const int64_t n = (int64_t)(*count) * T;
   if (range_words > 0) {
@@ -82,9 +158,7 @@ __global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long lon
         if (lbits[w]) atomicOr(bits + w0 + w, lbits[w]);
       __syncthreads();  // the next item zeroes lbits
     }
-    return;
-  }
-  if (lds_words > 0) {
+  } else if (lds_words > 0) {
     for (int w = threadIdx.x; w < lds_words; w += blockDim.x) lbits[w] = 0ull;
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -97,12 +171,33 @@ __global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long lon
     __syncthreads();
     for (int w = threadIdx.x; w < lds_words; w += blockDim.x)
       if (lbits[w]) atomicOr(bits + w, lbits[w]);
-    return;
+  } else {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t f = e / T, t = e - f * T;
+      mark(bits, nb[(int64_t)members[f] * ld + t]);
+    }
   }
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t f = e / T, t = e - f * T;
-    mark(bits, nb[(int64_t)members[f] * ld + t]);
+  if (!fz.ticket) return;
+  // The last block to finish finalises.  The bitmap is only ever changed by
+  // atomics, which are performed at the device's L2, and read back by the
+  // last block with device-coherent loads (finalize_block<true>): a block's
+  // ordering point is its atomics' completion (vmcnt), not a cache fence --
+  // a __threadfence in every thread (L2 writeback + invalidate) made this
+  // launch slower than the two it replaces.
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    last = __hip_atomic_fetch_add(fz.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    if (last) __hip_atomic_store(fz.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  finalize_block<true>(bits, bits, nullptr, nwords, fz.prefN, fz.memN, fz.cntN);
+  if (fz.dstS) {
+    __syncthreads();  // (finalize_block's scan scratch is reused)
+    finalize_block<true>(fz.dstS, bits, fz.bS, nwords, fz.prefS, fz.memS, fz.cntS);
   }
 }
 
@@ -210,65 +305,6 @@ __global__ __launch_bounds__(kScanBlock) void bits_scan_compact_kernel(
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) *count_out = (int)p;
 }
 
-// Single-block finalisation for bitmaps of <= kSmallWords words (<= 1M ids):
-// OR, popcount, block scan, prefixes, compaction and count in one launch.
-constexpr int kSmallWords = 16384;
-// kCoherent: read the bitmap with device-coherent loads (it was written by
-// atomics of this same kernel, which bypass the CU's L1)
-template <bool kCoherent>
-__device__ __forceinline__ void finalize_block(unsigned long long* __restrict__ dst,
-                                               const unsigned long long* a,
-                                               const unsigned long long* __restrict__ b,
-                                               int64_t nwords, uint32_t* __restrict__ prefix,
-                                               int32_t* __restrict__ members,
-                                               int* __restrict__ count_out) {
-  __shared__ uint32_t wsum[16];
-  const int per = (int)((nwords + 1023) / 1024);
-  const int64_t w0 = (int64_t)threadIdx.x * per;
-  unsigned long long xs[16];
-  uint32_t c = 0;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    xs[q] = 0ull;
-    const int64_t w = w0 + q;
-    if (q < per && w < nwords) {
-      unsigned long long x =
-          kCoherent ? __hip_atomic_load(a + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a[w];
-      if (b) x |= b[w];
-      if (dst != a || b) dst[w] = x;
-      xs[q] = x;
-      c += __popcll(x);
-    }
-  }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t inc = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) wsum[wv] = inc;
-  __syncthreads();
-  uint32_t p = inc - c;
-  for (int i = 0; i < wv; ++i) p += wsum[i];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t w = w0 + q;
-    if (q < per && w < nwords) {
-      prefix[w] = p;
-      unsigned long long m = xs[q];
-      uint32_t j = p;
-      while (m) {
-        const int bit = __ffsll((long long)m) - 1;
-        members[j++] = (int32_t)(w * 64 + bit);
-        m &= m - 1;
-      }
-      p += __popcll(xs[q]);
-    }
-  }
-  if (threadIdx.x == 1023) *count_out = (int)p;
-}
-
 __global__ __launch_bounds__(1024) void bits_finalize_small_kernel(
     unsigned long long* __restrict__ dst, const unsigned long long* a,
     const unsigned long long* __restrict__ b, int64_t nwords, uint32_t* __restrict__ prefix,
@@ -287,8 +323,11 @@ __global__ __launch_bounds__(1024) void bits_top_set_kernel(
     const int64_t* __restrict__ ids, int64_t n, int64_t limit, int64_t nwords,
     uint32_t* __restrict__ prefix, int32_t* __restrict__ members, int* __restrict__ count_out, int64_t x0,
     const int* __restrict__ x_n) {
+  // (one block: its own stores and atomics are ordered by their completion
+  // (vmcnt) and the barrier; the atomics are performed at L2 and read back
+  // with device-coherent loads -- no cache fence needed)
   for (int64_t w = threadIdx.x; w < zero_words; w += 1024) zero[w] = 0ull;
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int64_t i = threadIdx.x; i < n; i += 1024) {
     const int64_t v = ids[i];
@@ -299,7 +338,7 @@ __global__ __launch_bounds__(1024) void bits_top_set_kernel(
     for (int64_t v = x0 + threadIdx.x; v < x0 + nx; v += 1024)
       if (v >= 0 && v < limit) atomicOr(bits + (v >> 6), 1ull << (v & 63));
   }
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   finalize_block<true>(bits, bits, nullptr, nwords, prefix, members, count_out);
 }
@@ -334,15 +373,17 @@ int launch_mark_i64(unsigned long long* bits, const int64_t* ids, int64_t n, int
   return kOk;
 }
 
-int launch_mark_table(unsigned long long* bits, const int32_t* members, const int* count,
-                      int64_t max_count, const int32_t* nb, int64_t ld, int T, int64_t universe,
-                      hipStream_t st) {
-  if (max_count <= 0) return kOk;
+static int launch_mark_table_fz(unsigned long long* bits, const int32_t* members, const int* count,
+                                int64_t max_count, const int32_t* nb, int64_t ld, int T, int64_t universe,
+                                hipStream_t st, const MarkFinalize* fz) {
   const int64_t nw = bitset_words(universe);
-  // windows of a full CU's LDS (the limit is raised once, on the first call,
-  // before any graph capture); PINSAGE_MARK_RANGES caps the window count (0:
-  // global atomics beyond 64 KiB, A/B)
-  constexpr int kWinWords = 20480;  // 160 KiB
+  if (fz && (nw > kSmallWords || max_count <= 0)) return kErrArg;  // (callers check mark_finalize_fits)
+  if (max_count <= 0) return kOk;
+  const MarkFinalize f = fz ? *fz : MarkFinalize{};
+  // windows of a full CU's LDS less the finalisation's scan scratch (the limit
+  // is raised once, on the first call, before any graph capture);
+  // PINSAGE_MARK_RANGES caps the window count (0: global atomics beyond 64 KiB, A/B)
+  constexpr int kWinWords = 20448;  // 159.75 KiB
   static const int win_ok = hipFuncSetAttribute((const void*)bits_mark_table_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                                 kWinWords * 8) == hipSuccess;
@@ -350,16 +391,44 @@ int launch_mark_table(unsigned long long* bits, const int32_t* members, const in
   if (nw * 8 <= 64 * 1024) {
     const int gb = std::max(1, std::min(64, ceil_div(max_count * T, 4096)));
     hipLaunchKernelGGL(bits_mark_table_kernel, dim3(gb), dim3(1024), (size_t)nw * 8, st, bits,
-                       members, count, nb, ld, T, (int)nw, nw, 0);
+                       members, count, nb, ld, T, (int)nw, nw, 0, f);
   } else if (win_ok && ceil_div(nw, kWinWords) <= max_win) {
     hipLaunchKernelGGL(bits_mark_table_kernel, dim3(256), dim3(1024), (size_t)kWinWords * 8, st,
-                       bits, members, count, nb, ld, T, 0, nw, kWinWords);
+                       bits, members, count, nb, ld, T, 0, nw, kWinWords, f);
   } else {
     hipLaunchKernelGGL(bits_mark_table_kernel, dim3(grid_for(max_count * T, 1024)), dim3(1024), 0,
-                       st, bits, members, count, nb, ld, T, 0, nw, 0);
+                       st, bits, members, count, nb, ld, T, 0, nw, 0, f);
   }
   PS_CHECK_LAUNCH();
   return kOk;
+}
+
+int launch_mark_table(unsigned long long* bits, const int32_t* members, const int* count,
+                      int64_t max_count, const int32_t* nb, int64_t ld, int T, int64_t universe,
+                      hipStream_t st) {
+  return launch_mark_table_fz(bits, members, count, max_count, nb, ld, T, universe, st, nullptr);
+}
+
+// whether launch_mark_table can finalise its set itself (single-block finalisation)
+bool mark_finalize_fits(int64_t universe) { return bitset_words(universe) <= kSmallWords; }
+
+// mark N from the table rows of S and finalise N (and S_lo = N | S_l when
+// dstS is set) in the same launch
+int launch_mark_finalize(unsigned long long* bitsN, const int32_t* membersS, const int* countS, int64_t max_count,
+                         const int32_t* nb, int64_t ld, int T, int64_t universe, int* ticket, uint32_t* prefN,
+                         int32_t* memN, int* cntN, unsigned long long* dstS, const unsigned long long* bS,
+                         uint32_t* prefS, int32_t* memS, int* cntS, hipStream_t st) {
+  MarkFinalize f;
+  f.ticket = ticket;
+  f.prefN = prefN;
+  f.memN = memN;
+  f.cntN = cntN;
+  f.dstS = dstS;
+  f.bS = bS;
+  f.prefS = prefS;
+  f.memS = memS;
+  f.cntS = cntS;
+  return launch_mark_table_fz(bitsN, membersS, countS, max_count, nb, ld, T, universe, st, &f);
 }
 
 int launch_mark_table_i64(unsigned long long* bits, const int64_t* ids, int64_t n,

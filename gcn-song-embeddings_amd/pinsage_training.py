@@ -41,6 +41,31 @@ def max_margin_loss(h_q, h_pos, h_neg, margin):
     return torch.clamp(dot, min=0.0).mean()
 
 
+def _triplet_loss(Z, margin):
+    """max_margin_loss of outputs Z [3, B, d] and its cotangent [3, B, d] with
+    the train step's own kernels and summation order (pinsage_triplet_loss):
+    the micro-batched step then ends on the fused step's loss bits whenever
+    its output rows are the same.  Outputs the kernel does not take (d > 256
+    or not dividing 1024) go through torch.  Returns (loss, cotangent,
+    variance or None)."""
+    B, d = int(Z.shape[1]), int(Z.shape[2])
+    if d > 256 or 1024 % d or not Z.is_cuda:
+        Zr = Z.detach().requires_grad_()
+        with torch.enable_grad():
+            loss = max_margin_loss(Zr[0], Zr[1], Zr[2], margin)
+            (g,) = torch.autograd.grad(loss, [Zr])
+        return loss, g, None
+    L = nat.lib()
+    Zc = Z.detach().contiguous()
+    G = torch.empty((3, 3, B, d), dtype=torch.float32, device=Z.device)
+    scratch = torch.empty(int(L.pinsage_triplet_loss_scratch_bytes(B, d)), dtype=torch.uint8, device=Z.device)
+    scal = torch.empty(4, dtype=torch.float32, device=Z.device)
+    nat.check(L.pinsage_triplet_loss(nat.ptr(Zc), B, d, float(margin), nat.ptr(G), nat.ptr(scratch),
+                                     nat.ptr(scal), nat.stream_ptr()), "triplet_loss")
+    g = torch.stack([G[0, 0], G[1, 1], G[2, 2]])
+    return scal[0], g, scal[3]
+
+
 def cosine_dissimilarity(a, b):
     return 1 - F.cosine_similarity(a, b)
 
@@ -1330,10 +1355,7 @@ class PinSage:
         ids = batch.t().contiguous().to(dev)  # [3, B]: the q, pos and neg calls
         Z = self._micro_forward(ids)
         self.last_outputs = Z  # [3, B, out] rows the loss read (tests pin them)
-        Zr = Z.detach().requires_grad_()
-        with torch.enable_grad():
-            loss = max_margin_loss(Zr[0], Zr[1], Zr[2], self.margin)
-            (g,) = torch.autograd.grad(loss, [Zr])
+        loss, g, variance = _triplet_loss(Z, self.margin)
         self._micro_backward(ids, g)
         self._average_param_grads()
         self.optimizer.step()
@@ -1342,7 +1364,8 @@ class PinSage:
         bq = batch.to(f.device)
         node_feat_loss = COSINE_TRIPLET_LOSS(norm(f[bq[:, 0]], dim=1), norm(f[bq[:, 1]], dim=1),
                                              norm(f[bq[:, 2]], dim=1))
-        variance = batch_variance(Z[0])
+        if variance is None:
+            variance = batch_variance(Z[0])
         return loss.detach(), node_feat_loss, variance
 
     def _micro_forward(self, ids):

@@ -246,6 +246,16 @@ int pinsage_linear_split_b(const float* A, int64_t lda, const int32_t* a_idx, in
                            const float* W, const uint16_t* W_planes, int64_t ldws,
                            const float* bias, int64_t N, int act, float* C, int64_t ldc, int cfg,
                            void* stream);
+/* max_margin_loss (pinsage_training.py:31-41) of outputs given per position,
+ * Z f32 [3][B][d] (q, pos, neg calls; d <= 256 dividing 1024), with the train
+ * step's own kernels and reduction order (pinsage_engine_loss): scal f32[4] =
+ * {loss, 0, sum |z_q|^2, variance of the z_q}, G f32 [3][3B][d] = the loss
+ * cotangent of position (c, b) at row G[c][c*B + b] (other rows zero).  Equal
+ * rows give the step's loss bits.  scratch: pinsage_triplet_loss_scratch_bytes
+ * bytes, 16-B aligned.  The micro-batched step's loss. */
+int64_t pinsage_triplet_loss_scratch_bytes(int64_t B, int64_t d);
+int pinsage_triplet_loss(const float* Z, int64_t B, int64_t d, float margin, float* G, void* scratch, float* scal,
+                         void* stream);
 /* Interleaved split-bf16 table of src[rows][K] (K % 16 == 0, ld % 4 == 0):
  * row r at out + r * ldo (bf16 elements, ldo % 8 == 0, ldo >= 3K) holds K/16
  * stages of six 16-B chunks -- hi, mid, lo bf16 of the stage's 16 values, 8

@@ -128,11 +128,10 @@ def test_micro_batched_step_equals_fused_step(tmpdir_cwd, L, T, m):
     outs = [tr.train_batch(b) for tr in trs]
     torch.cuda.synchronize()
     l0, l1 = float(outs[0][0]), float(outs[1][0])
-    # the hinge terms are differences of cosines near 1: their fp32 rounding is
-    # ~1e-7 absolute (an ulp at 1) whatever the loss's size, so the floor is
-    # 1e-7 (the kernels' different row tilings of a 16-triple slice and of the
-    # whole batch round differently: 2.3e-8 apart on a 8.2e-4 loss, round 4)
-    assert abs(l0 - l1) <= 1e-5 * abs(l1) + 1e-7, (l0, l1)
+    # the sliced forward's rows are bitwise the whole batch's
+    # (tools/dbg/micro_z.py) and its loss runs the step's own loss kernels
+    # (pinsage_triplet_loss), so the loss agrees to the fused step's rounding
+    assert abs(l0 - l1) <= 1e-5 * abs(l1) + 1e-8, (l0, l1)
     p0, p1 = dict(trs[0].model.named_parameters()), dict(trs[1].model.named_parameters())
     for k in p0:
         a, c = p0[k].grad.double().cpu().numpy(), p1[k].grad.double().cpu().numpy()
@@ -209,3 +208,27 @@ def test_strided_nodeset_is_read_as_given(tmpdir_cwd):
             y = tr.model(tr.features, view)
             y_ref = tr.model(tr.features, view.contiguous().clone())
             assert torch.equal(y, y_ref)
+
+
+@pytest.mark.parametrize("B,d", [(1, 128), (5, 128), (64, 64), (512, 256)])
+def test_triplet_loss_kernel_matches_torch(B, d):
+    """pinsage_triplet_loss (the step's loss kernels on per-position rows,
+    used by the micro-batched step) against torch's max_margin_loss and its
+    autograd cotangent (pinsage_training.py:31-41): loss within 1e-6
+    relative, cotangent within 1e-5, variance within 1e-5; hinge-inactive
+    triples give zero rows."""
+    import pinsage_training as pt
+    g = torch.Generator(device="cuda").manual_seed(B + d)
+    Z = torch.randn(3, B, d, device="cuda", generator=g)
+    Z[2, ::3] = Z[1, ::3]  # some triples with the hinge exactly at the margin's side
+    margin = 0.3
+    loss, cot, var = pt._triplet_loss(Z, margin)
+    Zr = Z.detach().requires_grad_()
+    ref = pt.max_margin_loss(Zr[0], Zr[1], Zr[2], margin)
+    (gref,) = torch.autograd.grad(ref, [Zr])
+    torch.cuda.synchronize()
+    ref = ref.detach()
+    assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)) + 1e-9, (float(loss), float(ref))
+    assert ((cot - gref).norm() / gref.norm().clamp_min(1e-30)).item() <= 1e-5
+    if B > 1:
+        assert abs(float(var) - float(pt.batch_variance(Z[0]))) <= 1e-5 * abs(float(pt.batch_variance(Z[0])))
