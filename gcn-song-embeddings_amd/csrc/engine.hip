@@ -1179,6 +1179,9 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
 // once per workspace, before its first step.
 int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
   const EngineConfig& c = E.cfg;
+  // the side streams and events now, outside any capture (a stream or event
+  // created while a graph is being captured would invalidate that capture)
+  PS_TRY(ensure_streams(E));
   const int64_t top = E.L.back().S.cap;
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.G), 0, (size_t)(3 * top * c.out) * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.Kc), 0, (size_t)(3 * top) * 4, st));
