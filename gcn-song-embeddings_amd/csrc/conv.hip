@@ -1840,7 +1840,10 @@ int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64
   hipLaunchKernelGGL(csr_count_kernel, dim3(gb), dim3(1024), lds, st, loc, nS, T, nN, cnt,
                      (float*)nullptr, hid, nsplit, max_ranges);
   PS_CHECK_LAUNCH();
-  if (N_max <= 1024 * 64) {
+  // one block scans small sets; from ~4k rows on its threads' serial runs
+  // (N / 1024 rows each) outlast the two-launch form (C4 layer 1, ~15k rows:
+  // 26 us in one block)
+  if (N_max <= 4096) {
     hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, cnt, nN, off, cursor, cbase, chunks,
                        nchunks, split, nsplit);
     PS_CHECK_LAUNCH();
