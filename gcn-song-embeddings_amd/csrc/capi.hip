@@ -556,7 +556,6 @@ int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor,
     p.sk_slab = slab;
     p.sk_cnt = cnt;
     p.sk_cnt_len = kCnt;
-    if (const char* e = getenv("PINSAGE_SK_MIN_UNITS")) p.sk_min_units = std::max(1, atoi(e));
   }
   return launch_gemm(p, (hipStream_t)stream);
 }

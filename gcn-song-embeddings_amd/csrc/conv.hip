@@ -1860,8 +1860,7 @@ int launch_csr_build(const int32_t* loc, const float* wloc, const int* nS, int64
                      occ2, max_ranges, split, nsplit, chunks);
   PS_CHECK_LAUNCH();
   // canonical pair order (sorted by source row): bitwise-reproducible sums
-  static const bool canon = !getenv("PINSAGE_CSR_CANON") || atoi(getenv("PINSAGE_CSR_CANON")) != 0;
-  if (canon && occ2_tmp) {
+  if (occ2_tmp) {
     const int64_t max_chunks = dq_chunk_capacity(S_max, T, N_max);
     hipLaunchKernelGGL(csr_sort_chunks_kernel, dim3(grid_for(max_chunks * 64, 256, 2048)), dim3(256), 0, st,
                        chunks, nchunks, off, occ2);
@@ -1886,9 +1885,9 @@ int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks,
                      int hid, float* dpq, float* part, hipStream_t st, const int32_t* q_src,
                      int32_t* csrc) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
-  // persistent waves (each prefetches its next chunk): PINSAGE_DQ_GRID overrides (A/B)
-  static const int cap = getenv("PINSAGE_DQ_GRID") ? atoi(getenv("PINSAGE_DQ_GRID")) : 2048;
-  const int grid = grid_for(max_chunks * 64, 256, std::max(1, cap));
+  // persistent waves (each prefetches its next chunk); 512 to 4096 blocks
+  // measured alike at C2 (round 5), 2048 kept
+  const int grid = grid_for(max_chunks * 64, 256, 2048);
   if (csrc) {  // chunk rows: masked partials in part, no combine
     PS_REQUIRE(q_src, kErrArg, "dq: chunk rows need the rows' source indices");
     if (hid >= 512)

@@ -125,14 +125,13 @@ struct TimingSite {
 struct Engine {
   EngineConfig cfg{};
   bool timing = false;
-  // Which backward work runs beside the caller's stream (PINSAGE_BWD_STREAMS):
-  // 0 the CSR builds and the weight gradients (default), 1 nothing, 2 the CSR
-  // builds, 3 the weight gradients, 4 the CSR builds and layer 0's W gradient +
-  // the optimizer pass.  Measured at C2 in the one-launch step graph (bench.py):
-  // 0.605-0.615 / - / 0.645-0.648 / 0.611-0.640 / 0.620-0.626 ms per step.
-  int stream_mode = getenv("PINSAGE_BWD_STREAMS") ? atoi(getenv("PINSAGE_BWD_STREAMS")) : 0;
-  // PINSAGE_FUSED_HEAD=0: the head as separate GEMM launches (A/B measurement)
-  bool fused_head = !getenv("PINSAGE_FUSED_HEAD") || atoi(getenv("PINSAGE_FUSED_HEAD")) != 0;
+  // (The weight gradients run beside the caller's stream on side[1]; keeping
+  // them, the CSR work or layer 0's W gradient on the chain measured 0.611 to
+  // 0.648 ms/step against 0.605-0.615 in round 2 -- the A/B knob is retired.)
+  // The head as one fused forward / backward kernel (head.hip); the separate
+  // GEMM launches remain for the unfused arithmetic (fused_head false is no
+  // longer selectable: settled A/B).
+  bool fused_head = true;
   // the fused head backward sums repeated batch nodes' loss rows itself (no
   // rep_sum launch between the loss and it); PINSAGE_HEAD_REP_SUM=0: rep_sum
   // launch (A/B; bitwise the same G rows)
@@ -917,12 +916,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
   float* gr = E.grads;
   PS_TRY(ensure_streams(E));
   hipStream_t s_csr = E.side[0], s_wg = E.side[1];
-  if (E.stream_mode == 1 || E.stream_mode == 3) s_csr = st;
-  if (E.stream_mode == 1 || E.stream_mode == 2 || E.stream_mode == 4) s_wg = st;
-  // mode 4: layer 0's W gradient and the optimizer pass of every parameter but
-  // Q0 go beside the chain's tail (the transposed aggregation and dQ0, which
-  // do not need them); the other weight gradients stay on the chain
-  hipStream_t s_wg0 = E.stream_mode == 4 ? E.side[1] : s_wg;
+  hipStream_t s_wg0 = s_wg;
   // the CSR transposes were built with the frontier (engine_frontier)
   // weight gradients run on s_wg, each forked once its inputs exist on st
   const bool dfr = (E.defer_side & 1) != 0;

@@ -381,13 +381,13 @@ static int launch_mark_table_fz(unsigned long long* bits, const int32_t* members
   if (max_count <= 0) return kOk;
   const MarkFinalize f = fz ? *fz : MarkFinalize{};
   // windows of a full CU's LDS less the finalisation's scan scratch (the limit
-  // is raised once, on the first call, before any graph capture);
-  // PINSAGE_MARK_RANGES caps the window count (0: global atomics beyond 64 KiB, A/B)
+  // is raised once, on the first call, before any graph capture); beyond 64
+  // windows, global atomics
   constexpr int kWinWords = 20448;  // 159.75 KiB
   static const int win_ok = hipFuncSetAttribute((const void*)bits_mark_table_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                                 kWinWords * 8) == hipSuccess;
-  const int max_win = getenv("PINSAGE_MARK_RANGES") ? atoi(getenv("PINSAGE_MARK_RANGES")) : 64;
+  constexpr int max_win = 64;
   if (nw * 8 <= 64 * 1024) {
     const int gb = std::max(1, std::min(64, ceil_div(max_count * T, 4096)));
     hipLaunchKernelGGL(bits_mark_table_kernel, dim3(gb), dim3(1024), (size_t)nw * 8, st, bits,
