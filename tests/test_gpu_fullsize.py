@@ -124,3 +124,39 @@ def test_knn_full_size_sample():
     sims = np.einsum("qd,qkd->qk", e[q], e[n]) / (nrm[q][:, None] * nrm[n] + 1e-16)
     assert np.abs(sims - w).max() <= 2e-6
     assert float((n != rn).mean()) < 0.01
+
+
+def test_train_step_windowed_bitmaps_vs_oracle():
+    """A track universe between the LDS-bitmap and the multi-block sizes
+    (700k tracks: 10,938-word bitmaps, marked in LDS windows, finalised by
+    the marking launch's last workgroup -- frontier.hip MarkFinalize, the C3
+    path), one train step against the oracle at 1e-4."""
+    import graph
+    import pinsage_model as pm
+    import synthetic
+    from parity_util import check_train_step, make_trainer
+    n = 700_000
+    cols, memb, d, T_, B_ = n // 4, 4 * n, 128, 10, 64
+    pg = synthetic.make_playlist_graph(n, cols, memb, seed=5)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices)
+    pm.set_rng_mode("philox")
+    try:
+        torch.manual_seed(0)
+        w, nb = pm.precompute_neighborhoods_topt(g, n, pm.DEF_HOPS, pm.DEF_ALPHA, pm.DEF_T_PRECOMP, None)
+    finally:
+        pm.set_rng_mode("mt19937")
+    feats = torch.from_numpy(np.random.default_rng(6).standard_normal((n, d), dtype=np.float32))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 4 * B_, seed=7, csr=(indptr, indices)))
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g.nbhds_path = os.path.join(tmp, "nb.pt")
+            torch.save((w, nb), g.nbhds_path)
+            tr = make_trainer(g, n, feats.cuda(), pos, 2, T_, B_, 3.0, seed=0)
+            torch.manual_seed(3)
+            batch, _ = tr.next_batch()
+            check_train_step(tr, feats, w.numpy(), nb.numpy(), batch)
+        finally:
+            os.chdir(cwd)
