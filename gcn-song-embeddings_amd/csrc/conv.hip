@@ -1141,18 +1141,21 @@ int launch_pos_csr(const int32_t* pos_rank, int64_t n, const int* nS, int* rank_
 //     rep_sum_kernel, launched behind the writer, sums each group's rows in
 //     position order (pos_sorted) into G -- bitwise the same on every run.
 //   rank_off[0] == -1 (no position CSR): float atomics (order-dependent).
+// mode (det_mode): -1 atomics, 0 the only position, 1 a repeated node.  The
+// caller loads it with its other operands: read here, behind the row stores
+// of an earlier det_put, each load waited for those stores.
+__device__ __forceinline__ int det_mode(int ro0, int a0, int a1) { return ro0 < 0 ? -1 : a1 - a0 == 1 ? 0 : 1; }
 template <int XPL>
-__device__ __forceinline__ void det_put(const float (&x)[XPL], int d, int p, int r, int grp,
-                                        const int* __restrict__ rank_off, float* __restrict__ G, int64_t S_max,
-                                        float* __restrict__ Gp, int lane) {
+__device__ __forceinline__ void det_put(const float (&x)[XPL], int d, int p, int r, int grp, int mode,
+                                        float* __restrict__ G, int64_t S_max, float* __restrict__ Gp, int lane) {
   float* g = G + ((int64_t)grp * S_max + r) * d;
-  if (rank_off[0] < 0) {
+  if (mode < 0) {
 #pragma unroll
     for (int i = 0; i < XPL; ++i)
       if (lane + 64 * i < d) atomicAdd(g + lane + 64 * i, x[i]);
     return;
   }
-  float* dst = rank_off[r + 1] - rank_off[r] == 1 ? g : Gp + (int64_t)p * d;
+  float* dst = mode == 0 ? g : Gp + (int64_t)p * d;
 #pragma unroll
   for (int i = 0; i < XPL; ++i)
     if (lane + 64 * i < d) dst[lane + 64 * i] = x[i];
@@ -1248,6 +1251,7 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
   // round 1: indices
   int rq = 0, rp = 0, rn = 0;
   int64_t iq = 0, ip = 0, in = 0;
+  const int ro0 = rank_off[0];
   if (valid) {
     rq = pos_rank[3 * b];
     rp = pos_rank[3 * b + 1];
@@ -1258,7 +1262,21 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
       in = batch[3 * b + 2];
     }
   }
-  // round 2: rows into registers
+  // round 2: rows into registers, with each rank's position count (det_mode;
+  // no position CSR: rank_off[0], [1] are read and ignored)
+  int mode[3];
+  {
+    const int rr[3] = {rq, rp, rn};
+    int a0[3], a1[3];
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+      const int at = ro0 >= 0 ? rr[c3] : 0;
+      a0[c3] = rank_off[at];
+      a1[c3] = rank_off[at + 1];
+    }
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) mode[c3] = det_mode(ro0, a0[c3], a1[c3]);
+  }
   float zq[ZPL], zp[ZPL], zn[ZPL];
 #pragma unroll
   for (int i = 0; i < ZPL; ++i) {
@@ -1324,16 +1342,15 @@ __global__ __launch_bounds__(256) void loss_triple_kernel(
         xp[i] = (-g * a - p * pp) / np;
         xn[i] = (g * a - n * pn) / nn;
       }
-      det_put<ZPL>(xq, d, 3 * b, rq, 0, rank_off, G, S_max, Gp, lane);
-      det_put<ZPL>(xp, d, 3 * b + 1, rp, 1, rank_off, G, S_max, Gp, lane);
-      det_put<ZPL>(xn, d, 3 * b + 2, rn, 2, rank_off, G, S_max, Gp, lane);
-    } else if (valid && rank_off[0] >= 0) {
+      det_put<ZPL>(xq, d, 3 * b, rq, 0, mode[0], G, S_max, Gp, lane);
+      det_put<ZPL>(xp, d, 3 * b + 1, rp, 1, mode[1], G, S_max, Gp, lane);
+      det_put<ZPL>(xn, d, 3 * b + 2, rn, 2, mode[2], G, S_max, Gp, lane);
+    } else if (valid && ro0 >= 0) {
       // an inactive triple's positions of a repeated node hold zero rows (the
       // ordered sum reads every position of the node)
-      const int rr[3] = {rq, rp, rn};
 #pragma unroll
       for (int c3 = 0; c3 < 3; ++c3)
-        if (rank_off[rr[c3] + 1] - rank_off[rr[c3]] > 1)
+        if (mode[c3] == 1)
 #pragma unroll
           for (int i = 0; i < ZPL; ++i)
             if (lane + 64 * i < d) Gp[(int64_t)(3 * b + c3) * d + lane + 64 * i] = 0.f;
@@ -1591,7 +1608,8 @@ __global__ __launch_bounds__(256) void dout_accum_kernel(const float* __restrict
     float x[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) x[k] = lane + 64 * k < d ? dout[i * d + lane + 64 * k] : 0.f;
-    det_put<4>(x, d, (int)i, r, 0, rank_off, G, S_max, Gp, lane);
+    const int ro0 = rank_off[0], at = ro0 >= 0 ? r : 0;
+    det_put<4>(x, d, (int)i, r, 0, det_mode(ro0, rank_off[at], rank_off[at + 1]), G, S_max, Gp, lane);
     if (lane == 0) atomicAdd(Kc + r, 1);
   }
 }
@@ -1931,18 +1949,22 @@ int launch_loss(const float* Z, int d, const int32_t* pos_rank, int B, float mar
   PS_REQUIRE(d <= 256, kErrArg, "loss: out_dim must be <= 256");
   PS_REQUIRE(d <= 1024 && 1024 % d == 0, kErrArg, "loss: out_dim must divide 1024");
   const int nblk = ceil_div(B, 4);
-  const int fpl = d_in <= 128 ? 2 : d_in <= 256 ? 4 : 8;
+  // (features past 64 FPL per lane are streamed after the row stores, one
+  // waited round trip per 64 columns: C2's 1024 take 16 per lane instead)
+  const int fpl = d_in <= 128 ? 2 : d_in <= 256 ? 4 : d_in <= 512 ? 8 : 16;
 #define PS_LOSS(ZP, FP)                                                                           \
   hipLaunchKernelGGL((loss_triple_kernel<ZP, FP>), dim3(nblk), dim3(256), 0, st, Z, d, pos_rank, B, \
                      margin, feats, ld_f, d_in, batch, G, Kc, S_max, part, colpart, hinge, rank_off, Gp)
   if (d <= 128) {
     if (fpl == 2) PS_LOSS(2, 2);
     else if (fpl == 4) PS_LOSS(2, 4);
-    else PS_LOSS(2, 8);
+    else if (fpl == 8) PS_LOSS(2, 8);
+    else PS_LOSS(2, 16);
   } else {
     if (fpl == 2) PS_LOSS(4, 2);
     else if (fpl == 4) PS_LOSS(4, 4);
-    else PS_LOSS(4, 8);
+    else if (fpl == 8) PS_LOSS(4, 8);
+    else PS_LOSS(4, 16);
   }
 #undef PS_LOSS
   PS_CHECK_LAUNCH();

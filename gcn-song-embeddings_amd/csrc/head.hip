@@ -13,6 +13,8 @@
 // lane (l32, h) is row (r & 3) + 8 (r >> 2) + 4h, column l32 of the 32 x 32 tile.
 #include "common.h"
 
+#include <algorithm>
+
 namespace ps {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -73,8 +75,8 @@ __device__ __forceinline__ void head_fetch_rows(float4 (&v)[kHeadRows * (kHeadDi
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
-    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r0 + row < R && c < o) v[j] = *reinterpret_cast<const float4*>(src + (r0 + row) * o + c);
+    const float4 x = *reinterpret_cast<const float4*>(src + std::min<int64_t>(r0 + row, R - 1) * o + std::min(c, o - 4));
+    v[j] = r0 + row < R && c < o ? x : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 __device__ __forceinline__ void head_put_rows(float* sA, const float4 (&v)[kHeadRows * (kHeadDim / 4) / 256],
@@ -96,8 +98,8 @@ __device__ __forceinline__ void head_fetch_weight(float4 (&v)[kHeadWNI], const f
 #pragma unroll
   for (int j = 0; j < kHeadWNI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
-    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < o && c < o) v[j] = *reinterpret_cast<const float4*>(W + (int64_t)row * o + c);
+    const float4 x = *reinterpret_cast<const float4*>(W + (int64_t)std::min(row, o - 1) * o + std::min(c, o - 4));
+    v[j] = row < o && c < o ? x : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 __device__ __forceinline__ void head_put_weight(float* sW, const float4 (&v)[kHeadWNI], int tid) {
@@ -181,21 +183,53 @@ __device__ __forceinline__ void head_fetch_dz(float4 (&g)[3][kHeadRNI], int (&k)
   for (int j = 0; j < NI; ++j) {
     const int i = tid + 256 * j, row = i / (kHeadDim / 4), c = 4 * (i % (kHeadDim / 4));
     const bool ok = r0 + row < R && c < o;
+    const int64_t rr = std::min<int64_t>(r0 + row, R - 1);
+    const int cc = std::min(c, o - 4);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      k[q][j] = ok ? Kc[q * S_max + r0 + row] : 0;
-      g[q][j] = ok ? *reinterpret_cast<const float4*>(G + ((int64_t)q * S_max + r0 + row) * o + c)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int kv = Kc[q * S_max + rr];
+      const float4 gv = *reinterpret_cast<const float4*>(G + ((int64_t)q * S_max + rr) * o + cc);
+      k[q][j] = ok ? kv : 0;
+      g[q][j] = ok ? gv : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    o0[j] = reps && ok ? rank_off[r0 + row] : 0;
-    o1[j] = reps && ok ? rank_off[r0 + row + 1] : 0;
+    const int a0 = rank_off[reps ? rr : 0], a1 = rank_off[reps ? rr + 1 : 0];
+    o0[j] = reps && ok ? a0 : 0;
+    o1[j] = reps && ok ? a1 : 0;
   }
 }
 constexpr int kHeadRepBatch = 8;  // positions whose rows are in flight together
+constexpr int kHeadRepFirst = 4;  // the first positions of every item, all items together
+__device__ __forceinline__ void head_rep_add(float4 (&a)[3], int p, const float4& v) {
+  const int grp = p % 3;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (q == grp) a[q] = add4(a[q], v);
+}
 __device__ __forceinline__ void head_sum_reps(float4 (&g)[3][kHeadRNI], const int (&o0)[kHeadRNI],
                                               const int (&o1)[kHeadRNI], int o, int tid,
                                               const int32_t* __restrict__ pos_sorted,
                                               const float* __restrict__ Gp) {
+  // the first kHeadRepFirst positions of every repeated item: their position
+  // ids, then their rows, each as one round of loads over all items (item by
+  // item, every item cost two round trips of its own)
+  int pp[kHeadRNI][kHeadRepFirst];
+  float4 v[kHeadRNI][kHeadRepFirst];
+#pragma unroll
+  for (int j = 0; j < kHeadRNI; ++j)
+#pragma unroll
+    for (int t = 0; t < kHeadRepFirst; ++t) {
+      const int pv = pos_sorted[std::max(std::min(o0[j] + t, o1[j] - 1), 0)];
+      pp[j][t] = o1[j] - o0[j] >= 2 && o0[j] + t < o1[j] ? pv : -1;
+    }
+#pragma unroll
+  for (int j = 0; j < kHeadRNI; ++j) {
+    const int c = 4 * ((tid + 256 * j) % (kHeadDim / 4));
+#pragma unroll
+    for (int t = 0; t < kHeadRepFirst; ++t) {
+      const float4 x = *reinterpret_cast<const float4*>(Gp + (int64_t)std::max(pp[j][t], 0) * o + c);
+      v[j][t] = pp[j][t] >= 0 ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < kHeadRNI; ++j) {
     if (o1[j] - o0[j] < 2) continue;
@@ -203,23 +237,26 @@ __device__ __forceinline__ void head_sum_reps(float4 (&g)[3][kHeadRNI], const in
     float4 a[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) a[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int u0 = o0[j]; u0 < o1[j]; u0 += kHeadRepBatch) {
-      int pp[kHeadRepBatch];
-      float4 v[kHeadRepBatch];
+    // from zero in position order (rep_sum_kernel's additions)
 #pragma unroll
-      for (int t = 0; t < kHeadRepBatch; ++t) pp[t] = u0 + t < o1[j] ? pos_sorted[u0 + t] : -1;
-#pragma unroll
-      for (int t = 0; t < kHeadRepBatch; ++t)
-        v[t] = pp[t] >= 0 ? *reinterpret_cast<const float4*>(Gp + (int64_t)pp[t] * o + c)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = 0; t < kHeadRepFirst; ++t)
+      if (pp[j][t] >= 0) head_rep_add(a, pp[j][t], v[j][t]);
+    for (int u0 = o0[j] + kHeadRepFirst; u0 < o1[j]; u0 += kHeadRepBatch) {
+      int pb[kHeadRepBatch];
+      float4 w[kHeadRepBatch];
 #pragma unroll
       for (int t = 0; t < kHeadRepBatch; ++t) {
-        if (pp[t] < 0) continue;
-        const int grp = pp[t] % 3;
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (q == grp) a[q] = add4(a[q], v[t]);
+        const int pv = pos_sorted[std::min(u0 + t, o1[j] - 1)];
+        pb[t] = u0 + t < o1[j] ? pv : -1;
       }
+#pragma unroll
+      for (int t = 0; t < kHeadRepBatch; ++t) {
+        const float4 x = *reinterpret_cast<const float4*>(Gp + (int64_t)std::max(pb[t], 0) * o + c);
+        w[t] = pb[t] >= 0 ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int t = 0; t < kHeadRepBatch; ++t)
+        if (pb[t] >= 0) head_rep_add(a, pb[t], w[t]);
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) g[q][j] = a[q];
@@ -272,20 +309,25 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   const int lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int n0 = 32 * w, col = n0 + l32;
 #ifdef PS_HEAD_PROBE  // (diagnostic build only) wall-clock phases of block 0
-  uint64_t pt[6] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0};
+  uint64_t pt[10] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int pti = 1;
-#define PS_HPROBE() do { if (pti < 6) pt[pti++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define PS_HPROBE() do { if (pti < 10) pt[pti++] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define PS_HPROBE() do { } while (0)
 #endif
   // this lane's H1 (mask) and y values, fetched beside the staging loads
+  // (every load of the staging is unconditional, from a clamped address, and
+  // masked after: a load under a branch made the compiler wait for it inside
+  // the branch -- 16 serial round trips for these rows alone)
   float hv[16], yv[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = head_row(r, h);
     const bool ok = r0 + row < R && col < o;
-    hv[r] = ok ? H1[(r0 + row) * o + col] : 0.f;
-    yv[r] = ok ? y[(r0 + row) * o + col] : 0.f;
+    const int64_t at = std::min<int64_t>(r0 + row, R - 1) * o + std::min(col, o - 1);
+    const float hx = H1[at], yx = y[at];
+    hv[r] = ok ? hx : 0.f;
+    yv[r] = ok ? yx : 0.f;
   }
   // every global load first (the loss accumulators, both weights, the norms),
   // then the stores and LDS writes: a load issued behind a store waits for it
@@ -303,12 +345,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = head_row(r, h);
-    inv[r] = r0 + row < R ? nrm[r0 + row] : 1.f;
+    const float nx = nrm[std::min<int64_t>(r0 + row, R - 1)];
+    inv[r] = r0 + row < R ? nx : 1.f;
   }
+  PS_HPROBE();
   if (reps) head_sum_reps(g, o0, o1, o, tid, pos_sorted, Gp);
+  PS_HPROBE();
   head_put_dz(sA, G, g, k, S_max, dZ, r0, R, o, tid);
+  PS_HPROBE();
   head_put_weight(sW2, w2, tid);
   head_put_weight(sW1, w1, tid);
+  PS_HPROBE();
 #pragma unroll
   for (int r = 0; r < 16; ++r) inv[r] = 1.f / inv[r];
   __syncthreads();
@@ -333,15 +380,24 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   PS_HPROBE();
   acc = head_mm<false>(sA, sW1, n0, l32, h);  // dY
   PS_HPROBE();
-  // row dots y . dY: lane-partial over this wave's 32 columns, then 4 waves
+  // row dots y . dY: lane-partial over this wave's 32 columns, then 4 waves.
+  // The 16 rows' butterflies advance together, one level at a time: each level
+  // issues 16 independent cross-lane reads and waits once (row by row, every
+  // read waited for the one before it: 80 serial LDS-unit round trips, ~4 us)
+  float d[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = head_row(r, h);
-    float d = yv[r] * acc[r];
+  for (int r = 0; r < 16; ++r) d[r] = yv[r] * acc[r];
 #pragma unroll
-    for (int m = 1; m < 32; m <<= 1) d += __shfl_xor(d, m, 64);
-    if (l32 == 0) red[w * kHeadRows + row] = d;
+  for (int m = 1; m < 32; m <<= 1) {
+    float x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = __shfl_xor(d[r], m, 64);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) d[r] += x[r];
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (l32 == 0) red[w * kHeadRows + head_row(r, h)] = d[r];
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -355,8 +411,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   __syncthreads();
   PS_HPROBE();
   if (blockIdx.x == 0 && tid == 0)
-    printf("head_bwd probe [10ns]: loads %d mm1+dP1 %d mm2 %d tail %d\n", (int)(pt[1] - pt[0]),
-           (int)(pt[2] - pt[1]), (int)(pt[3] - pt[2]), (int)(pt[4] - pt[3]));
+    printf("head_bwd probe [10ns]: issue %d reps %d put_dz %d put_w %d sync %d mm1+dP1 %d mm2 %d tail %d\n",
+           (int)(pt[1] - pt[0]), (int)(pt[2] - pt[1]), (int)(pt[3] - pt[2]), (int)(pt[4] - pt[3]),
+           (int)(pt[5] - pt[4]), (int)(pt[6] - pt[5]), (int)(pt[7] - pt[6]), (int)(pt[8] - pt[7]));
 #endif
 }
 
