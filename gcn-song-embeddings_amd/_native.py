@@ -77,6 +77,7 @@ _SIGS = {
                                           i64, vp, vp, vp, i64, vp, i64, i64, vp, i64, vp, vp]),
     "pinsage_engine_set_fly": (ctypes.c_int, [vp, i64, vp, vp, i64, i64]),
     "pinsage_fly_publish_err": (ctypes.c_int, [vp, vp, i64, i64, vp, i64, vp]),
+    "pinsage_fly_gate_adam": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_frontier_workspace": (i64, [i64]),
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),
     "pinsage_frontier_local_idx": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),

@@ -29,6 +29,7 @@ int launch_visit_dense(const int32_t*, const int64_t*, int64_t, int64_t, int64_t
 int64_t fly_workspace_bytes(int64_t, int64_t, int64_t, int64_t, int64_t);
 int fly_init_workspace(void*, int64_t, int64_t, int64_t, int64_t, int64_t, hipStream_t);
 int fly_publish_err(const int*, void*, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);
+int fly_gate_adam(int*, float*, hipStream_t);
 int fly_sample(const int64_t*, const int32_t*, int64_t, const int64_t*, int64_t, int64_t, int64_t, int64_t, int64_t,
                float, const uint64_t*, void*, int64_t, int32_t* const*, float* const*, int32_t**, int64_t, int64_t*,
                int*, int64_t*, int64_t, const float*, int64_t, int64_t, float*, int64_t, int*, hipStream_t);
@@ -707,6 +708,10 @@ int pinsage_fly_sample(const int64_t* indptr, const int32_t* indices, int64_t n_
 int pinsage_fly_publish_err(const int* err, void* ring, int64_t slot_bytes, int64_t R, const int64_t* ctr,
                             int64_t err_off, void* stream) {
   return fly_publish_err(err, ring, slot_bytes, R, ctr, err_off, (hipStream_t)stream);
+}
+
+int pinsage_fly_gate_adam(int* err, float* coef, void* stream) {
+  return fly_gate_adam(err, coef, (hipStream_t)stream);
 }
 
 int pinsage_conv_agg_project(const float* h, int64_t ldh, int64_t d, const int32_t* self_src,

@@ -1539,6 +1539,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    int64_t n, const float* __restrict__ coef,
                                                    float beta1, float beta2, float eps) {
   const float ss = coef[0], bc2 = coef[1];
+  // bc2 = sqrt(1 - beta2^t) > 0 on every real step; 0 marks a step the device
+  // refused (the on-the-fly sampler's error words, pinsage_fly_gate_adam):
+  // parameters and moments stay untouched, as when the reference raises
+  if (!(bc2 > 0.f)) return;
   const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
   const int64_t n4 = n >> 2;
   float4* p4 = reinterpret_cast<float4*>(p);
@@ -1675,7 +1679,7 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
                                    (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
       const int64_t e = e4 * 4, m = e / N, n = e - m * N, o = m * ld + n;
       *reinterpret_cast<float4*>(out + o) = r;
-      if (ad.p) {  // the slice's Adam step, as adam_kernel would apply it
+      if (ad.p && bc2 > 0.f) {  // the slice's Adam step, as adam_kernel would apply it (bc2 0: refused)
         float4 pp = *reinterpret_cast<const float4*>(ad.p + o);
         float4 mm = *reinterpret_cast<const float4*>(ad.m + o);
         float4 vv = *reinterpret_cast<const float4*>(ad.v + o);
@@ -1701,7 +1705,7 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
   if (g == 0 && m < M) {
     const float r = (redf[j] + redf[64 + j]) + (redf[128 + j] + redf[192 + j]);
     bias_out[m] = r;
-    if (ad.pb) adam1(ad.pb[m], r, ad.mb[m], ad.vb[m], ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+    if (ad.pb && bc2 > 0.f) adam1(ad.pb[m], r, ad.mb[m], ad.vb[m], ss, bc2, ad.beta2, omb1, omb2, ad.eps);
   }
 }
 

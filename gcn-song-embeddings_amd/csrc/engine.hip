@@ -164,6 +164,13 @@ struct Engine {
   // 0.483 -> 0.476, 183 -> 179 -- the GEMM's K grows by the split rows' extra
   // chunks (C2 Q0 wgrad 69 -> 79 µs) about as much as the combine saved.
   bool dq_chunk_rows = getenv("PINSAGE_DQ_CHUNK_ROWS") && atoi(getenv("PINSAGE_DQ_CHUNK_ROWS")) != 0;
+  // PINSAGE_CSR_FORK: the frontier's CSR transposes with a fork onto side[0]
+  // (engine_frontier): 1 = layer 0's CSR on side[0] beside the upper layers',
+  // 2 = an empty branch (fork + join, no work); 0 (default) = one stream.
+  // Either fork is joined back into the frontier's stream before
+  // engine_frontier returns, so no engine call leaves a side stream unjoined
+  // inside a caller's capture (tests/test_gpu_trainer.py)
+  int csr_fork = getenv("PINSAGE_CSR_FORK") ? atoi(getenv("PINSAGE_CSR_FORK")) : 0;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -620,16 +627,27 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
   // inference forward (no backward will follow) skips them.
   if (!with_csr) return kOk;
   PS_TRY(csr_prepare());
+  // (PINSAGE_CSR_FORK) the fork's wait binds to an event recorded on st here,
+  // after the index tables the CSR builds read; the join below is recorded on
+  // side[0] after its last launch and waited on st before this call returns
+  hipStream_t s_fk = st;
+  if (E.csr_fork) {
+    PS_TRY(ensure_streams(E));
+    s_fk = E.side[0];
+    PS_TRY(dep(E, st, s_fk));
+  }
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
-    Timed tc(E, lname("fwd.csr", l), st);
+    hipStream_t sl = (E.csr_fork == 1 && l == 0) ? s_fk : st;
+    Timed tc(E, lname("fwd.csr", l), sl);
     PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), cnt(lb.S), lb.S.cap, T, cnt(lb.N),
                             lb.N.cap, at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
                             at<int>(ws, lb.cursor), at<int>(ws, lb.cbase), at<int2>(ws, lb.occ2),
                             at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), at<int2>(ws, lb.split),
-                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, st,
+                            at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, sl,
                             at<int2>(ws, lb.occ2b)));
   }
+  if (E.csr_fork) PS_TRY(dep(E, s_fk, st));  // join: nothing of this call stays on side[0]
   return kOk;
 }
 

@@ -168,9 +168,13 @@ __global__ void fly_top_tables_kernel(const int64_t* __restrict__ src, int B, in
   const int64_t id = src[m];
   const int64_t row = vj[m] >= 0 ? x0 + vj[m] : id;
   const int32_t v = nb32[e];
-  if (v < 0 || v >= n) atomicOr(err + 1, 1);
-  nbt[row * T + t] = v + (int32_t)(c * n);
-  wnt[row * T + t] = wn[e];
+  // a drawn id outside [0, n) flags err[1] and is stored as the source itself
+  // with weight 0, so no table entry ever names a node outside the universe
+  // (the engine's frontier marks table ids unchecked, before the error is read)
+  const bool bad = v < 0 || v >= n;
+  if (bad) atomicOr(err + 1, 1);
+  nbt[row * T + t] = bad ? (int32_t)id : v + (int32_t)(c * n);
+  wnt[row * T + t] = bad ? 0.f : wn[e];
   (void)last;
 }
 
@@ -185,10 +189,11 @@ __global__ void fly_tables_kernel(const int32_t* __restrict__ cur, const int* __
     int c = 0;
     while (c + 1 < kFlyC && s >= seg[c + 1]) ++c;
     const int32_t v = nb32[e];
-    if (v < 0 || v >= n) atomicOr(err + 1, 1);
+    const bool bad = v < 0 || v >= n;  // (as fly_top_tables_kernel: the source itself, weight 0)
+    if (bad) atomicOr(err + 1, 1);
     const int64_t row = cur[s];
-    nbt[row * T + t] = v + (int32_t)(c * n);
-    wnt[row * T + t] = wn[e];
+    nbt[row * T + t] = bad ? (int32_t)row : v + (int32_t)(c * n);
+    wnt[row * T + t] = bad ? 0.f : wn[e];
   }
 }
 
@@ -210,8 +215,9 @@ __global__ void fly_mark_kernel(unsigned long long* __restrict__ bits, const Src
     } else {
       c = (int)(s / B);
     }
+    if (t < T && (nb32[s * T + t] < 0 || nb32[s * T + t] >= n)) continue;  // (err[1]: the table kernels)
     const int64_t v = t < T ? (int64_t)nb32[s * T + t] + (int64_t)c * n : (int64_t)cur[s];
-    if (v < 0 || v >= kFlyC * n) continue;  // (err[1] is set by the table kernels)
+    if (v < 0 || v >= kFlyC * n) continue;
     const unsigned long long bit = 1ull << (v & 63);
     if (!(__hip_atomic_load(bits + (v >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
       atomicOr(bits + (v >> 6), bit);
@@ -276,7 +282,26 @@ __global__ void fly_publish_err_kernel(const int* __restrict__ err, char* __rest
   }
 }
 
+// Refuse the step's optimizer update when its sampling failed: err[2] is a
+// sticky halt word (set here, cleared only by the host once it has raised the
+// error), and a halted step's Adam coefficient bc2 = 0 makes every Adam kernel
+// of the step leave parameters and moments untouched (conv.hip adam_kernel,
+// reduce_slabs_2d_kernel).  The reference raises before optimizer.step().
+__global__ void fly_gate_adam_kernel(int* __restrict__ err, float* __restrict__ coef) {
+  if (threadIdx.x == 0) {
+    if (err[0] != 0x7f7f7f7f || err[1] != 0) err[2] = 1;
+    if (err[2]) coef[1] = 0.f;
+  }
+}
+
 // ---------------------------------------------------------------- host side
+int fly_gate_adam(int* err, float* coef, hipStream_t st) {
+  PS_REQUIRE(err && coef, kErrArg, "fly_gate_adam: null argument");
+  hipLaunchKernelGGL(fly_gate_adam_kernel, dim3(1), dim3(64), 0, st, err, coef);
+  PS_CHECK_LAUNCH();
+  return kOk;
+}
+
 int fly_publish_err(const int* err, void* ring, int64_t slot_bytes, int64_t R, const int64_t* ctr, int64_t err_off,
                     hipStream_t st) {
   PS_REQUIRE(err && ring && ctr && R > 0 && err_off >= 0 && err_off % 4 == 0 && err_off + 8 <= slot_bytes, kErrArg,

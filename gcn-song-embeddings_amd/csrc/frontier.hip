@@ -166,7 +166,7 @@ __global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long lon
     for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
       const int64_t f = e / T, t = e - f * T;
       const int64_t v = nb[(int64_t)members[f] * ld + t];
-      atomicOr(lbits + (v >> 6), 1ull << (v & 63));
+      if (v >= 0 && v < (int64_t)lds_words * 64) atomicOr(lbits + (v >> 6), 1ull << (v & 63));
     }
     __syncthreads();
     for (int w = threadIdx.x; w < lds_words; w += blockDim.x)
@@ -175,22 +175,32 @@ __global__ __launch_bounds__(1024) void bits_mark_table_kernel(unsigned long lon
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (int64_t)gridDim.x * blockDim.x) {
       const int64_t f = e / T, t = e - f * T;
-      mark(bits, nb[(int64_t)members[f] * ld + t]);
+      const int64_t v = nb[(int64_t)members[f] * ld + t];
+      if (v >= 0 && v < nwords * 64) mark(bits, v);
     }
   }
   if (!fz.ticket) return;
-  // The last block to finish finalises.  The bitmap is only ever changed by
-  // atomics, which are performed at the device's L2, and read back by the
-  // last block with device-coherent loads (finalize_block<true>): a block's
-  // ordering point is its atomics' completion (vmcnt), not a cache fence --
-  // a __threadfence in every thread (L2 writeback + invalidate) made this
-  // launch slower than the two it replaces.
+  // The last block to finish finalises (the split-K counter hand-off of the
+  // HIP guide): every wave drains its atomics, then ONE lane per block runs an
+  // agent-scope release before its ticket add, and the block drawing the last
+  // ticket runs ONE agent-scope acquire before it reads the bitmap back (with
+  // device-coherent loads, finalize_block<true>).  One fence per block, not
+  // per thread: a __threadfence in every thread made this launch slower than
+  // the two it replaces.
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    last = __hip_atomic_fetch_add(fz.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-    if (last) __hip_atomic_store(fz.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (keep: the fence's own wait can be dropped)
+    const bool l = __hip_atomic_fetch_add(fz.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (int)gridDim.x - 1;
+    if (l) {
+      __hip_atomic_store(fz.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last = l;
   }
   __syncthreads();
   if (!last) return;
@@ -323,10 +333,12 @@ __global__ __launch_bounds__(1024) void bits_top_set_kernel(
     const int64_t* __restrict__ ids, int64_t n, int64_t limit, int64_t nwords,
     uint32_t* __restrict__ prefix, int32_t* __restrict__ members, int* __restrict__ count_out, int64_t x0,
     const int* __restrict__ x_n) {
-  // (one block: its own stores and atomics are ordered by their completion
-  // (vmcnt) and the barrier; the atomics are performed at L2 and read back
-  // with device-coherent loads -- no cache fence needed)
-  for (int64_t w = threadIdx.x; w < zero_words; w += 1024) zero[w] = 0ull;
+  // (one block: the zeroing stores are agent-scope atomic stores, like the
+  // ORs that follow them on the same words, so the block's own completion
+  // (vmcnt) and barrier order them; the bitmap is read back with
+  // device-coherent loads)
+  for (int64_t w = threadIdx.x; w < zero_words; w += 1024)
+    __hip_atomic_store(zero + w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int64_t i = threadIdx.x; i < n; i += 1024) {

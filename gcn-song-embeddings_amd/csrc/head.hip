@@ -454,8 +454,11 @@ int launch_head_bwd(float* G, int* Kc, int64_t S_max, float* dZ, int o, const in
   PS_REQUIRE(!Gp || (rank_off && pos_sorted), kErrArg, "head: repeated-rank rows need rank_off and pos_sorted");
   PS_TRY(head_prepare());
   if (max_rows <= 0) return kOk;
+  // head_fetch_dz reads rank_off[0] whether or not the repeated ranks are
+  // summed: without Gp any valid int works (the loss's Kc counters)
+  const int* ro = rank_off ? rank_off : Kc;
   hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)ceil_div(max_rows, kHeadRows)), dim3(256),
-                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp, rank_off,
+                     kHeadBwdLds, st, G, Kc, S_max, dZ, o, nrows, H1, G1w, G2w, y, nrm, dP1, dp, ro,
                      pos_sorted, Gp);
   PS_CHECK_LAUNCH();
   return kOk;

@@ -619,7 +619,9 @@ class _FlyDevice:
         self.pos_ids = torch.empty(_FLY_CALLS * self.B, dtype=torch.int64, device=dev)
         self.n_x = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ids_xo = torch.zeros(self.x_cap, dtype=torch.int64, device=dev)
-        self.err = torch.zeros(2, dtype=torch.int32, device=dev)
+        # [walk error, id error, halt]: halt is the captured step's sticky
+        # refusal of its optimizer update (pinsage_fly_gate_adam)
+        self.err = torch.zeros(3, dtype=torch.int32, device=dev)
         self.seeds = torch.zeros(_FLY_CALLS * self.L, dtype=torch.int64, device=dev)
         self.batch_dev = torch.zeros((self.B, _FLY_CALLS), dtype=torch.int64, device=dev)
         self.feats = feats
@@ -644,7 +646,7 @@ class _FlyDevice:
     def check_err(self):
         """Raise what the reference raises if the last sampled step met a
         zero-degree node or drew an id >= n (synchronises)."""
-        e = self.err.tolist()
+        e = self.err[:2].tolist()
         if e[0] != 0x7f7f7f7f:
             raise RuntimeError("walk: zero-degree node met (the reference's torch.randint(0) raises here)")
         if e[1]:

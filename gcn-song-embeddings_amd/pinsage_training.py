@@ -998,7 +998,12 @@ class _FusedFlyStep(_FusedStep):
 
     A zero-degree node met by a walk, or a drawn id >= n_items, is reported
     through the ring slot and raised when the host next waits for that slot
-    (up to HOST_RING steps late; the per-call path raises at the draw)."""
+    (up to HOST_RING steps late; the per-call path raises at the draw), or
+    at the latest when the optimizer state is synchronised (save_model, the
+    end of train(): sync_optimizer_step checks every outstanding slot).  The
+    device refuses the optimizer update of that step and of every later one
+    until the host has raised (pinsage_fly_gate_adam: a sticky halt word), so
+    the parameters are the ones the reference holds when it raises."""
 
     def __init__(self, trainer):
         super().__init__(trainer)
@@ -1043,11 +1048,32 @@ class _FusedFlyStep(_FusedStep):
         e = self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32).tolist()
         self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32)[0] = 0x7f7f7f7f
         self.ring[k, self.slot_err:self.slot_err + 8].view(torch.int32)[1] = 0
+        if e[0] != 0x7f7f7f7f or e[1]:
+            # raising now: the steps after the failed one (already enqueued)
+            # stay refused; steps enqueued from here on update again
+            self.fd.err[2:3].zero_()
         if e[0] != 0x7f7f7f7f:
             raise RuntimeError("walk: zero-degree node met (the reference's torch.randint(0) raises here)")
         if e[1]:
             raise IndexError("sampled neighbourhood reaches ids >= n_items (collection ids in the "
                              "zero-weight tail: the reference's h[nb] raises IndexError)")
+
+    def check_outstanding(self):
+        """Wait for every step whose error words the host has not read yet and
+        raise the first failure among them (in step order)."""
+        R = self.HOST_RING
+        for i in range(max(0, self.nstep - R), self.nstep):
+            k = i % R
+            ev = self.ring_ev[k]
+            if ev is None:
+                continue
+            ev.synchronize()
+            self.ring_ev[k] = None
+            self._check_slot(k)
+
+    def sync_optimizer_step(self):
+        self.check_outstanding()
+        super().sync_optimizer_step()
 
     def _fly_seq(self, B):
         """One step's device work (the captured graph's contents)."""
@@ -1064,6 +1090,8 @@ class _FusedFlyStep(_FusedStep):
                                        self.slot_seeds, fd.seeds.numel() * 8, nat.ptr(fd.seeds), 0, None, st),
                   "step_stage")
         fd.sample(fd.batch_dev, pos_out=self.ids_view[0])
+        # a failed sampling refuses this step's Adam update (and later ones)
+        nat.check(L.pinsage_fly_gate_adam(nat.ptr(fd.err), coef, st), "fly_gate_adam")
         nat.check(L.pinsage_engine_frontier(e.h, nat.ptr(ws), nat.ptr(self.ids_view[0]), 3 * B, st), "frontier")
         nat.check(L.pinsage_engine_forward_layers(e.h, nat.ptr(ws), st), "forward_layers")
         nat.check(L.pinsage_engine_loss(e.h, nat.ptr(ws), B, float(self.tr.margin), 1, st), "loss")
@@ -1441,6 +1469,9 @@ class PinSage:
             self.b = 0
             self.e += 1
             self.scheduler.step()
+        # the fused step's optimizer bookkeeping (and, sampling on the fly, the
+        # error words of its last steps) before control returns to the caller
+        self._sync_state()
 
     def embed(self, ids=None, bsize=None):
         """Node embeddings, optionally in bsize batches (pinsage_training.py:258-275,
@@ -1460,8 +1491,9 @@ class PinSage:
         return self.embeddings
 
     def _sync_state(self):
-        if self._fused is not None:
-            self._fused.sync_optimizer_step()
+        for f in (self._fused, getattr(self, "_fused_fly", None)):
+            if f is not None:
+                f.sync_optimizer_step()
 
     def load_model(self):
         load_path = os.path.join(BASE_RUN_DIR, self.run_name, "state.pt")

@@ -182,6 +182,13 @@ int pinsage_fly_sample(const int64_t* indptr, const int32_t* indices, int64_t n_
  * it next waits for that slot). */
 int pinsage_fly_publish_err(const int* err, void* ring, int64_t slot_bytes, int64_t R, const int64_t* ctr,
                             int64_t err_off, void* stream);
+/* Refuse the captured on-the-fly step's optimizer update when its sampling
+ * failed (err[0] / err[1] as pinsage_fly_sample sets them): err[2] becomes a
+ * sticky halt word (the host clears it after raising), and a halted step's
+ * Adam coefficients get bc2 = coef[1] = 0, which every fused Adam kernel takes
+ * as "leave parameters and moments untouched" -- the reference raises before
+ * optimizer.step() (pinsage_model.py:25, pinsage_training.py:188-191). */
+int pinsage_fly_gate_adam(int* err, float* coef, void* stream);
 /* sample_neighborhood (pinsage_model.py:88-101): dense f64 [n_src][n_all]. */
 int pinsage_visit_dense(const int32_t* trace, const int64_t* sources, int64_t n_src,
                         int64_t n_hops, int64_t n_all, double* dense, void* stream);

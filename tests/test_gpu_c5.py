@@ -1,0 +1,154 @@
+"""The full C5 configuration on one MI355X (BASELINE.json configs[4]: 100M
+nodes / 1B edges, d_in 256, 3 layers, fanout 50), built on the device exactly as
+bench.py --config c5 builds it (VERDICT r05 "missing" item 4).  Checked at full
+size, in pieces the host can afford:
+
+* the device-built graph's shape (100M nodes, >= 1B directed edges, track /
+  collection bipartition);
+* precompute_device_table over all 80M sources (pinsage_model.py:109-132, the
+  model's first T = 50 of the top-100, kept in HBM), chunk by chunk on the
+  device: weights sorted, each row's weights summing to 1 (or an all-zero row),
+  ids are tracks and never the source where the weight is positive;
+* 8 of those rows (the first, the last, 6 random) bit-exact against the oracle's Philox walk + libstdc++ top-k
+  on the host copy of the CSR (ids exactly, weights to the f32 rounding of the
+  f64 normalisation), and 32 sources re-walked in MT19937 mode (the reference's
+  stream) bit-exact against the oracle (ids and f64 weights);
+* the frontier of one micro-batch slice (16 triples, three layers) against the
+  oracle's relevant_nodes_per_layer_precomp restatement on the same table rows;
+* one micro-batched train step (slices of 16 triples) with finite loss and
+  finite gradients that change the parameters.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class _RowsOnDevice:
+    """table[cur, :T] for the oracle's frontier restatement, gathered from the
+    device table (the host never holds the 32 GB table)."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __getitem__(self, key):
+        rows, cols = key
+        idx = torch.from_numpy(np.asarray(rows, np.int64)).to(self.t.device)
+        return self.t[idx][:, cols].cpu().numpy()
+
+
+def _dense_topk(indptr, indices, n_all, src, trace, T):
+    """The oracle's visit_prob + libstdc++ top-k for one source at a time (a
+    [1, 100M] f64 row each: sample_neighborhood_topt's dense matrix, bounded)."""
+    from oracle import oracle as orc
+    W = np.zeros((len(src), T), np.float64)
+    N = np.zeros((len(src), T), np.int64)
+    for i, s in enumerate(src):
+        vp = orc.visit_prob(trace[i:i + 1], [s], n_all)
+        W[i], N[i] = (a[0] for a in orc.topk(vp, T))
+        del vp
+    return W, N
+
+
+def test_full_size_c5_precompute_frontier_and_step():
+    import bench
+    import pinsage_model as pm
+    import pinsage_training as pt
+    from oracle import oracle as orc
+    cfg = dict(bench.CONFIGS["c5"])
+    n, T, L = cfg["n_tracks"], cfg["T"], cfg["n_layers"]
+    pg, g, feats, pos = bench.build_problem_device(cfg)
+    n_all = pg.n_all
+    assert n_all == 100_000_000 and pg.n_edges >= 1_000_000_000, (n_all, pg.n_edges)
+    indptr_d, indices_d = g.device_csr(torch.device("cuda"))
+    # the bipartition: tracks link only to collections and back
+    for i in range(0, n_all, 1 << 24):
+        lo, hi = int(indptr_d[i].item()), int(indptr_d[min(i + (1 << 24), n_all)].item())
+        seg = indices_d[lo:hi]
+        assert int(seg.min()) >= 0 and int(seg.max()) < n_all
+    assert int(indices_d[:int(indptr_d[n].item())].min()) >= n  # track rows name collections
+
+    # ---- precompute_device_table over every source (Philox, one key)
+    pm.set_rng_mode("philox")
+    try:
+        torch.manual_seed(0)
+        key_mt = orc.MT(0)
+        d = key_mt.draws(2)
+        key = (int(d[0]) << 32) | int(d[1])
+        tab = pm.precompute_device_table(g, n, pm.DEF_HOPS, pm.DEF_ALPHA, T, pm.DEF_T_PRECOMP)
+    finally:
+        pm.set_rng_mode("mt19937")
+    nb, wn = tab.nb32, tab.wn
+    assert tuple(nb.shape) == (n, T) and tuple(wn.shape) == (n, T)
+    step = 1 << 22
+    for i in range(0, n, step):
+        w_c, nb_c = wn[i:i + step], nb[i:i + step]
+        assert bool((w_c[:, 1:] <= w_c[:, :-1]).all())                       # sorted descending
+        s = w_c.double().sum(1)
+        assert bool(((s - 1).abs() <= 1e-5).logical_or(s == 0).all())          # normalised over T
+        assert bool(((nb_c >= 0) & (nb_c < n)).all())                          # tracks
+        src = torch.arange(i, i + nb_c.shape[0], device=nb_c.device, dtype=torch.int32)[:, None]
+        assert not bool(((nb_c == src) & (w_c > 0)).any())                     # never the source
+    # 8 rows against the oracle's Philox walk (source s keyed at position s)
+    indptr = indptr_d.cpu().numpy()
+    indices = indices_d.cpu().numpy()
+    rows = np.random.default_rng(11).integers(0, n, 8).astype(np.int64)
+    rows[0], rows[1] = 0, n - 1
+    traces = np.concatenate([orc.walk_philox(indptr, indices, [s], pm.DEF_HOPS, pm.DEF_ALPHA, key, 0, int(s))
+                             for s in rows])
+    rw, rn = _dense_topk(indptr, indices, n_all, rows, traces, pm.DEF_T_PRECOMP)
+    got_nb = nb[torch.from_numpy(rows).cuda()].cpu().numpy()
+    got_w = wn[torch.from_numpy(rows).cuda()].cpu().numpy()
+    assert np.array_equal(got_nb, rn[:, :T])
+    ref_w = rw[:, :T] / np.maximum(rw[:, :T].sum(1, keepdims=True), 1e-300)
+    assert np.allclose(got_w, ref_w.astype(np.float32), rtol=2e-7, atol=0)
+
+    # ---- 32 sources in MT19937 mode (the reference's stream), bit-exact
+    src = np.random.default_rng(1).integers(0, n, 32).astype(np.int64)
+    torch.manual_seed(17)
+    tk = pm.sample_neighborhood_topt(g, n, torch.from_numpy(src), pm.DEF_HOPS, pm.DEF_ALPHA, 100)
+    mt = orc.MT(17)
+    trace = orc.walk_mt(indptr, indices, src, pm.DEF_HOPS, pm.DEF_ALPHA, mt)
+    rw2, rn2 = _dense_topk(indptr, indices, n_all, src, trace, 100)
+    assert np.array_equal(tk.indices.numpy(), rn2) and np.array_equal(tk.values.numpy(), rw2)
+    del indices, trace
+
+    # ---- one micro-batch slice's frontier (16 triples = 48 ids, three layers)
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g.nbhds_path = os.path.join(tmp, "nb.pt")
+            torch.manual_seed(0)
+            tr = pt.PinSage(g, n, feats, pos, log=False, load_save=False, nbhds=tab)
+            if tr.T != T or tr.n_layers != L:
+                tr.T, tr.n_layers = T, L
+                torch.manual_seed(0)
+                tr.model = pm.PinSageModel(g, tr.n, L, tr.dimensions, tr.n_hops, tr.alpha, T, tr.nbhds)
+                tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+            tr.batch_size = cfg["batch"]
+            tr.micro_batch = cfg["micro_batch"]
+            torch.manual_seed(1234)
+            batch, _ = tr.next_batch()
+            ids = batch[:cfg["micro_batch"]].reshape(-1)
+            got = pm.relevant_nodes_per_layer_precomp(ids, L, T, (wn, nb))
+            ref = orc.frontier(ids.numpy(), L, T, _RowsOnDevice(wn), _RowsOnDevice(nb))
+            assert got[0][0].shape[0] > 100_000  # (the bottom layer reaches ~10^5-10^6 nodes)
+            for (gs, gw, gn), (rs, rw_, rn_) in zip(got, ref):
+                assert np.array_equal(gs.cpu().numpy(), rs)
+                assert np.array_equal(gn.cpu().numpy(), rn_) and np.array_equal(gw.cpu().numpy(), rw_)
+            # ---- one micro-batched step
+            before = torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).clone()
+            loss, nfl, var = tr.train_batch(batch)
+            torch.cuda.synchronize()
+            assert np.isfinite(float(loss)) and np.isfinite(float(nfl)) and np.isfinite(float(var))
+            after = torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()])
+            assert bool(torch.isfinite(after).all()) and not torch.equal(before, after)
+            for p in tr.model.parameters():
+                assert p.grad is not None and bool(torch.isfinite(p.grad).all())
+        finally:
+            os.chdir(cwd)

@@ -152,3 +152,96 @@ def test_fused_fly_step_trains_like_the_per_call_path(L, T, monkeypatch):
                 os.chdir(cwd)
     finally:
         pm.set_rng_mode("mt19937")
+
+
+def _drop_track(indptr, indices, z):
+    """The CSR with every membership of track z removed (z keeps a zero-degree
+    row): a walk from z meets a zero-degree node."""
+    n_all = indptr.shape[0] - 1
+    rows = np.repeat(np.arange(n_all), np.diff(indptr))
+    keep = (rows != z) & (indices != z)
+    cnt = np.bincount(rows[keep], minlength=n_all)
+    ip = np.zeros(n_all + 1, np.int64)
+    ip[1:] = np.cumsum(cnt)
+    return ip, indices[keep].astype(np.int32)
+
+
+@pytest.mark.parametrize("captured", [False, True])
+def test_fused_fly_step_refuses_update_after_sampling_error(captured, monkeypatch):
+    """A zero-degree node met by the captured on-the-fly step:
+    the reference raises inside the model call, before optimizer.step().  The
+    device step reports it through its ring slot; pinsage_fly_gate_adam
+    refuses that step's Adam update and every later one until the host has
+    raised, and the host raises at the latest when the optimizer state is
+    synchronised (sync_optimizer_step checks every outstanding slot).  So after
+    the error is raised, the parameters and Adam moments are exactly those
+    after the last good step; once raised, training continues and updates."""
+    import graph
+    import pinsage_model as pm
+    import pinsage_training as pt
+    import synthetic
+    pm.set_rng_mode("philox")
+    monkeypatch.setenv("PINSAGE_FLY_FUSED", "1")
+    try:
+        with tempfile.TemporaryDirectory() as tmp:
+            cwd = os.getcwd()
+            os.chdir(tmp)
+            try:
+                pg = synthetic.make_playlist_graph(N, 750, 40000, seed=51)
+                z = 17
+                indptr, indices = _drop_track(*pg.csr(), z)
+                g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
+                feats = torch.from_numpy(synthetic.make_features(N, D_IN, seed=52))
+                pos = torch.from_numpy(synthetic.make_positives(pg, 5 * N, seed=53))
+                pos = pos[(pos != z).all(1)]
+                torch.manual_seed(1)
+                tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+                torch.manual_seed(2)
+                tr.model = pm.PinSageModel(g, N, 2, tr.dimensions, 200, 0.85, 5, None)
+                tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)
+                good = [_batch(64, 300 + i) for i in range(4)]
+                for b in good:
+                    assert not (b == z).any()
+                bad = _batch(64, 399)
+                bad[5, 1] = z
+                torch.manual_seed(99)
+                n_good = 2 if captured else 0  # (the first two steps: eager tune, then the capture)
+                for b in good[:n_good]:
+                    tr.train_batch(b)
+                torch.cuda.synchronize()
+                fs = tr._fused_fly if n_good else None
+
+                def state():
+                    f = tr._fused_fly
+                    return (torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu(),
+                            f.m.detach().cpu().clone(), f.v.detach().cpu().clone())
+
+                if n_good:
+                    assert fs is not None and (fs.graphs is not None) == captured
+                    before = state()
+                else:
+                    before = None
+                    snap = [p.detach().cpu().clone() for p in tr.model.parameters()]
+                tr.train_batch(bad)  # reported through the ring: no raise yet
+                tr.train_batch(good[2])  # refused too (the halt word is sticky)
+                with pytest.raises(RuntimeError, match="zero-degree"):
+                    tr._sync_state()
+                torch.cuda.synchronize()
+                after = state()
+                if before is not None:
+                    for a, b in zip(before, after):
+                        assert torch.equal(a, b)
+                else:
+                    now = [p.detach().cpu() for p in tr.model.parameters()]
+                    for a, b in zip(snap, now):
+                        assert torch.equal(a, b)
+                    assert float(after[1].abs().max()) == 0.0 and float(after[2].abs().max()) == 0.0
+                # raised: the next step updates again
+                tr.train_batch(good[3])
+                tr._sync_state()
+                torch.cuda.synchronize()
+                assert not torch.equal(state()[0], after[0])
+            finally:
+                os.chdir(cwd)
+    finally:
+        pm.set_rng_mode("mt19937")

@@ -356,3 +356,55 @@ def test_engine_on_second_device_after_first_device_engine_destroyed():
                 assert all(torch.isfinite(p.grad).all() for p in tr.model.parameters())
         finally:
             os.chdir(cwd)
+
+
+@pytest.mark.parametrize("fork", [2, 1])
+def test_step_capture_with_forked_csr_branch(fork, monkeypatch):
+    """the step graphs captured with a fork onto the
+    engine's side stream inside the frontier (PINSAGE_CSR_FORK: 2 = an empty
+    branch, 1 = layer 0's CSR transpose on side[0] beside the upper layers').
+    The fork's wait binds to an event recorded on the frontier's stream, and
+    the join is recorded on the side stream and waited on the frontier's
+    stream before engine_frontier returns -- so every captured graph (the
+    frontier graph, the step graph, and the step graph whose branch computes
+    the look-ahead frontier) ends its capture with the side stream joined.
+    Six steps (an eager first step, the capture, five replays with look-ahead
+    hits) end bitwise equal to the unforked run, and the graphs were used.
+    (tools/dbg/capture_fork_probe.cpp holds what hipStreamEndCapture does
+    with the other shapes: an unjoined fork, work created inside a capture.)"""
+    import graph
+    import pinsage_training as pt
+    import synthetic
+    pg = synthetic.make_playlist_graph(3000, 600, 20000, seed=71)
+    indptr, indices = pg.csr()
+    feats = torch.from_numpy(synthetic.make_features(3000, 128, seed=72))
+    pos = torch.from_numpy(synthetic.make_positives(pg, 15000, seed=73))
+    monkeypatch.setenv("PINSAGE_AUTOTUNE", "0")
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
+            pt.PinSage(g, 3000, feats, pos, log=False, load_save=False)  # (precompute the table once)
+
+            def run(knob):
+                monkeypatch.setenv("PINSAGE_CSR_FORK", str(knob))
+                torch.manual_seed(5)
+                tr = pt.PinSage(g, 3000, feats, pos, log=False, load_save=False)
+                tr.batch_size = 256
+                torch.manual_seed(6)
+                losses = []
+                for _ in range(6):
+                    batch, _ = tr.next_batch()
+                    losses.append(float(tr.train_batch(batch)[0]))
+                torch.cuda.synchronize()
+                f = tr._fused
+                assert f.graphs is not None and f.ahead_hits >= 3, (f.graphs, f.ahead_hits)
+                return losses, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).cpu()
+
+            l0, p0 = run(0)
+            l1, p1 = run(fork)
+            assert l0 == l1, (l0, l1)
+            assert torch.equal(p0, p1), (p0 - p1).abs().max().item()
+        finally:
+            os.chdir(cwd)

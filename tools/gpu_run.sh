@@ -1,14 +1,10 @@
 set -o pipefail
-out=gpurun_out/r5al; R=$(pwd); mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_trainer.py -x -q --timeout 300 --timeout-method thread > $out/t.log 2>&1 || { tail -n 30 $out/t.log; exit 1; }
-tail -n 1 $out/t.log
-for rep in 1 2 3 4; do for v in 0 1; do for c in c2 c4; do
-PINSAGE_WG2=$v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 --config $c > $out/b_${c}_${v}_$rep.json 2> $out/b_${c}_${v}_$rep.err || { tail $out/b_${c}_${v}_$rep.err; exit 1; }
-done; done; done
-python - <<'PY'
-import json, statistics as st
-for c in ("c2","c4"):
-  for v in (0,1):
-    ds=[json.load(open(f"gpurun_out/r5al/b_{c}_{v}_{r}.json")) for r in (1,2,3,4)]
-    print("wg2", c, v, "median %.4f" % st.median([d["ms_per_step"] for d in ds]), ["%.4f" % d["ms_per_step"] for d in ds])
-PY
+out=gpurun_out/r6b; mkdir -p $out
+timeout -k 10 60 ./tools/dbg/capture_fork_probe > $out/capture_probe.log 2>&1; echo "probe rc $?"; cat $out/capture_probe.log | grep -E "end capture|replay|CHILD|child|create|memcpy"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fly_fused.py tests/test_gpu_trainer.py -x -v --timeout 200 --timeout-method thread -k "refuses or forked" > $out/t1.log 2>&1 || { tail -60 $out/t1.log; exit 1; }
+grep -E "PASS|FAIL" $out/t1.log | tail
+timeout -k 10 600 python -u -m pytest tests/test_gpu_c5.py -x -v -s --timeout 500 --timeout-method thread > $out/c5.log 2>&1 || { tail -60 $out/c5.log; exit 1; }
+grep -E "PASS|FAIL|passed|failed" $out/c5.log | tail -3
+timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_micro.py tests/test_gpu_dashboard.py tests/test_gpu_fly.py -x -q -s --timeout 300 --timeout-method thread > $out/norm.log 2>&1 || { tail -60 $out/norm.log; exit 1; }
+tail -1 $out/norm.log
+grep -o "'grad_normrel_B_max': [0-9.e-]*" $out/norm.log | sort -t: -k2 -g | tail -3
