@@ -82,6 +82,10 @@ _SIGS = {
     "pinsage_frontier_step": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp, vp]),
     "pinsage_frontier_local_idx": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "pinsage_linear": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, ctypes.c_int, vp, i64, vp]),
+    "pinsage_wgrad_scratch_bytes": (i64, [i64, i64]),
+    "pinsage_wgrad": (ctypes.c_int, [i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp,
+                                     ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_float, vp]),
     "pinsage_gemm_ex": (ctypes.c_int, [i64, i64, i64, ctypes.c_int, ctypes.c_int, vp, i64, vp, vp, i64,
                                        vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, vp]),
@@ -136,8 +140,8 @@ _SIGS = {
     "pinsage_engine_backward": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_reset_backward": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_backward_stage": (ctypes.c_int, [vp, vp, ctypes.c_int, vp]),
-    "pinsage_engine_adam": (ctypes.c_int, [vp, vp, f32, f32, f32, vp]),
-    "pinsage_engine_backward_adam": (ctypes.c_int, [vp, vp, vp, f32, f32, f32, vp]),
+    "pinsage_engine_adam": (ctypes.c_int, [vp, vp, ctypes.c_double, ctypes.c_double, f32, vp]),
+    "pinsage_engine_backward_adam": (ctypes.c_int, [vp, vp, vp, ctypes.c_double, ctypes.c_double, f32, vp]),
     "pinsage_engine_read_counts": (ctypes.c_int, [vp, vp, vp, vp, vp]),
     "pinsage_engine_set_hints": (ctypes.c_int, [vp, vp, vp]),
     "pinsage_engine_timing": (ctypes.c_int, [vp, ctypes.c_int]),

@@ -11,6 +11,7 @@
 #include "../../include/pinsage_hip.h"
 #include "common.h"
 #include "gemm.h"
+#include "wgrad.h"
 #include "mt19937.h"
 
 namespace ps {
@@ -505,6 +506,58 @@ int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M,
   p.bias = bias;
   p.act = act != 0;
   return launch_gemm(p, (hipStream_t)stream);
+}
+
+int64_t pinsage_wgrad_scratch_bytes(int64_t M, int64_t N) {
+  if (M <= 0 || N <= 0) return 0;
+  return align_up(wgrad_kw_tickets((int)M, (int)N) * 4, 256) + wgrad_kw_slab_floats((int)M, (int)N) * 4 +
+         wgrad_kw_bslab_floats((int)M) * 4;
+}
+
+int pinsage_wgrad(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const float* A, int64_t lda,
+                  const float* B, int64_t ldb, const int32_t* b_idx, int64_t N1, const float* B2, int64_t ldb2,
+                  float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, float* adam_p,
+                  float* adam_m, float* adam_v, float* adam_pb, float* adam_mb, float* adam_vb,
+                  const float* coef, double beta1, double beta2, float eps, void* stream) {
+  PS_REQUIRE(M > 0 && N > 0 && M <= INT32_MAX && N <= INT32_MAX && K_max >= 0 && K_max <= INT32_MAX &&
+                 splits >= 0 && scratch,
+             kErrArg, "wgrad: bad argument");
+  KwParams p;
+  p.A = A;
+  p.lda = lda;
+  p.M = (int)M;
+  p.B = B;
+  p.ldb = ldb;
+  p.b_idx = b_idx;
+  p.N1 = B2 ? (int)N1 : -1;
+  p.B2 = B2;
+  p.ldb2 = ldb2;
+  p.N = (int)N;
+  p.K_dev = K_dev;
+  p.K_max = (int)K_max;
+  p.dst = dst;
+  p.ld_dst = ld_dst;
+  p.dst_b = dst_b;
+  if (adam_p) {
+    p.ad.p = adam_p;
+    p.ad.m = adam_m;
+    p.ad.v = adam_v;
+    p.ad.pb = adam_pb;
+    p.ad.mb = adam_mb;
+    p.ad.vb = adam_vb;
+    p.ad.coef = coef;
+    p.ad.beta1 = beta1;
+    p.ad.beta2 = beta2;
+    p.ad.eps = eps;
+  }
+  char* sc = static_cast<char*>(scratch);
+  p.cnt = reinterpret_cast<int*>(sc);
+  sc += align_up(wgrad_kw_tickets((int)M, (int)N) * 4, 256);
+  p.slab = reinterpret_cast<float*>(sc);
+  sc += wgrad_kw_slab_floats((int)M, (int)N) * 4;
+  p.bslab = reinterpret_cast<float*>(sc);
+  p.S = splits;
+  return launch_wgrad_kw(p, (hipStream_t)stream);
 }
 
 int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor, const float* A,

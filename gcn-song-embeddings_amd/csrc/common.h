@@ -60,7 +60,10 @@ struct AdamSlice {
   float* mb = nullptr;
   float* vb = nullptr;
   const float* coef = nullptr;
-  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f;
+  // betas as torch holds them (Python floats): 1 - beta is formed in double
+  // and rounded once, as torch rounds its `value=1 - beta2` / lerp weight
+  double beta1 = 0.9, beta2 = 0.999;
+  float eps = 1e-8f;
 };
 
 // ---------------------------------------------------------------- device helpers

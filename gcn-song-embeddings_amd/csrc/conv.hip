@@ -1537,13 +1537,12 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, flo
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int64_t n, const float* __restrict__ coef,
-                                                   float beta1, float beta2, float eps) {
+                                                   float beta2, float omb1, float omb2, float eps) {
   const float ss = coef[0], bc2 = coef[1];
   // bc2 = sqrt(1 - beta2^t) > 0 on every real step; 0 marks a step the device
   // refused (the on-the-fly sampler's error words, pinsage_fly_gate_adam):
   // parameters and moments stay untouched, as when the reference raises
   if (!(bc2 > 0.f)) return;
-  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
   const int64_t n4 = n >> 2;
   float4* p4 = reinterpret_cast<float4*>(p);
   float4* m4 = reinterpret_cast<float4*>(m);
@@ -1644,8 +1643,8 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
   if (ad.coef) {
     ss = ad.coef[0];
     bc2 = ad.coef[1];
-    omb1 = (float)(1.0 - (double)ad.beta1);
-    omb2 = (float)(1.0 - (double)ad.beta2);
+    omb1 = (float)(1.0 - ad.beta1);
+    omb2 = (float)(1.0 - ad.beta2);
   }
   if ((int)blockIdx.x < nb_main) {
     const int64_t e4 = (int64_t)blockIdx.x * 64 + j;  // float4 index into [M][N]
@@ -1683,10 +1682,10 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
         float4 pp = *reinterpret_cast<const float4*>(ad.p + o);
         float4 mm = *reinterpret_cast<const float4*>(ad.m + o);
         float4 vv = *reinterpret_cast<const float4*>(ad.v + o);
-        adam1(pp.x, r.x, mm.x, vv.x, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
-        adam1(pp.y, r.y, mm.y, vv.y, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
-        adam1(pp.z, r.z, mm.z, vv.z, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
-        adam1(pp.w, r.w, mm.w, vv.w, ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.x, r.x, mm.x, vv.x, ss, bc2, (float)ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.y, r.y, mm.y, vv.y, ss, bc2, (float)ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.z, r.z, mm.z, vv.z, ss, bc2, (float)ad.beta2, omb1, omb2, ad.eps);
+        adam1(pp.w, r.w, mm.w, vv.w, ss, bc2, (float)ad.beta2, omb1, omb2, ad.eps);
         *reinterpret_cast<float4*>(ad.p + o) = pp;
         *reinterpret_cast<float4*>(ad.m + o) = mm;
         *reinterpret_cast<float4*>(ad.v + o) = vv;
@@ -1705,7 +1704,7 @@ __global__ __launch_bounds__(256) void reduce_slabs_2d_kernel(const float* __res
   if (g == 0 && m < M) {
     const float r = (redf[j] + redf[64 + j]) + (redf[128 + j] + redf[192 + j]);
     bias_out[m] = r;
-    if (ad.pb && bc2 > 0.f) adam1(ad.pb[m], r, ad.mb[m], ad.vb[m], ss, bc2, ad.beta2, omb1, omb2, ad.eps);
+    if (ad.pb && bc2 > 0.f) adam1(ad.pb[m], r, ad.mb[m], ad.vb[m], ss, bc2, (float)ad.beta2, omb1, omb2, ad.eps);
   }
 }
 
@@ -2091,12 +2090,12 @@ int launch_loss_monitor(const float* part, int nparts, const float* colpart, int
 }
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const float* coef,
-                float beta1, float beta2, float eps, hipStream_t st) {
+                double beta1, double beta2, float eps, hipStream_t st) {
   PS_REQUIRE(((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
                reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0,
              kErrArg, "adam: buffers must be 16-byte aligned");
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4, 256, 2048)), dim3(256), 0, st, p, g, m,
-                     v, n, coef, beta1, beta2, eps);
+                     v, n, coef, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), eps);
   PS_CHECK_LAUNCH();
   return kOk;
 }

@@ -27,6 +27,7 @@
 #include "common.h"
 #include "conv.h"
 #include "gemm.h"
+#include "wgrad.h"
 
 namespace ps {
 
@@ -64,7 +65,7 @@ int launch_loss(const float*, int, const int32_t*, int, float, const float*, int
                 float*, bool, bool, const int*, const int32_t*, float*, hipStream_t);
 int launch_pos_csr(const int32_t*, int64_t, const int*, int*, int32_t*, hipStream_t);
 int launch_loss_monitor(const float*, int, const float*, int, int, float*, hipStream_t);
-int launch_adam(float*, const float*, float*, float*, int64_t, const float*, float, float, float,
+int launch_adam(float*, const float*, float*, float*, int64_t, const float*, double, double, float,
                 hipStream_t);
 int csr_prepare();
 int launch_reduce_slabs_2d(const float*, int, int64_t, int, int, float*, int64_t, const float*,
@@ -171,6 +172,13 @@ struct Engine {
   // engine_frontier returns, so no engine call leaves a side stream unjoined
   // inside a caller's capture (tests/test_gpu_trainer.py)
   int csr_fork = getenv("PINSAGE_CSR_FORK") ? atoi(getenv("PINSAGE_CSR_FORK")) : 0;
+  // which side stream the frontier forks: 2 (default, its own), or 0 (the
+  // backward's side[0]: the round-5 shape, kept for tools/dbg reproduction)
+  int csr_fork_stream = getenv("PINSAGE_CSR_FORK_STREAM") ? atoi(getenv("PINSAGE_CSR_FORK_STREAM")) : 2;
+  // PINSAGE_WGRAD_KW: weight gradients by the long-K kernel (wgrad.hip: 64 x 64
+  // tiles, few splits combined inside the launch, Adam fused) instead of the
+  // split-K GEMM + reduce_slabs_2d; 1 (default) every site it supports, 0 none
+  int wgrad_kw = getenv("PINSAGE_WGRAD_KW") ? atoi(getenv("PINSAGE_WGRAD_KW")) : 1;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -206,6 +214,9 @@ struct Engine {
   // stream-K scratch of the main stream's GEMMs (gemm.h)
   size_t sk_slab = 0, sk_cnt = 0;
   int64_t sk_cnt_len = 0;
+  // long-K weight gradients' split tickets (wgrad.hip), per stream
+  size_t kw_cnt_main = 0, kw_cnt_side = 0;
+  int64_t kw_cnt_len = 0;
   size_t total = 0;
   int64_t max_bsum_blocks = 0;
   // external device pointers (owned by the caller)
@@ -220,7 +231,10 @@ struct Engine {
   float* adam_v = nullptr;
   // backward side streams: [0] transposes (CSR) of the neighbour slots, [1]
   // weight gradients; forked from / joined to the caller's stream with events
-  hipStream_t side[2] = {nullptr, nullptr};
+  // [2]: the frontier's own fork (engine_frontier, PINSAGE_CSR_FORK): never
+  // forked by the backward, so a step graph whose look-ahead branch holds the
+  // next frontier does not fork one stream from two parallel branches
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
   int side_dev = 0;  // the device side[] and ev were created on (the retired pool's key)
   std::vector<hipEvent_t> ev;
   int ev_next = 0;
@@ -508,6 +522,9 @@ static void layout(Engine& E) {
     E.sk_cnt_len = ceil_div(max_rows, 32) * ceil_div(max_cols, 128);
     E.sk_cnt = carve(cur, E.sk_cnt_len * 4);
     E.sk_slab = carve(cur, gemm_sk_slab_floats() * 4);
+    E.kw_cnt_len = (int64_t)ceil_div(std::max(c.hid, c.out), 64) * ceil_div(max_cols, 64);
+    E.kw_cnt_main = carve(cur, E.kw_cnt_len * 4);
+    E.kw_cnt_side = carve(cur, E.kw_cnt_len * 4);
   }
   E.total = (size_t)align_up((int64_t)cur, 256);
 }
@@ -633,7 +650,7 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
   hipStream_t s_fk = st;
   if (E.csr_fork) {
     PS_TRY(ensure_streams(E));
-    s_fk = E.side[0];
+    s_fk = E.side[std::min(std::max(E.csr_fork_stream, 0), 2)];
     PS_TRY(dep(E, st, s_fk));
   }
   for (int l = Lc - 1; l >= 0; --l) {
@@ -836,7 +853,8 @@ struct WGrad {
 // Adam applied by the gradient reductions (pinsage_engine_backward_adam)
 struct AdamStep {
   const float* coef;
-  float beta1, beta2, eps;
+  double beta1, beta2;
+  float eps;
 };
 
 // Adam slice of the parameter at flat offsets (w_off, b_off); b_off < 0: none
@@ -866,6 +884,37 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
                        bool main = false, bool beside = false) {
   float* const slab = at<float>(ws, main ? E.slab_main : E.slab);
   float* const bslab = at<float>(ws, main ? E.bslab_main : E.bslab);
+  if (E.wgrad_kw && wgrad_kw_supported(w.M, w.N, w.N1, w.B2 != nullptr) &&
+      (int64_t)(w.M / 64) * (w.N / 64) <= E.kw_cnt_len) {
+    // the long-K kernel: splits combined in the launch, Adam fused (no
+    // reduce_slabs_2d launch, no slab round trip through a second kernel)
+    KwParams k;
+    k.A = w.A;
+    k.lda = w.lda;
+    k.M = w.M;
+    k.B = w.B;
+    k.ldb = w.ldb;
+    k.b_idx = w.b_idx;
+    if (w.B2) {
+      k.N1 = w.N1;
+      k.B2 = w.B2;
+      k.ldb2 = w.ldb2;
+    }
+    k.N = w.N;
+    k.K_dev = w.K_dev;
+    k.K_max = (int)w.K_max;
+    k.dst = w.dst;
+    k.ld_dst = w.ld_dst;
+    k.dst_b = w.dst_b;
+    if (adam) k.ad = *adam;
+    k.slab = slab;
+    k.bslab = bslab;
+    k.cnt = at<int>(ws, main ? E.kw_cnt_main : E.kw_cnt_side);
+    k.S = wgrad_kw_splits(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max);
+    PS_REQUIRE((int64_t)k.S * w.M * w.N <= E.slab_floats, kErrWorkspace, "engine: wgrad slab too small");
+    if (adam && after_use) PS_CHECK_HIP(hipStreamWaitEvent(st, after_use, 0));
+    return launch_wgrad_kw(k, st);
+  }
   int cfg = 0, S = 1;
   // (a side-stream target of 256 workgroups measured faster at C2 and slower
   // at C4, 128 slower, and a grid cap on side launches even or slower: one
@@ -1201,6 +1250,8 @@ int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
   for (auto& lb : E.L)
     PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, lb.cnt), 0, (size_t)(lb.N.cap + 1) * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.sk_cnt), 0, (size_t)E.sk_cnt_len * 4, st));
+  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.kw_cnt_main), 0, (size_t)E.kw_cnt_len * 4, st));
+  PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.kw_cnt_side), 0, (size_t)E.kw_cnt_len * 4, st));
   return kOk;
 }
 
@@ -1555,8 +1606,8 @@ int pinsage_engine_backward_stage(pinsage_engine* e, void* ws, int stage, void* 
   return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream, nullptr, stage);
 }
 
-int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, float beta1,
-                                 float beta2, float eps, void* stream) {
+int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, double beta1,
+                                 double beta2, float eps, void* stream) {
   if (!coef) {
     set_error("engine_backward_adam: null coefficients");
     return kErrArg;
@@ -1565,7 +1616,7 @@ int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef,
   return engine_backward(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream, &a);
 }
 
-int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,
+int pinsage_engine_adam(pinsage_engine* e, const float* coef, double beta1, double beta2, float eps,
                         void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
   PS_TRY(run_pend(*E));

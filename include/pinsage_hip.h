@@ -225,6 +225,23 @@ int pinsage_linear(const float* A, int64_t lda, const int32_t* a_idx, int64_t M,
  * stream_k -1 chooses by size, 0 disables, 1 forces the stream-K schedule
  * (in-launch combine of tiles cut between workgroups; scratch is owned by
  * the library). */
+/* Weight gradient of an nn.Linear weight over a device-side row count
+ * (the AddmmBackward of pinsage_model.py:196-201 / 208-210):
+ *   dst[M][N] = A^T [B || B2]  (A [K][M] row-major; B rows gathered by b_idx
+ *   when set, columns >= N1 from B2 -- torch.cat along N), dst_b[M] = column
+ *   sums of A (nullable), K = *K_dev (nullable: K_max rows).  Long-K form
+ *   (wgrad.hip): 64 x 64 tiles, K cut into `splits` runs (0: by size) that
+ *   are combined inside the launch in a fixed order (deterministic); with
+ *   adam_p set, torch.optim.Adam is applied to the slice (adam_* pointers in
+ *   dst's layout, coef = {lr / (1 - b1^t), sqrt(1 - b2^t)} on the device).
+ *   M, N, N1 multiples of 64.  scratch: pinsage_wgrad_scratch_bytes(M, N)
+ *   bytes, zeroed once before the first call (its tickets reset themselves). */
+int64_t pinsage_wgrad_scratch_bytes(int64_t M, int64_t N);
+int pinsage_wgrad(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const float* A, int64_t lda,
+                  const float* B, int64_t ldb, const int32_t* b_idx, int64_t N1, const float* B2, int64_t ldb2,
+                  float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, float* adam_p,
+                  float* adam_m, float* adam_v, float* adam_pb, float* adam_mb, float* adam_vb,
+                  const float* coef, double beta1, double beta2, float eps, void* stream);
 int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor, const float* A,
                     int64_t lda, const int32_t* a_idx, const float* B, int64_t ldb,
                     const int32_t* b_idx, float* C, int64_t ldc, const float* bias, int act,
@@ -506,15 +523,15 @@ int pinsage_engine_backward_stage(pinsage_engine* e, void* ws, int stage, void* 
  * coef: device f32[2] = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} for this step
  * t, computed by the caller in double as torch does (kept in device memory so
  * a captured step graph picks up each step's values). */
-int pinsage_engine_adam(pinsage_engine* e, const float* coef, float beta1, float beta2, float eps,
+int pinsage_engine_adam(pinsage_engine* e, const float* coef, double beta1, double beta2, float eps,
                         void* stream);
 /* backward followed by that Adam step, scheduled off the critical path: the
  * last gradient (layer 0's Q) applies its own Adam step in the reduction that
  * produces it, and every other parameter is updated beside that reduction.
  * Gradients are still written to the grad buffer; the arithmetic is that of
  * pinsage_engine_backward + pinsage_engine_adam. */
-int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, float beta1,
-                                 float beta2, float eps, void* stream);
+int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef, double beta1,
+                                 double beta2, float eps, void* stream);
 
 /* Frontier sizes of the last forward in ws (synchronises the stream): S[l] =
  * |S_l| (nodes convolved at layer l), N[l] = |N_l| (distinct neighbours). */

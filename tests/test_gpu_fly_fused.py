@@ -179,7 +179,6 @@ def test_fused_fly_step_refuses_update_after_sampling_error(captured, monkeypatc
     import graph
     import pinsage_model as pm
     import pinsage_training as pt
-    import synthetic
     pm.set_rng_mode("philox")
     monkeypatch.setenv("PINSAGE_FLY_FUSED", "1")
     try:
@@ -187,15 +186,15 @@ def test_fused_fly_step_refuses_update_after_sampling_error(captured, monkeypatc
             cwd = os.getcwd()
             os.chdir(tmp)
             try:
-                pg = synthetic.make_playlist_graph(N, 750, 40000, seed=51)
+                pg, g0, feats, pos = _problem(tmp)
                 z = 17
                 indptr, indices = _drop_track(*pg.csr(), z)
-                g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb.pt"))
-                feats = torch.from_numpy(synthetic.make_features(N, D_IN, seed=52))
-                pos = torch.from_numpy(synthetic.make_positives(pg, 5 * N, seed=53))
+                g = graph.CSRGraph.from_csr(indptr, indices, base_dir=tmp, nbhds_path=os.path.join(tmp, "nb2.pt"))
                 pos = pos[(pos != z).all(1)]
                 torch.manual_seed(1)
-                tr = pt.PinSage(g, N, feats, pos, log=False, load_save=False)
+                # (the trainer's precomputed table comes from the intact graph: the
+                # reference's precompute would itself raise on the zero-degree track)
+                tr = pt.PinSage(g0, N, feats, pos, log=False, load_save=False)
                 torch.manual_seed(2)
                 tr.model = pm.PinSageModel(g, N, 2, tr.dimensions, 200, 0.85, 5, None)
                 tr.optimizer = torch.optim.Adam(tr.model.parameters(), lr=tr.lr)

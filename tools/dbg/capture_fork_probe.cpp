@@ -8,6 +8,10 @@
 //   unjoined_empty fork only (B holds no node), end capture
 //   create_inside create a stream and an event while A captures (global mode)
 //   err_then_end  a failing call inside the capture (invalidates it), then end
+//   reuse_after_unjoined_empty  an unjoined empty fork of B, end capture (HIP
+//                 accepts it), then a second capture that forks B again and
+//                 joins it properly, then an eager launch on B
+//   reuse_after_joined  the same with the first fork joined (control)
 // Build: hipcc --offload-arch=gfx950 -O1 -o capture_fork_probe capture_fork_probe.cpp
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
@@ -19,7 +23,116 @@
 
 __global__ void tick(int* p) { if (threadIdx.x == 0) p[0] += 1; }
 
+static int run_reuse(const std::string& c) {
+  int* d = nullptr;
+  if (hipMalloc(&d, 64) != hipSuccess) return 90;
+  hipMemset(d, 0, 64);
+  hipStream_t A, B;
+  hipStreamCreateWithFlags(&A, hipStreamNonBlocking);
+  hipStreamCreateWithFlags(&B, hipStreamNonBlocking);
+  hipEvent_t e1, e2;
+  hipEventCreateWithFlags(&e1, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e2, hipEventDisableTiming);
+  const bool join1 = c == "reuse_after_joined";
+  for (int cap = 0; cap < 2; ++cap) {
+    hipGraph_t g = nullptr;
+    hipError_t r = hipStreamBeginCapture(A, hipStreamCaptureModeGlobal);
+    printf("[%s] capture %d begin %s\n", c.c_str(), cap, hipGetErrorName(r));
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    r = hipEventRecord(e1, A);
+    printf("[%s] capture %d record %s\n", c.c_str(), cap, hipGetErrorName(r));
+    r = hipStreamWaitEvent(B, e1, 0);
+    printf("[%s] capture %d wait %s\n", c.c_str(), cap, hipGetErrorName(r));
+    if (cap == 1) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, B, d + 4);
+    if (cap == 1 || join1) {
+      r = hipEventRecord(e2, B);
+      printf("[%s] capture %d join record %s\n", c.c_str(), cap, hipGetErrorName(r));
+      r = hipStreamWaitEvent(A, e2, 0);
+      printf("[%s] capture %d join wait %s\n", c.c_str(), cap, hipGetErrorName(r));
+    }
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    fflush(stdout);
+    r = hipStreamEndCapture(A, &g);
+    printf("[%s] capture %d end %s graph %p\n", c.c_str(), cap, hipGetErrorName(r), (void*)g);
+    fflush(stdout);
+    if (r == hipSuccess && g) {
+      hipGraphExec_t x;
+      r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+      if (r == hipSuccess) r = hipGraphLaunch(x, A);
+      r = hipStreamSynchronize(A);
+      printf("[%s] capture %d replay %s\n", c.c_str(), cap, hipGetErrorName(r));
+    }
+  }
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, B, d + 8);
+  hipError_t r = hipStreamSynchronize(B);
+  int hv[16];
+  hipMemcpy(hv, d, 64, hipMemcpyDeviceToHost);
+  printf("[%s] eager on B %s counters A %d B-captured %d B-eager %d\n", c.c_str(), hipGetErrorName(r), hv[0], hv[4],
+         hv[8]);
+  fflush(stdout);
+  return 0;
+}
+
+// The shape of the trainer's look-ahead step graph (pinsage_training
+// _capture_graphs, graph `ga`): the origin stream A forks a branch S (the
+// next batch's frontier); inside that branch the engine forks its side stream
+// B off S and joins it back into S (nested_*: B empty or with a kernel); then
+// the main chain on A forks the SAME side stream B again (the backward's
+// monitors / weight gradients) and joins it into A; S is joined into A last.
+// nested_separate: the branch's fork uses a third stream C instead of B.
+static int run_nested(const std::string& c) {
+  int* d = nullptr;
+  if (hipMalloc(&d, 64) != hipSuccess) return 90;
+  hipMemset(d, 0, 64);
+  hipStream_t A, S, B, C;
+  for (hipStream_t* x : {&A, &S, &B, &C}) hipStreamCreateWithFlags(x, hipStreamNonBlocking);
+  hipEvent_t e[8];
+  for (auto& x : e) hipEventCreateWithFlags(&x, hipEventDisableTiming);
+  hipStream_t F = c == "nested_separate" ? C : B;  // the stream the branch forks
+  hipGraph_t g = nullptr;
+  hipError_t r = hipStreamBeginCapture(A, hipStreamCaptureModeGlobal);
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+  hipEventRecord(e[0], A);
+  hipStreamWaitEvent(S, e[0], 0);                 // branch S off A
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, S, d + 4);
+  hipEventRecord(e[1], S);
+  r = hipStreamWaitEvent(F, e[1], 0);             // F off S
+  printf("[%s] fork F off S %s\n", c.c_str(), hipGetErrorName(r));
+  if (c != "nested_empty") hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, F, d + 8);
+  hipEventRecord(e[2], F);
+  r = hipStreamWaitEvent(S, e[2], 0);             // F joined into S
+  printf("[%s] join F into S %s\n", c.c_str(), hipGetErrorName(r));
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, S, d + 4);
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+  hipEventRecord(e[3], A);
+  r = hipStreamWaitEvent(B, e[3], 0);             // B off A (again, for nested_*)
+  printf("[%s] fork B off A %s\n", c.c_str(), hipGetErrorName(r));
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, B, d + 12);
+  hipEventRecord(e[4], B);
+  hipStreamWaitEvent(A, e[4], 0);                 // B joined into A
+  hipEventRecord(e[5], S);
+  hipStreamWaitEvent(A, e[5], 0);                 // S joined into A
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+  fflush(stdout);
+  r = hipStreamEndCapture(A, &g);
+  printf("[%s] end capture %s graph %p\n", c.c_str(), hipGetErrorName(r), (void*)g);
+  fflush(stdout);
+  if (r == hipSuccess && g) {
+    hipGraphExec_t x;
+    r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (r == hipSuccess) r = hipGraphLaunch(x, A);
+    hipStreamSynchronize(A);
+    int h[16];
+    hipMemcpy(h, d, 64, hipMemcpyDeviceToHost);
+    printf("[%s] replay %s counters A %d S %d F %d B %d\n", c.c_str(), hipGetErrorName(r), h[0], h[4], h[8], h[12]);
+  }
+  fflush(stdout);
+  return 0;
+}
+
 static int run_case(const std::string& c) {
+  if (c.rfind("nested", 0) == 0) return run_nested(c);
+  if (c.rfind("reuse", 0) == 0) return run_reuse(c);
   int* d = nullptr;
   if (hipMalloc(&d, 64) != hipSuccess) return 90;
   hipStream_t A, B;
@@ -78,7 +191,10 @@ static int run_case(const std::string& c) {
 }
 
 int main(int argc, char** argv) {
-  const char* cases[] = {"joined", "joined_empty", "unjoined", "unjoined_empty", "create_inside", "err_then_end"};
+  const char* cases[] = {"joined",        "joined_empty", "unjoined",
+                         "unjoined_empty", "create_inside", "err_then_end",
+                         "reuse_after_joined", "reuse_after_unjoined_empty",
+                         "nested_separate", "nested_kernel", "nested_empty"};
   if (argc > 1) return run_case(argv[1]);
   for (const char* c : cases) {
     fflush(stdout);

@@ -1,10 +1,10 @@
 set -o pipefail
-out=gpurun_out/r6b; mkdir -p $out
-timeout -k 10 60 ./tools/dbg/capture_fork_probe > $out/capture_probe.log 2>&1; echo "probe rc $?"; cat $out/capture_probe.log | grep -E "end capture|replay|CHILD|child|create|memcpy"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fly_fused.py tests/test_gpu_trainer.py -x -v --timeout 200 --timeout-method thread -k "refuses or forked" > $out/t1.log 2>&1 || { tail -60 $out/t1.log; exit 1; }
-grep -E "PASS|FAIL" $out/t1.log | tail
-timeout -k 10 600 python -u -m pytest tests/test_gpu_c5.py -x -v -s --timeout 500 --timeout-method thread > $out/c5.log 2>&1 || { tail -60 $out/c5.log; exit 1; }
-grep -E "PASS|FAIL|passed|failed" $out/c5.log | tail -3
-timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_micro.py tests/test_gpu_dashboard.py tests/test_gpu_fly.py -x -q -s --timeout 300 --timeout-method thread > $out/norm.log 2>&1 || { tail -60 $out/norm.log; exit 1; }
-tail -1 $out/norm.log
-grep -o "'grad_normrel_B_max': [0-9.e-]*" $out/norm.log | sort -t: -k2 -g | tail -3
+out=gpurun_out/r6c; mkdir -p $out
+timeout -k 10 120 ./tools/dbg/capture_fork_probe > $out/capture_probe.log 2>&1; echo "probe rc $?"; grep -E "end|replay|CHILD|child|eager" $out/capture_probe.log | grep reuse
+timeout -k 10 600 python -u -m pytest tests/test_gpu_wgrad.py tests/test_gpu_fly_fused.py tests/test_gpu_trainer.py -x -v --timeout 200 --timeout-method thread -k "wgrad or refuses or forked" > $out/t1.log 2>&1 || { tail -60 $out/t1.log; exit 1; }
+grep -cE "PASSED" $out/t1.log; grep -E "FAIL" $out/t1.log | head
+for rep in 1 2; do for v in "0 0" "1 0" "1 1"; do set -- $v; for c in c2 c4; do
+PINSAGE_WGRAD_KW=$1 PINSAGE_DQ_CHUNK_ROWS=$2 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 --config $c > $out/b_${c}_$1$2_$rep.json 2> $out/b_${c}_$1$2_$rep.err || { tail $out/b_${c}_$1$2_$rep.err; exit 1; }
+echo "kw=$1 cr=$2 $(python tools/bench_summary.py $out/b_${c}_$1$2_$rep.json)"
+done; done; done
+bash tools/prof_timeline.sh $out c2 || exit 1

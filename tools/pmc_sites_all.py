@@ -25,6 +25,10 @@ def occurrences(trace, kernel, grid):
 
 
 def algo(bench, site):
+    for key in ("roofline", "roofline_other"):  # (round 6: the bench line names both launches)
+        r = bench.get(key) or {}
+        if r.get("kernel", "").startswith(site):
+            return r["algorithmic_bytes_per_launch"]
     if site == "fwd.q_gemm.l0":
         return bench["roofline"]["algorithmic_bytes_per_launch"]
     if site == "fwd.aggw.l0":

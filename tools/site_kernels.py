@@ -7,7 +7,10 @@ eagerly behind a stream hold, after the timed graph replays):
 fwd.q_gemm.l0 = the step's first gemm_f32_kernel<true, true, ...> (gathered
 rows x Q^T), fwd.aggw.l0 = its first agg_w*_kernel, bwd.q_wgrad.l0 = the last
 gemm_f32_kernel<false, false, ...> before the publish kernel (dQ0 closes the
-backward on the main stream, pinsage engine_backward)."""
+backward on the main stream, pinsage engine_backward); with the long-K weight
+gradients (wgrad.hip) it is the first wgrad_kw_kernel on the main queue after
+that queue's last dq kernel (the side stream runs wgrad_kw_kernel launches of
+the same grid for the other weights)."""
 import csv
 import json
 import sys
@@ -34,6 +37,13 @@ def main(path):
             out["fwd.aggw.l0"] = rec(r)
         if "gemm_f32_kernel<false, false" in n:
             out["bwd.q_wgrad.l0"] = rec(r)
+    dq = [i for i, r in enumerate(step) if "dq_combine_kernel" in r["Kernel_Name"] or "dq_chunk_kernel" in r["Kernel_Name"]]
+    if dq:
+        q = step[dq[-1]]["Queue_Id"] if "Queue_Id" in step[dq[-1]] else None
+        for r in step[dq[-1] + 1:]:
+            if "wgrad_kw_kernel" in r["Kernel_Name"] and (q is None or r.get("Queue_Id") == q):
+                out["bwd.q_wgrad.l0"] = rec(r)
+                break
     print(json.dumps(out, indent=1))
 
 
