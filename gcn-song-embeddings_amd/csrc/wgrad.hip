@@ -30,6 +30,7 @@
 #include "wgrad.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "bf16split.h"
 #include "lds_dma.h"
@@ -38,23 +39,32 @@ namespace ps {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kKwWaves = 8;
 constexpr int kKwBK = 16;                     // k-rows per stage
 constexpr int kKwT = 64;                      // tile edge (M and N)
 constexpr int kKwImg = kKwBK * kKwT;          // floats per operand image
-constexpr int kKwStage = 2 * kKwImg;          // A + B
-constexpr int kKwRing = kKwWaves * 2 * kKwStage;  // two stages per wave: 32768 floats (128 KiB)
+constexpr int kKwStage = 2 * kKwImg;          // A + B (8 KiB)
+constexpr int kKwRing = 32768;                // ring floats (128 KiB): NW waves x NS stages
 constexpr int kKwWin = 6144;                  // gathered row numbers staged per pass (24 KiB)
 constexpr int kKwMaxSplits = 16;
-static_assert(kKwRing >= kKwWaves * kKwT * kKwT, "the wave partials reuse the ring");
 
-// lane l of a 1-KiB DMA covers row 4 j + l / 16 of a stage, columns 4 (l % 16) ..
+// four k-rows of one column of a [16][64] stage image
 __device__ __forceinline__ float4 kw_frag(const float* img, int col, int k4) {
   return make_float4(img[(k4 + 0) * kKwT + col], img[(k4 + 1) * kKwT + col], img[(k4 + 2) * kKwT + col],
                      img[(k4 + 3) * kKwT + col]);
 }
 
-__global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
+// NW waves, each with an NS-stage private ring (NW * NS * 8 KiB = 128 KiB):
+// (8, 2) two waves per SIMD, one stage in flight per wave; (4, 4) one wave per
+// SIMD, three stages in flight.  GATHER: B rows come through the staged row
+// numbers (the identity for an ungathered segment), so no DMA branches.
+// PROBE (timing diagnostics only, tools/wgrad_bench.py; results are wrong):
+// 1 = the DMAs without the products, 2 = the products without the DMAs
+template <int NW, int NS, bool GATHER, int PROBE = 0>
+__global__ __launch_bounds__(NW * 64, 1) void wgrad_kw_kernel(KwParams p) {
+  static_assert(NW * NS * kKwStage == kKwRing, "ring size");
+  static_assert(kKwRing >= NW * kKwT * kKwT, "the wave partials reuse the ring");
+  constexpr int NT = NW * 64;
+  constexpr int E4 = kKwT * kKwT / 4 / NT;  // float4s of the tile per thread
   __shared__ __attribute__((aligned(16))) float smem[kKwRing + kKwWin];
   int* const sidx = reinterpret_cast<int*>(smem + kKwRing);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -82,7 +92,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
   const int bc0 = seg2 ? n0 - p.N1 : n0;
   const bool do_bias = p.dst_b && nb == 0;
   const unsigned smem_lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)smem);
-  const unsigned ring_w = smem_lds + (unsigned)(wave * 2 * kKwStage) * 4u;  // this wave's two stages
+  const unsigned ring_w = smem_lds + (unsigned)(wave * NS * kKwStage) * 4u;  // this wave's stages
   // this lane's DMA column chunk and row within each 1-KiB group
   const int dc = 4 * (lane & 15), dr = lane >> 4;
 
@@ -97,33 +107,53 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
 
   for (int pb = kb; pb < ke; pb += kKwWin) {
     const int pe = min(ke, pb + kKwWin);
-    if (bidx) {
-      for (int i = tid; i < pe - pb; i += 512) sidx[i] = bidx[pb + i];
+    if constexpr (GATHER) {
+      for (int i = tid; i < pe - pb; i += NT) sidx[i] = bidx ? bidx[pb + i] : pb + i;
       __syncthreads();
     }
     const int ns = (pe - pb + kKwBK - 1) / kKwBK;  // stages of this pass
-    const int nw = ns > wave ? (ns - wave + kKwWaves - 1) / kKwWaves : 0;  // this wave's
-    // stage it of this wave: rows pb + 16 (wave + 8 it) ..
+    const int nw = ns > wave ? (ns - wave + NW - 1) / NW : 0;  // this wave's
+    // stage it of this wave: rows pb + 16 (wave + NW it) ..; the gathered row
+    // numbers of the next stage to issue are read from LDS one iteration early
+    // (into `nxt`), so issuing a stage waits on no LDS round trip
+    int nxt[4];
+    auto fetch_rows = [&](int it) __attribute__((always_inline)) {
+      const int k0 = pb + kKwBK * (wave + NW * it);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = min(k0 + 4 * j + dr, pe - 1);
+        nxt[j] = GATHER ? sidx[k - pb] : k;
+      }
+    };
     auto issue = [&](int it) __attribute__((always_inline)) {
-      const int k0 = pb + kKwBK * (wave + kKwWaves * it);
-      const unsigned img = ring_w + (unsigned)((it & 1) * kKwStage) * 4u;
+      if constexpr (PROBE == 2) return;
+      const int k0 = pb + kKwBK * (wave + NW * it);
+      const unsigned img = ring_w + (unsigned)((it % NS) * kKwStage) * 4u;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = min(k0 + 4 * j + dr, pe - 1);
         glds16(p.A + (int64_t)k * p.lda + m0 + dc, img + (unsigned)j * 1024u);
-        const int64_t row = bidx ? sidx[k - pb] : k;
-        glds16(Bp + row * ldb + bc0 + dc, img + (unsigned)(kKwImg * 4 + j * 1024));
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        glds16(Bp + (int64_t)nxt[j] * ldb + bc0 + dc, img + (unsigned)(kKwImg * 4 + j * 1024));
     };
-    if (nw > 0) issue(0);
+    for (int st = 0; st < NS - 1 && st < nw; ++st) {
+      fetch_rows(st);
+      issue(st);
+    }
+    if (NS - 1 < nw) fetch_rows(NS - 1);
     for (int it = 0; it < nw; ++it) {
-      // stage it has landed (nothing younger is in flight yet); then stage it+1
-      // goes out into the other slot (read by this wave one iteration ago)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (it + 1 < nw) issue(it + 1);
-      float* const As = smem + wave * 2 * kKwStage + (it & 1) * kKwStage;
+      // stage it has landed (the younger ones stay in flight); stage it+NS-1
+      // goes out into the slot this wave read one iteration ago
+      wait_stage<8, NS - 2 >= 1 ? NS - 2 : 1>(min(NS - 2, nw - 1 - it));
+      if (it + NS - 1 < nw) {
+        issue(it + NS - 1);
+        if (it + NS < nw) fetch_rows(it + NS);
+      }
+      float* const As = smem + wave * NS * kKwStage + (it % NS) * kKwStage;
       const float* const Bs = As + kKwImg;
-      const int k0 = pb + kKwBK * (wave + kKwWaves * it);
+      const int k0 = pb + kKwBK * (wave + NW * it);
       if (k0 + kKwBK > pe) {  // k-tail: A rows past the pass end contribute nothing
         for (int r = pe - k0; r < kKwBK; ++r) As[r * kKwT + lane] = 0.f;
       }
@@ -131,6 +161,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
 #pragma unroll
         for (int r = 0; r < kKwBK; ++r) bsum += As[r * kKwT + lane];
       }
+      if constexpr (PROBE == 1) continue;
       // 16 k: lane (col l32, half h) holds k = 8 h .. 8 h + 7 of each fragment
       bf16x8 aH[2], aM[2], aL[2], bH[2], bM[2], bL[2];
 #pragma unroll
@@ -148,11 +179,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
       PS_KW_ALL(aH, bM)
       PS_KW_ALL(aH, bH)
 #undef PS_KW_ALL
+      // the next issue's row numbers are in registers by now (read at the top
+      // of this iteration): pinning them here keeps the compiler from sinking
+      // the LDS reads down to the DMAs that use them
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(nxt[j]));
     }
     __syncthreads();  // (the next pass rewrites sidx; the epilogue reuses the ring)
   }
 
-  // ---- the 8 wave partials, added in wave order
+  // ---- the NW wave partials, added in wave order
   float* const part = smem;  // [wave][64 x 64] row-major (the ring is free)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -166,31 +202,35 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
   float* const bpart = smem + kKwRing;  // [wave][64] (sidx is free)
   if (do_bias) bpart[wave * kKwT + lane] = bsum;
   __syncthreads();
-  const int e = tid * 8;  // this thread's 8 consecutive elements of the tile
-  float v[8];
+  // this thread's float4s of the tile: e4 = q NT + tid (coalesced rows)
+  float4 v[E4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = 0.f;
+  for (int q = 0; q < E4; ++q) {
+    v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int w = 0; w < kKwWaves; ++w) {
-    const float4 x0 = *reinterpret_cast<const float4*>(part + w * kKwT * kKwT + e);
-    const float4 x1 = *reinterpret_cast<const float4*>(part + w * kKwT * kKwT + e + 4);
-    v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
-    v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+    for (int w = 0; w < NW; ++w) {
+      const float4 x = *reinterpret_cast<const float4*>(part + w * kKwT * kKwT + 4 * (q * NT + tid));
+      v[q].x += x.x;
+      v[q].y += x.y;
+      v[q].z += x.z;
+      v[q].w += x.w;
+    }
   }
   float bv = 0.f;
   if (do_bias && tid < kKwT)
 #pragma unroll
-    for (int w = 0; w < kKwWaves; ++w) bv += bpart[w * kKwT + tid];
+    for (int w = 0; w < NW; ++w) bv += bpart[w * kKwT + tid];
 
   // ---- the splits of this tile, combined by the last to arrive (in split order)
   if (S > 1) {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, 0x7fffffff, 0x00020000);
-    const unsigned so = (unsigned)(((int64_t)tile * S + s) * kKwT * kKwT + e) * 4u;
-    const v4i w0{__float_as_int(v[0]), __float_as_int(v[1]), __float_as_int(v[2]), __float_as_int(v[3])};
-    const v4i w1{__float_as_int(v[4]), __float_as_int(v[5]), __float_as_int(v[6]), __float_as_int(v[7])};
-    __builtin_amdgcn_raw_buffer_store_b128(w0, rs, so, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(w1, rs, so + 16u, 0, 16);
+    const unsigned so = (unsigned)(((int64_t)tile * S + s) * kKwT * kKwT) * 4u;
+#pragma unroll
+    for (int q = 0; q < E4; ++q) {
+      const v4i w{__float_as_int(v[q].x), __float_as_int(v[q].y), __float_as_int(v[q].z), __float_as_int(v[q].w)};
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, so + (unsigned)(q * NT + tid) * 16u, 0, 16);
+    }
     if (do_bias && tid < kKwT)
       __hip_atomic_store(p.bslab + ((int64_t)mb * S + s) * kKwT + tid, bv, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -203,16 +243,18 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
     if (!last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = 0.f;
+    for (int q = 0; q < E4; ++q) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     bv = 0.f;
     for (int t = 0; t < S; ++t) {
-      const unsigned o = (unsigned)(((int64_t)tile * S + t) * kKwT * kKwT + e) * 4u;
-      const v4i y0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16);
-      const v4i y1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16u, 0, 16);
-      v[0] += __int_as_float(y0.x); v[1] += __int_as_float(y0.y);
-      v[2] += __int_as_float(y0.z); v[3] += __int_as_float(y0.w);
-      v[4] += __int_as_float(y1.x); v[5] += __int_as_float(y1.y);
-      v[6] += __int_as_float(y1.z); v[7] += __int_as_float(y1.w);
+      const unsigned o = (unsigned)(((int64_t)tile * S + t) * kKwT * kKwT) * 4u;
+#pragma unroll
+      for (int q = 0; q < E4; ++q) {
+        const v4i y = __builtin_amdgcn_raw_buffer_load_b128(rs, o + (unsigned)(q * NT + tid) * 16u, 0, 16);
+        v[q].x += __int_as_float(y.x);
+        v[q].y += __int_as_float(y.y);
+        v[q].z += __int_as_float(y.z);
+        v[q].w += __int_as_float(y.w);
+      }
       if (do_bias && tid < kKwT)
         bv += __hip_atomic_load(p.bslab + ((int64_t)mb * S + t) * kKwT + tid, __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_AGENT);
@@ -221,39 +263,36 @@ __global__ __launch_bounds__(512, 1) void wgrad_kw_kernel(KwParams p) {
   }
 
   // ---- store (and Adam)
-  const int m = m0 + e / kKwT, n = n0 + (e % kKwT);
-  const int64_t o = (int64_t)m * p.ld_dst + n;
-  const float4 g0 = make_float4(v[0], v[1], v[2], v[3]), g1 = make_float4(v[4], v[5], v[6], v[7]);
-  *reinterpret_cast<float4*>(p.dst + o) = g0;
-  *reinterpret_cast<float4*>(p.dst + o + 4) = g1;
   if (do_bias && tid < kKwT) p.dst_b[m0 + tid] = bv;
-  if (p.ad.p) {
-    const float ss = p.ad.coef[0], bc2 = p.ad.coef[1];
-    if (!(bc2 > 0.f)) return;  // a refused step (pinsage_fly_gate_adam)
-    const float omb1 = (float)(1.0 - p.ad.beta1), omb2 = (float)(1.0 - p.ad.beta2);
-    const float b2 = (float)p.ad.beta2, eps = p.ad.eps;
-    auto adam1 = [&](float& pp, float g, float& mm, float& vv) {
-      mm = mm + omb1 * (g - mm);
-      vv = vv * b2 + omb2 * g * g;
-      const float denom = sqrtf(vv) / bc2 + eps;
-      pp = pp - ss * (mm / denom);
-    };
+  const bool adam = p.ad.p && p.ad.coef[1] > 0.f;  // (bc2 = 0: a refused step, pinsage_fly_gate_adam)
+  const float ss = adam ? p.ad.coef[0] : 0.f, bc2 = adam ? p.ad.coef[1] : 1.f;
+  const float omb1 = (float)(1.0 - p.ad.beta1), omb2 = (float)(1.0 - p.ad.beta2);
+  const float b2 = (float)p.ad.beta2, eps = p.ad.eps;
+  auto adam1 = [&](float& pp, float g, float& mm, float& vv) {
+    mm = mm + omb1 * (g - mm);
+    vv = vv * b2 + omb2 * g * g;
+    const float denom = sqrtf(vv) / bc2 + eps;
+    pp = pp - ss * (mm / denom);
+  };
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float4 pp = *reinterpret_cast<const float4*>(p.ad.p + o + 4 * q);
-      float4 mm = *reinterpret_cast<const float4*>(p.ad.m + o + 4 * q);
-      float4 vv = *reinterpret_cast<const float4*>(p.ad.v + o + 4 * q);
-      const float4 g = q ? g1 : g0;
-      adam1(pp.x, g.x, mm.x, vv.x);
-      adam1(pp.y, g.y, mm.y, vv.y);
-      adam1(pp.z, g.z, mm.z, vv.z);
-      adam1(pp.w, g.w, mm.w, vv.w);
-      *reinterpret_cast<float4*>(p.ad.p + o + 4 * q) = pp;
-      *reinterpret_cast<float4*>(p.ad.m + o + 4 * q) = mm;
-      *reinterpret_cast<float4*>(p.ad.v + o + 4 * q) = vv;
+  for (int q = 0; q < E4; ++q) {
+    const int e = 4 * (q * NT + tid);
+    const int64_t o = (int64_t)(m0 + e / kKwT) * p.ld_dst + n0 + (e % kKwT);
+    *reinterpret_cast<float4*>(p.dst + o) = v[q];
+    if (adam) {
+      float4 pp = *reinterpret_cast<const float4*>(p.ad.p + o);
+      float4 mm = *reinterpret_cast<const float4*>(p.ad.m + o);
+      float4 vv = *reinterpret_cast<const float4*>(p.ad.v + o);
+      adam1(pp.x, v[q].x, mm.x, vv.x);
+      adam1(pp.y, v[q].y, mm.y, vv.y);
+      adam1(pp.z, v[q].z, mm.z, vv.z);
+      adam1(pp.w, v[q].w, mm.w, vv.w);
+      *reinterpret_cast<float4*>(p.ad.p + o) = pp;
+      *reinterpret_cast<float4*>(p.ad.m + o) = mm;
+      *reinterpret_cast<float4*>(p.ad.v + o) = vv;
     }
-    if (do_bias && tid < kKwT && p.ad.pb) adam1(p.ad.pb[m0 + tid], bv, p.ad.mb[m0 + tid], p.ad.vb[m0 + tid]);
   }
+  if (adam && do_bias && tid < kKwT && p.ad.pb) adam1(p.ad.pb[m0 + tid], bv, p.ad.mb[m0 + tid], p.ad.vb[m0 + tid]);
 }
 
 // ---------------------------------------------------------------- host side
@@ -287,7 +326,20 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   p.S = std::min(p.S, kKwMaxSplits);
   PS_REQUIRE(p.S == 1 || (p.slab && p.cnt && (!p.dst_b || p.bslab)), kErrArg, "wgrad: split scratch not set");
   const int grid = (p.M / kKwT) * (p.N / kKwT) * p.S;
-  hipLaunchKernelGGL(wgrad_kw_kernel, dim3(grid), dim3(512), 0, st, p);
+  // PINSAGE_KW_WAVES: 8 (default: 8 waves x 2-stage rings) or 4 (4 x 4)
+  static const int waves = getenv("PINSAGE_KW_WAVES") ? atoi(getenv("PINSAGE_KW_WAVES")) : 8;
+  const int probe = getenv("PINSAGE_KW_PROBE") ? atoi(getenv("PINSAGE_KW_PROBE")) : 0;  // (read per call)
+  const bool gather = p.b_idx || p.b2_idx;
+  if (probe == 1 || probe == 2) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
+    if (probe == 1) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 1>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 2>), dim3(grid), dim3(512), 0, st, p);
+  } else if (waves == 4) {
+    if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<4, 4, true>), dim3(grid), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kw_kernel<4, 4, false>), dim3(grid), dim3(256), 0, st, p);
+  } else {
+    if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, false>), dim3(grid), dim3(512), 0, st, p);
+  }
   PS_CHECK_LAUNCH();
   return kOk;
 }

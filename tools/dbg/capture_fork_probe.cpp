@@ -130,7 +130,64 @@ static int run_nested(const std::string& c) {
   return 0;
 }
 
+// The trainer's capture ORDER (pinsage_training._capture_graphs): graph gf
+// (the frontier on the origin stream A forks the side stream B and joins it),
+// then graph ga (the origin forks a branch S; the frontier on S forks the
+// SAME B and joins it into S; S joins A).  reuse_nested_fresh: ga's branch
+// forks a stream no earlier capture used.
+static int run_reuse_nested(const std::string& c) {
+  int* d = nullptr;
+  if (hipMalloc(&d, 64) != hipSuccess) return 90;
+  hipMemset(d, 0, 64);
+  hipStream_t A, S, B, C;
+  for (hipStream_t* x : {&A, &S, &B, &C}) hipStreamCreateWithFlags(x, hipStreamNonBlocking);
+  hipEvent_t e[8];
+  for (auto& x : e) hipEventCreateWithFlags(&x, hipEventDisableTiming);
+  const bool empty = c.find("empty") != std::string::npos;
+  hipStream_t F = c == "reuse_nested_fresh" ? C : B;
+  for (int cap = 0; cap < 2; ++cap) {
+    hipGraph_t g = nullptr;
+    hipError_t r = hipStreamBeginCapture(A, hipStreamCaptureModeGlobal);
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    hipStream_t from = A, fk = B;
+    if (cap == 1) {  // the look-ahead branch
+      hipEventRecord(e[0], A);
+      hipStreamWaitEvent(S, e[0], 0);
+      from = S;
+      fk = F;
+    }
+    hipEventRecord(e[1], from);
+    r = hipStreamWaitEvent(fk, e[1], 0);
+    printf("[%s] capture %d fork %s\n", c.c_str(), cap, hipGetErrorName(r));
+    if (!empty) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, fk, d + 8);
+    hipEventRecord(e[2], fk);
+    r = hipStreamWaitEvent(from, e[2], 0);
+    printf("[%s] capture %d join %s\n", c.c_str(), cap, hipGetErrorName(r));
+    if (cap == 1) {
+      hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, S, d + 4);
+      hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+      hipEventRecord(e[3], S);
+      hipStreamWaitEvent(A, e[3], 0);
+    }
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    fflush(stdout);
+    r = hipStreamEndCapture(A, &g);
+    printf("[%s] capture %d end %s graph %p\n", c.c_str(), cap, hipGetErrorName(r), (void*)g);
+    fflush(stdout);
+    if (r == hipSuccess && g) {
+      hipGraphExec_t x;
+      r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+      if (r == hipSuccess) r = hipGraphLaunch(x, A);
+      hipStreamSynchronize(A);
+      printf("[%s] capture %d replay %s\n", c.c_str(), cap, hipGetErrorName(r));
+    }
+  }
+  fflush(stdout);
+  return 0;
+}
+
 static int run_case(const std::string& c) {
+  if (c.rfind("reuse_nested", 0) == 0) return run_reuse_nested(c);
   if (c.rfind("nested", 0) == 0) return run_nested(c);
   if (c.rfind("reuse", 0) == 0) return run_reuse(c);
   int* d = nullptr;
@@ -194,7 +251,8 @@ int main(int argc, char** argv) {
   const char* cases[] = {"joined",        "joined_empty", "unjoined",
                          "unjoined_empty", "create_inside", "err_then_end",
                          "reuse_after_joined", "reuse_after_unjoined_empty",
-                         "nested_separate", "nested_kernel", "nested_empty"};
+                         "nested_separate", "nested_kernel", "nested_empty",
+                         "reuse_nested_kernel", "reuse_nested_empty", "reuse_nested_fresh"};
   if (argc > 1) return run_case(argv[1]);
   for (const char* c : cases) {
     fflush(stdout);
