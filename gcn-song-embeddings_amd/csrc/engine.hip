@@ -179,6 +179,12 @@ struct Engine {
   // tiles, few splits combined inside the launch, Adam fused) instead of the
   // split-K GEMM + reduce_slabs_2d; 1 (default) every site it supports, 0 none
   int wgrad_kw = getenv("PINSAGE_WGRAD_KW") ? atoi(getenv("PINSAGE_WGRAD_KW")) : 1;
+  // the side stream's long-K weight gradients run beside the chain's kernels:
+  // PINSAGE_KW_SIDE_FORM 1 = the 64-KiB form (wgrad.hip), so a CU holding one
+  // still takes the chain's workgroups; PINSAGE_KW_SIDE_WG = their grid target
+  int kw_side_form = getenv("PINSAGE_KW_SIDE_FORM") ? atoi(getenv("PINSAGE_KW_SIDE_FORM")) : 0;
+  int kw_side_wg = getenv("PINSAGE_KW_SIDE_WG") ? atoi(getenv("PINSAGE_KW_SIDE_WG")) : 256;
+  int kw_main_form = getenv("PINSAGE_KW_MAIN_FORM") ? atoi(getenv("PINSAGE_KW_MAIN_FORM")) : 0;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -257,6 +263,19 @@ struct Engine {
   // then ends after the chain)
   int defer_side = getenv("PINSAGE_DEFER_SIDE") ? atoi(getenv("PINSAGE_DEFER_SIDE")) : 3;
   std::vector<std::function<int()>> pend;  // deferred side launches, in order
+  // PINSAGE_FORK_PLAN: every fork point on the chain costs the chain's next
+  // launch ~5.5 us (the rocprofv3 step timeline: the node after a fork starts
+  // late), so side launches are merged into fewer forks -- side work may
+  // always start LATER than its inputs exist.  Bit 0: the loss monitors ride
+  // on the head backward's fork instead of forking at the loss; bit 1: layer
+  // l > 0's Q weight gradient rides on the next W-gradient fork (layer l-1's,
+  // after its normalisation backward); bit 2: layer 0's W weight gradient (and
+  // what rides with it) forks with the optimizer pass, after layer 0's dcat.
+  int fork_plan = getenv("PINSAGE_FORK_PLAN") ? atoi(getenv("PINSAGE_FORK_PLAN")) : 0;
+  // launches with no fork point of their own (fork_plan bit 0: the monitors),
+  // enqueued on the side stream of the next fork, after its wait
+  std::vector<std::function<int(hipStream_t)>> ride;
+  hipStream_t ride_st = nullptr;  // the stream the riders are ordered behind
   // the on-the-fly step (pinsage_engine_set_fly, fly.hip): the virtual nodes
   // x0 .. x0 + *fly_nx - 1 join the top set, and the loss hands each the
   // summed G row of its real node fly_xids[j] (call fly_xids[j] / fly_unit)
@@ -330,18 +349,31 @@ static int dep(Engine& E, hipStream_t from, hipStream_t to) {
 // binds to an event recorded on `from` now; with `defer` the launch itself
 // waits in E.pend until run_pend (after the main chain's next launch).
 static int fork_side(Engine& E, hipStream_t from, hipStream_t to, bool defer, std::function<int()> fn) {
-  if (from == to) return fn();
+  std::vector<std::function<int(hipStream_t)>> ride;
+  if (from == E.ride_st) ride.swap(E.ride);  // (only a fork behind the riders' inputs)
+  if (from == to) {
+    for (auto& r : ride) PS_TRY(r(to));
+    return fn();
+  }
   hipEvent_t e = E.ev[(size_t)(E.ev_next++ % kEvents)];
   PS_CHECK_HIP(hipEventRecord(e, from));
   if (!defer) {
     PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+    for (auto& r : ride) PS_TRY(r(to));
     return fn();
   }
-  E.pend.push_back([to, e, fn]() -> int {
+  E.pend.push_back([to, e, fn, ride]() -> int {
     PS_CHECK_HIP(hipStreamWaitEvent(to, e, 0));
+    for (auto& r : ride) PS_TRY(r(to));
     return fn();
   });
   return kOk;
+}
+// launches still riding (no fork has taken them): fork them now
+static int flush_ride(Engine& E) {
+  if (E.ride.empty()) return kOk;
+  PS_TRY(ensure_streams(E));
+  return fork_side(E, E.ride_st, E.side[0], false, []() -> int { return kOk; });
 }
 static int run_pend(Engine& E) {
   std::vector<std::function<int()>> v;
@@ -914,7 +946,9 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
     k.slab = slab;
     k.bslab = bslab;
     k.cnt = at<int>(ws, main ? E.kw_cnt_main : E.kw_cnt_side);
-    k.S = wgrad_kw_splits(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max);
+    k.form = main ? E.kw_main_form : E.kw_side_form;
+    k.S = wgrad_kw_splits(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max,
+                          main ? 256 : E.kw_side_wg);
     PS_REQUIRE((int64_t)k.S * w.M * w.N <= E.slab_floats, kErrWorkspace, "engine: wgrad slab too small");
     if (adam && after_use) PS_CHECK_HIP(hipStreamWaitEvent(st, after_use, 0));
     return launch_wgrad_kw(k, st);
@@ -992,6 +1026,18 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
   // weight gradients run on s_wg, each forked once its inputs exist on st
   const bool dfr = (E.defer_side & 1) != 0;
   PS_REQUIRE(stage < 0 || !adam, kErrArg, "engine: a staged backward runs without the fused optimizer");
+  // side launches waiting for a later fork (E.fork_plan bits 1, 2): every
+  // fork_late takes them along, ahead of its own launch
+  std::vector<std::function<int()>> late;
+  auto fork_late = [&](hipStream_t to, std::function<int()> fn) -> int {
+    std::vector<std::function<int()>> v;
+    v.swap(late);
+    if (v.empty()) return fork_side(E, st, to, dfr, fn);
+    return fork_side(E, st, to, dfr, [v, fn]() -> int {
+      for (auto& f : v) PS_TRY(f());
+      return fn();
+    });
+  };
   if (stage <= 0) {
   Timed t_hb(E, "bwd.head", st);
   auto wgrad_g2 = [&]() -> int {  // dG2 = dZ^T H1 beside the chain
@@ -1027,7 +1073,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
                            at<float>(ws, E.dP1), at<float>(ws, top.dp), at<int>(ws, E.rank_off),
                            at<int32_t>(ws, E.pos_sorted), E.reps_in_gp ? at<float>(ws, E.Gp) : nullptr, st));
     PS_TRY(run_pend(E));  // the loss monitors (PINSAGE_DEFER_SIDE bit 1)
-    PS_TRY(fork_side(E, st, s_wg, dfr, wgrad_g2));
+    PS_TRY(fork_late(s_wg, wgrad_g2));
   } else {
     GemmParams p;  // dP1 = (dZ G2) * lrelu'(H1)
     p.M_dev = cnt(top.S);
@@ -1071,7 +1117,7 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
     w.dst = gr + E.pG1w;
     w.ld_dst = o;
     w.dst_b = gr + E.pG1b;
-    PS_TRY(fork_side(E, st, s_wg, dfr, [&E, ws, w, s_wg, st]() -> int {
+    PS_TRY(fork_late(s_wg, [&E, ws, w, s_wg, st]() -> int {
       Timed tw(E, "bwd.wgrad.g1", s_wg);
       return weight_grad(E, ws, w, s_wg, "bwd.wgrad.g1", nullptr, nullptr, false, s_wg != st);
     }));
@@ -1145,10 +1191,12 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
       with_sk(E, ws, p);
       apply_choice(E, lname("bwd.dcat", l), p);
       // the W gradient forks before this launch (it reads dp), enqueued after it
-      PS_TRY(fork_side(E, st, s_w, dfr, [&E, ws, w_wgrad, s_w, st, l]() -> int {
+      auto wfn = [&E, ws, w_wgrad, s_w, st, l]() -> int {
         Timed tw(E, lname("bwd.w_wgrad", l), s_w);
         return weight_grad(E, ws, w_wgrad, s_w, lname("bwd.w_wgrad", l), nullptr, nullptr, false, s_w != st);
-      }));
+      };
+      if (l == 0 && (E.fork_plan & 4)) late.push_back(wfn);  // (forked with the optimizer pass)
+      else PS_TRY(fork_late(s_w, wfn));
       Timed td(E, lname("bwd.dcat", l), st);
       PS_TRY(launch_gemm(p, st));
       E.sk_used[lname("bwd.dcat", l)] = gemm_last_stream_k();
@@ -1157,11 +1205,13 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
     if (adam && l == 0) {  // every gradient but Q0's exists on s_w; W0 was read last
       const int64_t off = l0.pWw, n = E.n_params - l0.pWw;
       const AdamStep a = *adam;
-      PS_TRY(fork_side(E, st, s_w, dfr, [&E, s_w, off, n, a]() -> int {
+      PS_TRY(fork_late(s_w, [&E, s_w, off, n, a]() -> int {
         Timed ta(E, "adam", s_w);
         return launch_adam(E.params + off, E.grads + off, E.adam_m + off, E.adam_v + off, n, a.coef,
                            a.beta1, a.beta2, a.eps, s_w);
       }));
+    } else if (l == 0 && !late.empty()) {
+      PS_TRY(fork_late(s_w, []() -> int { return kOk; }));
     }
     const bool chunk_rows = l == 0 && E.dq_chunk_rows;
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
@@ -1194,11 +1244,13 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
     if (l > 0) {
       // dQ of this layer beside the chain, forked here (dpq complete), enqueued
       // after the dh launch
-      PS_TRY(fork_side(E, st, s_wg, dfr, [&E, ws, q_wgrad, s_wg, st, l]() -> int {
+      auto qfn = [&E, ws, q_wgrad, s_wg, st, l]() -> int {
         Timed tq(E, lname("bwd.q_wgrad", l), s_wg);
         return weight_grad(E, ws, q_wgrad, s_wg, lname("bwd.q_wgrad", l), nullptr, nullptr, false,
                            s_wg != st);
-      }));
+      };
+      if (E.fork_plan & 2) late.push_back(qfn);  // (rides on the next W-gradient fork)
+      else PS_TRY(fork_late(s_wg, qfn));
       GemmParams p;  // dh = dpq Q  -> scatter-add into the rows of layer l-1
       p.M_dev = cnt(lb.N);
       p.M_hint = (int)lb.N.hint;
@@ -1229,6 +1281,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
                          false));
     }
   }
+  if (!late.empty()) PS_TRY(fork_late(s_wg, []() -> int { return kOk; }));  // (a stage-0 call)
+  PS_TRY(flush_ride(E));
   PS_TRY(run_pend(E));
   // every gradient is written once the side streams drain into st (side[0]
   // also carries the loss monitors, pinsage_engine_loss)
@@ -1468,23 +1522,27 @@ int pinsage_engine_init_workspace(pinsage_engine* e, void* ws, void* stream) {
 
 int pinsage_engine_forward(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                            void* stream) {
+  PS_TRY(flush_ride(*reinterpret_cast<Engine*>(e)));
   PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
 }
 
 int pinsage_engine_forward_inference(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                                      void* stream) {
+  PS_TRY(flush_ride(*reinterpret_cast<Engine*>(e)));
   PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_forward(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream, false);
 }
 
 int pinsage_engine_frontier(pinsage_engine* e, void* ws, const int64_t* ids, int64_t n_ids,
                             void* stream) {
+  PS_TRY(flush_ride(*reinterpret_cast<Engine*>(e)));
   PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_frontier(*reinterpret_cast<Engine*>(e), ws, ids, n_ids, (hipStream_t)stream);
 }
 
 int pinsage_engine_forward_layers(pinsage_engine* e, void* ws, void* stream) {
+  PS_TRY(flush_ride(*reinterpret_cast<Engine*>(e)));
   PS_TRY(run_pend(*reinterpret_cast<Engine*>(e)));
   return engine_layers(*reinterpret_cast<Engine*>(e), ws, (hipStream_t)stream);
 }
@@ -1503,6 +1561,7 @@ int pinsage_engine_set_fork(pinsage_engine* e, void* ws_next, const int64_t* ids
 int pinsage_engine_gather_output(pinsage_engine* e, void* ws, int64_t n_ids, float* out,
                                  void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(flush_ride(*E));
   PS_TRY(run_pend(*E));
   return launch_gather_out(at<float>(ws, E->Z), (int)E->cfg.out, at<int32_t>(ws, E->pos_rank), n_ids,
                            out, (hipStream_t)stream);
@@ -1518,6 +1577,7 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
   }
   LayerBuf& top = E->L.back();
   hipStream_t st = (hipStream_t)stream;
+  PS_TRY(flush_ride(*E));  // (an earlier loss's monitors read what this one rewrites)
   {
     Timed t(*E, "loss", st);
     // (on the fly the repeated ranks are summed in the loss launch: the
@@ -1548,11 +1608,16 @@ int pinsage_engine_loss(pinsage_engine* e, void* ws, int64_t batch_size, float m
   float* scal = at<float>(ws, E->scal);
   const int nb4 = (int)ceil_div(batch_size, 4), out = (int)c.out, B = (int)batch_size;
   hipStream_t s0 = E->side[0];
-  auto mon = [E, part, varpart, scal, nb4, out, B, s0]() -> int {
-    Timed tm(*E, "loss.monitor", s0);
-    return launch_loss_monitor(part, nb4, varpart, out, B, scal, s0);
+  auto mon = [E, part, varpart, scal, nb4, out, B](hipStream_t s) -> int {
+    Timed tm(*E, "loss.monitor", s);
+    return launch_loss_monitor(part, nb4, varpart, out, B, scal, s);
   };
-  return fork_side(*E, st, s0, (E->defer_side & 2) != 0, mon);
+  if (E->fork_plan & 1) {  // no fork at the loss: the head backward's fork takes them
+    E->ride.push_back(mon);
+    E->ride_st = st;
+    return kOk;
+  }
+  return fork_side(*E, st, s0, (E->defer_side & 2) != 0, [mon, s0]() -> int { return mon(s0); });
 }
 
 int pinsage_engine_set_fly(pinsage_engine* e, int64_t x0, const int* n_x, const int64_t* xids, int64_t unit,
@@ -1573,6 +1638,7 @@ int pinsage_engine_set_fly(pinsage_engine* e, int64_t x0, const int* n_x, const 
 int pinsage_engine_set_output_grad(pinsage_engine* e, void* ws, const float* dout, int64_t n_ids,
                                    void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(flush_ride(*E));
   PS_TRY(run_pend(*E));
   LayerBuf& top = E->L.back();
   E->reps_in_gp = false;
@@ -1589,6 +1655,7 @@ int pinsage_engine_reset_backward(pinsage_engine* e, void* ws, void* stream) {
     return kErrArg;
   }
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(flush_ride(*E));
   PS_TRY(run_pend(*E));
   // the dY scatter-add targets of the layers below the top (the forward's
   // layer_prep zeroed them; a backward accumulates into them)
@@ -1623,6 +1690,7 @@ int pinsage_engine_backward_adam(pinsage_engine* e, void* ws, const float* coef,
 int pinsage_engine_adam(pinsage_engine* e, const float* coef, double beta1, double beta2, float eps,
                         void* stream) {
   Engine* E = reinterpret_cast<Engine*>(e);
+  PS_TRY(flush_ride(*E));
   PS_TRY(run_pend(*E));
   Timed t(*E, "adam", (hipStream_t)stream);
   if (!E->adam_m || !E->adam_v) {

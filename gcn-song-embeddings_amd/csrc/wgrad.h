@@ -29,10 +29,11 @@ struct KwParams {
   float* bslab = nullptr;
   int* cnt = nullptr;
   int S = 0;                  // K splits (0: wgrad_kw_splits)
+  int form = 0;               // 0: 8 waves, 128-KiB ring; 1: 4 waves, 64-KiB ring
 };
 
 bool wgrad_kw_supported(int M, int N, int N1, bool has_b2);
-int wgrad_kw_splits(int M, int N, int64_t K_est);
+int wgrad_kw_splits(int M, int N, int64_t K_est, int target = 256);  // ~target workgroups
 int64_t wgrad_kw_slab_floats(int M, int N);
 int64_t wgrad_kw_bslab_floats(int M);
 int64_t wgrad_kw_tickets(int M, int N);

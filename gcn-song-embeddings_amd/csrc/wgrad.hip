@@ -43,7 +43,6 @@ constexpr int kKwBK = 16;                     // k-rows per stage
 constexpr int kKwT = 64;                      // tile edge (M and N)
 constexpr int kKwImg = kKwBK * kKwT;          // floats per operand image
 constexpr int kKwStage = 2 * kKwImg;          // A + B (8 KiB)
-constexpr int kKwRing = 32768;                // ring floats (128 KiB): NW waves x NS stages
 constexpr int kKwWin = 6144;                  // gathered row numbers staged per pass (24 KiB)
 constexpr int kKwMaxSplits = 16;
 
@@ -53,9 +52,11 @@ __device__ __forceinline__ float4 kw_frag(const float* img, int col, int k4) {
                      img[(k4 + 3) * kKwT + col]);
 }
 
-// NW waves, each with an NS-stage private ring (NW * NS * 8 KiB = 128 KiB):
-// (8, 2) two waves per SIMD, one stage in flight per wave; (4, 4) one wave per
-// SIMD, three stages in flight.  GATHER: B rows come through the staged row
+// NW waves, each with an NS-stage private ring (NW * NS * 8 KiB):
+// (8, 2) two waves per SIMD, one stage in flight per wave (128 KiB); (4, 4) one
+// wave per SIMD, three stages in flight (128 KiB); (4, 2) one wave per SIMD, one
+// stage in flight (64 KiB: the side stream's form, which leaves a CU room for the
+// chain's kernels beside it -- a 152-KiB workgroup holds its CU alone).  GATHER: B rows come through the staged row
 // numbers (the identity for an ungathered segment), so no DMA branches.
 // PROBE (timing diagnostics only, tools/wgrad_bench.py; results are wrong):
 // 1 = the DMAs without the products, 2 = the products without the DMAs
@@ -67,8 +68,8 @@ __device__ __forceinline__ float4 kw_frag(const float* img, int col, int k4) {
 // row layout into the MFMA operand layout (lanes 0-31: k 0..7, lanes 32-63:
 // k 8..15 of the same 32 columns).
 template <int NW, int NS, bool GATHER, int PROBE = 0, bool REG = false>
-__global__ __launch_bounds__(NW * 64, 1) void wgrad_kw_kernel(KwParams p) {
-  static_assert(NW * NS * kKwStage == kKwRing, "ring size");
+__global__ __launch_bounds__(NW * 64, 8 / NW) void wgrad_kw_kernel(KwParams p) {
+  constexpr int kKwRing = NW * NS * kKwStage;  // ring floats
   static_assert(kKwRing >= NW * kKwT * kKwT, "the wave partials reuse the ring");
   constexpr int NT = NW * 64;
   constexpr int E4 = kKwT * kKwT / 4 / NT;  // float4s of the tile per thread
@@ -80,12 +81,17 @@ __global__ __launch_bounds__(NW * 64, 1) void wgrad_kw_kernel(KwParams p) {
   const int tm = p.M / kKwT, tn = p.N / kKwT, S = p.S;
   const int G = tm * tn * S;
   // blocks b and b + 8 share an XCD: with G % 8 == 0 each XCD takes a
-  // contiguous run of n-blocks, so the workgroups reading one B column slice
-  // (the gathered rows) share its L2
+  // contiguous run of L, and L runs over the tiles of one split before the
+  // next split, so an XCD's workgroups work on ONE split's rows of A and B
+  // (or, for S < 8, on 8 / S of its tiles): every A / B row of a split is
+  // fetched into one or two XCDs' L2 and re-read there by the tiles that share
+  // it.  (Ordered n-block first, the eight m-blocks of a column slice shared an
+  // XCD but every XCD read all of A: 4.2x the algorithmic bytes at C2 dQ0,
+  // profiles/r06/pmc_c2_q_wgrad.json.)
   const int b = blockIdx.x;
   const int L = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
-  const int nb = L / (tm * S), rem = L - nb * tm * S;
-  const int mb = rem / S, s = rem - (rem / S) * S;
+  const int s = L / (tm * tn), t_ = L - s * tm * tn;
+  const int nb = t_ / tm, mb = t_ - nb * tm;
   const int m0 = mb * kKwT, n0 = nb * kKwT;
   const int tile = nb * tm + mb;
   // this split's rows, on the 16-row stage grid
@@ -392,9 +398,9 @@ bool wgrad_kw_supported(int M, int N, int N1, bool has_b2) {
   return M > 0 && N > 0 && M % kKwT == 0 && N % kKwT == 0 && (!has_b2 || (N1 >= 0 && N1 % kKwT == 0));
 }
 
-int wgrad_kw_splits(int M, int N, int64_t K_est) {
+int wgrad_kw_splits(int M, int N, int64_t K_est, int target) {
   const int tiles = (M / kKwT) * (N / kKwT);
-  int S = std::max(1, (256 + tiles - 1) / tiles);
+  int S = std::max(1, (std::max(1, target) + tiles - 1) / tiles);
   S = std::min<int64_t>(S, std::max<int64_t>(1, K_est / 256));  // >= 256 rows (16 stages) per split
   S = std::min(S, kKwMaxSplits);
   while (S > 1 && (tiles * S) % 8 != 0 && tiles * S > 8) --S;  // (XCD-aware placement)
@@ -414,7 +420,7 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
              kErrArg, "wgrad: operands and 16-B aligned row strides");
   PS_REQUIRE(!p.ad.p || (p.ad.m && p.ad.v && p.ad.coef && (!p.dst_b || (p.ad.pb && p.ad.mb && p.ad.vb))),
              kErrArg, "wgrad: incomplete Adam slice");
-  if (p.S <= 0) p.S = wgrad_kw_splits(p.M, p.N, p.K_max);
+  if (p.S <= 0) p.S = wgrad_kw_splits(p.M, p.N, p.K_max, 256);
   p.S = std::min(p.S, kKwMaxSplits);
   PS_REQUIRE(p.S == 1 || (p.slab && p.cnt && (!p.dst_b || p.bslab)), kErrArg, "wgrad: split scratch not set");
   const int grid = (p.M / kKwT) * (p.N / kKwT) * p.S;
@@ -422,12 +428,18 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   const int waves = getenv("PINSAGE_KW_WAVES") ? atoi(getenv("PINSAGE_KW_WAVES")) : 8;  // (per call: A/B)
   const int probe = getenv("PINSAGE_KW_PROBE") ? atoi(getenv("PINSAGE_KW_PROBE")) : 0;  // (read per call)
   const bool gather = p.b_idx || p.b2_idx;
+  // PINSAGE_KW_FORM (tests / microbenchmarks through the C-ABI): the form of a
+  // launch whose caller did not choose one
+  if (p.form == 0 && getenv("PINSAGE_KW_FORM")) p.form = atoi(getenv("PINSAGE_KW_FORM"));
   if (waves == 1) {  // PINSAGE_KW_WAVES=1: the register-ring k loop (REG), 8 waves
     if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 0, true>), dim3(grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, false, 0, true>), dim3(grid), dim3(512), 0, st, p);
   } else if (probe == 1 || probe == 2) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
     if (probe == 1) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 1>), dim3(grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 2>), dim3(grid), dim3(512), 0, st, p);
+  } else if (p.form == 1) {  // 4 waves x 2 stages: 64-KiB ring
+    if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<4, 2, true>), dim3(grid), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kw_kernel<4, 2, false>), dim3(grid), dim3(256), 0, st, p);
   } else if (waves == 4) {
     if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<4, 4, true>), dim3(grid), dim3(256), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<4, 4, false>), dim3(grid), dim3(256), 0, st, p);

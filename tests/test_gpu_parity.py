@@ -397,7 +397,9 @@ def test_frontier_ahead_matches_serial_step(mode):
 
 
 @pytest.mark.parametrize("var,a,b", [("PINSAGE_DEFER_SIDE", "0", "3"), ("PINSAGE_DQ_CHUNK_ROWS", "0", "1"),
-                                     ("PINSAGE_FUSED_NEXT_Q", "0", "1"), ("PINSAGE_HEAD_IN_AGGW", "0", "1")])
+                                     ("PINSAGE_FUSED_NEXT_Q", "0", "1"), ("PINSAGE_HEAD_IN_AGGW", "0", "1"),
+                                     ("PINSAGE_FORK_PLAN", "0", "7"), ("PINSAGE_FORK_PLAN", "0", "3"),
+                                     ("PINSAGE_KW_SIDE_FORM", "0", "1")])
 def test_engine_variants_train_alike(var, a, b, monkeypatch):
     """Engine variants that change only launch order or summation order train
     alike -- same published losses (the monitors' output) and parameters within
@@ -409,7 +411,10 @@ def test_engine_variants_train_alike(var, a, b, monkeypatch):
     PINSAGE_FUSED_NEXT_Q (layer 1's Q projection inside layer 0's 32-row
     aggregation + W kernel, that form forced here) and PINSAGE_HEAD_IN_AGGW
     (the model head's forward inside the top layer's 16-row tile, exact fp32
-    MFMAs in another k order than head_fwd_kernel's)."""
+    MFMAs in another k order than head_fwd_kernel's) and PINSAGE_FORK_PLAN
+    (side launches merged into fewer forks: the same kernels on the same data,
+    so bitwise) and PINSAGE_KW_SIDE_FORM (the side weight gradients as 4-wave
+    workgroups: another wave-partial order)."""
     if var != "PINSAGE_HEAD_IN_AGGW":  # (the head is fused into the 16-row form only)
         monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
     import graph
@@ -444,6 +449,8 @@ def test_engine_variants_train_alike(var, a, b, monkeypatch):
 
             l0, p0 = run(a)
             l1, p1 = run(b)
+            if var == "PINSAGE_FORK_PLAN":
+                assert l0 == l1 and torch.equal(p0, p1)
             assert all(v > 0 for v in l0)
             for x, y in zip(l0, l1):
                 assert abs(x - y) <= 1e-4 * abs(x) + 1e-7

@@ -63,6 +63,13 @@ def main():
                                           vp(B2), (N - n1) if B2 is not None else 0, vp(dst), N, vp(db), S, vp(sc),
                                           None, None, None, None, None, None, None, 0.9, 0.999, 1e-8, st), "wgrad")
             res[f"kw S={S or 'auto'}"] = timed(kw, a.reps)
+        os.environ["PINSAGE_KW_FORM"] = "1"  # 4 waves, 64-KiB ring
+        for S in (0, 4, 8, 16):
+            res[f"f1 S={S or 'auto'}"] = timed(lambda: nat.check(L.pinsage_wgrad(
+                M, N, vp(K_dev), K, vp(A), M, vp(B), n1, vp(idx), n1 if B2 is not None else -1, vp(B2),
+                (N - n1) if B2 is not None else 0, vp(dst), N, vp(db), S, vp(sc), None, None, None, None, None,
+                None, None, 0.9, 0.999, 1e-8, st), "wgrad"), a.reps)
+        os.environ.pop("PINSAGE_KW_FORM")
         os.environ["PINSAGE_KW_WAVES"] = "1"  # the register-ring k loop
         for S in (0, 4, 8):
             res[f"reg S={S or 'auto'}"] = timed(lambda: nat.check(L.pinsage_wgrad(
