@@ -727,12 +727,101 @@ __global__ __launch_bounds__(1024) void csr_sort_rows_kernel(const int2* __restr
 // add up to dpq[u]; the Q weight gradient dpq^T h[q_src] is then the same
 // GEMM over chunk rows (h gathered through csrc) and no combine is needed --
 // at the bottom layer nothing else reads dpq (no dh below the input features).
-template <int VEC, bool CM = false>
+// Row-granular write-through store / L2-bypassing load of one float4 of a
+// partial row (the split-row tree below: a partial written on one XCD is read
+// by a wave on another, and the XCDs' L2s are not coherent; the same hand-off
+// as wgrad.hip's split combine).  `row` must be wave-uniform.
+typedef int dq_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void dq_st_wt(float* row, int i, float4 v) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff, 0x00020000);
+  const dq_v4i w{__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(w, rs, (unsigned)i * 16u, 0, 16);
+}
+__device__ __forceinline__ float4 dq_ld_wt(const float* row, int i) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), 0, 0x7fffffff, 0x00020000);
+  const dq_v4i y = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)i * 16u, 0, 16);
+  return make_float4(__int_as_float(y.x), __int_as_float(y.y), __int_as_float(y.z), __int_as_float(y.w));
+}
+// Split-row tree (TREE, PINSAGE_DQ_TREE): a row u split over k chunks
+// cbase[u] .. cbase[u] + k - 1 is combined by the chunk waves themselves, with
+// no dq_combine launch: the chunks are the leaves of a fan-in-8 tree whose node
+// (L, g) holds the sum of leaves 8^L g .. 8^L (g + 1) - 1 in part row
+// cbase[u] + 8^L g.  A finished node bumps its parent's ticket (level L's
+// array, entry cbase[u] + g / 8); the child that arrives last sums the
+// parent's children in child order, so every sum has a fixed order whatever
+// the timing (deterministic), and the root applies lrelu'(q) and writes
+// dpq[u].  Tickets reset themselves.  acc: this chunk's raw partial.
+template <int VEC>
+__device__ __forceinline__ void dq_tree_leaf(float4 (&acc)[VEC], const float4 (&qv)[VEC], int u, int64_t ci,
+                                             int lane, int h4, int hid, const int* __restrict__ off,
+                                             const int* __restrict__ cbase, int* __restrict__ tk,
+                                             int64_t tk_stride, float* __restrict__ part,
+                                             float* __restrict__ dpq) {
+  const int k = n_chunks(off[u + 1] - off[u]);
+  const int64_t cb = cbase[u];
+  int64_t g = ci - cb, span = 1, nodes = k;
+  float* leaf = part + (int64_t)__builtin_amdgcn_readfirstlane((int)ci) * hid;
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+    if (v * 64 + lane < h4) dq_st_wt(leaf, v * 64 + lane, acc[v]);
+  for (int L = 0;; ++L) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this node's row is written through
+    const int64_t gp = g >> 3;
+    const int nch = (int)min<int64_t>(8, nodes - 8 * gp);
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(tk + L * tk_stride + cb + gp, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0, 64);
+    if (t != nch - 1) return;  // a sibling still runs: the last one carries on
+    if (lane == 0) __hip_atomic_store(tk + L * tk_stride + cb + gp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float4 x[8][VEC];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int cc = c < nch ? c : nch - 1;  // (a repeated child: loaded, not added)
+      const float* row = part + (cb + span * (8 * gp + cc)) * hid;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) x[c][v] = dq_ld_wt(row, min(v * 64 + lane, h4 - 1));
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc[v] = x[0][v];
+#pragma unroll
+    for (int c = 1; c < 8; ++c)
+      if (c < nch)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          acc[v].x += x[c][v].x;
+          acc[v].y += x[c][v].y;
+          acc[v].z += x[c][v].z;
+          acc[v].w += x[c][v].w;
+        }
+    span *= 8;
+    nodes = (nodes + 7) >> 3;
+    g = gp;
+    if (nodes == 1) {  // the root: dpq[u]
+      float4* o = reinterpret_cast<float4*>(dpq + (int64_t)u * hid);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+        if (v * 64 + lane < h4)
+          o[v * 64 + lane] = make_float4(acc[v].x * lrelu_grad(qv[v].x), acc[v].y * lrelu_grad(qv[v].y),
+                                         acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
+      return;
+    }
+    float* node = part + (int64_t)__builtin_amdgcn_readfirstlane((int)(cb + span * g)) * hid;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+      if (v * 64 + lane < h4) dq_st_wt(node, v * 64 + lane, acc[v]);
+  }
+}
+
+template <int VEC, bool CM = false, bool TREE = false>
 __global__ __launch_bounds__(256) void dq_chunk_kernel(
     const int2* __restrict__ chunks, const int* __restrict__ nchunks, const int2* __restrict__ occ2,
     const float* __restrict__ dagg, int64_t ld_dagg, const float* __restrict__ q, int hid,
     float* __restrict__ dpq, float* __restrict__ part, const int32_t* __restrict__ q_src = nullptr,
-    int32_t* __restrict__ csrc = nullptr) {
+    int32_t* __restrict__ csrc = nullptr, const int* __restrict__ off = nullptr,
+    const int* __restrict__ cbase = nullptr, int* __restrict__ tk = nullptr, int64_t tk_stride = 0) {
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -801,6 +890,18 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
             }
           }
         }
+      }
+      if (TREE && split) {  // this chunk is a leaf of its row's tree (no pending store)
+        if (pend_o) {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v)
+            if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
+          pend_o = nullptr;
+        }
+        dq_tree_leaf<VEC>(acc, qv, u, ci, lane, h4, hid, off, cbase, tk, tk_stride, part, dpq);
+        dsc = dsc_n;
+        oc = oc_n;
+        continue;
       }
 #pragma unroll
       for (int v = 0; v < VEC; ++v)
@@ -1900,11 +2001,18 @@ int64_t dq_chunk_capacity(int64_t S_max, int T, int64_t N_max) {
 // upper bound of the split-row list: a split row holds more than kDqChunk slots
 int64_t dq_split_capacity(int64_t S_max, int T) { return S_max * T / (kDqChunk + 1) + 1; }
 
+// levels of the split-row tree for rows of up to max_chunks chunks (fan-in 8)
+int dq_tree_levels(int64_t max_chunks) {
+  int L = 1;
+  for (int64_t n = 8; n < max_chunks; n *= 8) ++L;
+  return L;
+}
+
 int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks, const int2* split,
                      const int* nsplit, int64_t max_split, const int* off, const int2* occ2,
                      const float* dagg, int64_t ld_dagg, const float* q,
                      int hid, float* dpq, float* part, hipStream_t st, const int32_t* q_src,
-                     int32_t* csrc) {
+                     int32_t* csrc, const int* cbase, int* tk) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
   // persistent waves (each prefetches its next chunk); 512 to 4096 blocks
   // measured alike at C2 (round 5), 2048 kept
@@ -1924,6 +2032,16 @@ int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks,
   // each XCD gathers its eighth of d_agg from its own L2 -- was bitwise this
   // kernel and slower in the step: C2 0.398-0.406 -> 0.408-0.50 ms, C4
   // 0.426-0.431 -> 0.447-0.452, round 6; removed)
+  if (tk && cbase && hid <= 512) {  // split rows combined by their own chunks (no combine launch)
+    if (hid > 256)
+      hipLaunchKernelGGL((dq_chunk_kernel<2, false, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2,
+                         dagg, ld_dagg, q, hid, dpq, part, nullptr, nullptr, off, cbase, tk, max_chunks);
+    else
+      hipLaunchKernelGGL((dq_chunk_kernel<1, false, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2,
+                         dagg, ld_dagg, q, hid, dpq, part, nullptr, nullptr, off, cbase, tk, max_chunks);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
   if (hid >= 512)
     hipLaunchKernelGGL((dq_chunk_kernel<2>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2, dagg, ld_dagg,
                        q, hid, dpq, part);

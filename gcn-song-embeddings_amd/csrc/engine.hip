@@ -57,7 +57,9 @@ int64_t dq_chunk_capacity(int64_t, int, int64_t);
 int64_t dq_split_capacity(int64_t, int);
 int launch_dq_chunks(const int2*, const int*, int64_t, const int2*, const int*, int64_t, const int*,
                      const int2*, const float*, int64_t, const float*, int, float*, float*, hipStream_t,
-                     const int32_t* q_src = nullptr, int32_t* csrc = nullptr);
+                     const int32_t* q_src = nullptr, int32_t* csrc = nullptr, const int* cbase = nullptr,
+                     int* tk = nullptr);
+int dq_tree_levels(int64_t max_chunks);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
 int launch_loss(const float*, int, const int32_t*, int, float, const float*, int64_t, int,
@@ -106,6 +108,8 @@ struct LayerBuf {
          occ2 = 0, occ2b = 0, chunks = 0, nchunks = 0, dqpart = 0, split = 0, nsplit = 0;
   size_t csrc = 0;  // chunk rows' source indices (bottom layer, Engine::dq_chunk_rows)
   int64_t max_chunks = 0, max_split = 0;
+  size_t dqtk = 0;  // split-row tree tickets (dq_tree_levels x max_chunks ints, self-resetting)
+  int64_t dqtk_len = 0;
   // parameter offsets (floats) into the flat param / grad buffers
   int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
   // this layer's own neighbourhood table (pinsage_engine_set_layer_table: the
@@ -185,6 +189,12 @@ struct Engine {
   int kw_side_form = getenv("PINSAGE_KW_SIDE_FORM") ? atoi(getenv("PINSAGE_KW_SIDE_FORM")) : 0;
   int kw_side_wg = getenv("PINSAGE_KW_SIDE_WG") ? atoi(getenv("PINSAGE_KW_SIDE_WG")) : 256;
   int kw_main_form = getenv("PINSAGE_KW_MAIN_FORM") ? atoi(getenv("PINSAGE_KW_MAIN_FORM")) : 0;
+  // PINSAGE_DQ_TREE (default 1): rows of the transposed aggregation split over
+  // several chunks are summed by their chunk waves as a fixed fan-in-8 tree
+  // (conv.hip dq_tree_leaf) instead of by a dq_combine launch after them
+  // (three interleaved pairs at C2, ms/step: 0.3949 / 0.3975 / 0.3985 with the
+  // combine launch, 0.3872 / 0.3855 / 0.3939 without; C4 even)
+  int dq_tree = getenv("PINSAGE_DQ_TREE") ? atoi(getenv("PINSAGE_DQ_TREE")) : 1;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -521,6 +531,8 @@ static void layout(Engine& E) {
     lb.max_split = dq_split_capacity(FS, (int)T);
     lb.split = carve(cur, lb.max_split * 8);
     lb.nsplit = carve(cur, 16);
+    lb.dqtk_len = (int64_t)dq_tree_levels(lb.max_chunks) * lb.max_chunks;
+    lb.dqtk = carve(cur, lb.dqtk_len * 4);
   }
   const int64_t top = E.L.back().S.cap;
   E.ids = carve(cur, c.max_pos * 8 + 16);  // + Adam coefficients staged behind the ids
@@ -1219,7 +1231,8 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
                             at<int>(ws, lb.off), at<int2>(ws, lb.occ2),
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
                             at<float>(ws, lb.dqpart), st, at<int32_t>(ws, lb.q_src),
-                            chunk_rows ? at<int32_t>(ws, lb.csrc) : nullptr));
+                            chunk_rows ? at<int32_t>(ws, lb.csrc) : nullptr,
+                            E.dq_tree ? at<int>(ws, lb.cbase) : nullptr, E.dq_tree ? at<int>(ws, lb.dqtk) : nullptr));
     PS_TRY(run_pend(E));
     WGrad q_wgrad;
     {
@@ -1305,8 +1318,10 @@ int engine_init_workspace(Engine& E, void* ws, hipStream_t st) {
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.G), 0, (size_t)(3 * top * c.out) * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.Kc), 0, (size_t)(3 * top) * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.rank_off), 0xff, 4, st));  // (no positions yet)
-  for (auto& lb : E.L)
+  for (auto& lb : E.L) {
     PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, lb.cnt), 0, (size_t)(lb.N.cap + 1) * 4, st));
+    PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, lb.dqtk), 0, (size_t)lb.dqtk_len * 4, st));
+  }
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.sk_cnt), 0, (size_t)E.sk_cnt_len * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.kw_cnt_main), 0, (size_t)E.kw_cnt_len * 4, st));
   PS_CHECK_HIP(hipMemsetAsync(at<char>(ws, E.kw_cnt_side), 0, (size_t)E.kw_cnt_len * 4, st));

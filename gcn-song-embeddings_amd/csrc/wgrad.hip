@@ -59,7 +59,9 @@ __device__ __forceinline__ float4 kw_frag(const float* img, int col, int k4) {
 // chain's kernels beside it -- a 152-KiB workgroup holds its CU alone).  GATHER: B rows come through the staged row
 // numbers (the identity for an ungathered segment), so no DMA branches.
 // PROBE (timing diagnostics only, tools/wgrad_bench.py; results are wrong):
-// 1 = the DMAs without the products, 2 = the products without the DMAs
+// 1 = the DMAs without the products, 2 = the products without the DMAs,
+// 3 = 2 without the split (the LDS reads and MFMAs only), 4 = the whole k loop
+// without the split
 // REG: the k loop without the LDS ring -- every load is one 256-B row of A
 // or B (row base in SGPRs: the gathered row numbers are wave-uniform, read by
 // scalar loads; lane l takes column l), held in a three-stage register ring
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void wgrad_kw_kernel(KwParams p) {
       }
     };
     auto issue = [&](int it) __attribute__((always_inline)) {
-      if constexpr (PROBE == 2) return;
+      if constexpr (PROBE == 2 || PROBE == 3) return;
       const int k0 = pb + kKwBK * (wave + NW * it);
       const unsigned img = ring_w + (unsigned)((it % NS) * kKwStage) * 4u;
 #pragma unroll
@@ -262,6 +264,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void wgrad_kw_kernel(KwParams p) {
       if constexpr (PROBE == 1) continue;
       // 16 k: lane (col l32, half h) holds k = 8 h .. 8 h + 7 of each fragment
       bf16x8 aH[2], aM[2], aL[2], bH[2], bM[2], bL[2];
+      if constexpr (PROBE >= 3) {  // the operands' bits as bf16, unsplit (timing only)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const float4 a0 = kw_frag(As, i * 32 + l32, 8 * h), a1 = kw_frag(As, i * 32 + l32, 8 * h + 4);
+          const float4 b0 = kw_frag(Bs, i * 32 + l32, 8 * h), b1 = kw_frag(Bs, i * 32 + l32, 8 * h + 4);
+          aH[i] = aM[i] = aL[i] = __builtin_bit_cast(bf16x8, make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w));
+          bH[i] = bM[i] = bL[i] = __builtin_bit_cast(bf16x8, make_float4(b0.x + b1.x, b0.y + b1.y, b0.z + b1.z, b0.w + b1.w));
+        }
+      } else
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         split3(kw_frag(As, i * 32 + l32, 8 * h), kw_frag(As, i * 32 + l32, 8 * h + 4), aH[i], aM[i], aL[i]);
@@ -434,9 +445,11 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   if (waves == 1) {  // PINSAGE_KW_WAVES=1: the register-ring k loop (REG), 8 waves
     if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 0, true>), dim3(grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, false, 0, true>), dim3(grid), dim3(512), 0, st, p);
-  } else if (probe == 1 || probe == 2) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
+  } else if (probe >= 1 && probe <= 4) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
     if (probe == 1) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 1>), dim3(grid), dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 2>), dim3(grid), dim3(512), 0, st, p);
+    else if (probe == 2) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 2>), dim3(grid), dim3(512), 0, st, p);
+    else if (probe == 3) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 3>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 4>), dim3(grid), dim3(512), 0, st, p);
   } else if (p.form == 1) {  // 4 waves x 2 stages: 64-KiB ring
     if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<4, 2, true>), dim3(grid), dim3(256), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<4, 2, false>), dim3(grid), dim3(256), 0, st, p);

@@ -77,7 +77,7 @@ def main():
                 (N - n1) if B2 is not None else 0, vp(dst), N, vp(db), S, vp(sc), None, None, None, None, None,
                 None, None, 0.9, 0.999, 1e-8, st), "wgrad"), a.reps)
         os.environ.pop("PINSAGE_KW_WAVES")
-        for probe in ("1", "2"):  # DMAs only / products only (wgrad.hip PROBE: timing, wrong results)
+        for probe in ("1", "2", "3", "4"):  # wgrad.hip PROBE (timing, wrong results)
             os.environ["PINSAGE_KW_PROBE"] = probe
             res[f"probe{probe} S=auto"] = timed(lambda: nat.check(L.pinsage_wgrad(
                 M, N, vp(K_dev), K, vp(A), M, vp(B), n1, vp(idx), n1 if B2 is not None else -1, vp(B2),
