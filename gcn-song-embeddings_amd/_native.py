@@ -83,6 +83,8 @@ _SIGS = {
     "pinsage_frontier_local_idx": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "pinsage_linear": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, ctypes.c_int, vp, i64, vp]),
     "pinsage_wgrad_scratch_bytes": (i64, [i64, i64]),
+    "pinsage_wgrad_planes": (ctypes.c_int, [i64, i64, vp, i64, vp, i64, i64, vp, i64, i64, vp, vp, i64, vp,
+                                            ctypes.c_int, vp, vp]),
     "pinsage_wgrad": (ctypes.c_int, [i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp,
                                      ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_float, vp]),
@@ -129,6 +131,7 @@ _SIGS = {
     "pinsage_engine_num_params": (i64, [vp]),
     "pinsage_engine_offsets": (ctypes.c_int, [vp, ctypes.POINTER(EngineOffsets)]),
     "pinsage_engine_set_tensors": (ctypes.c_int, [vp, vp, i64, vp, vp, i64, vp, vp, vp, vp]),
+    "pinsage_engine_set_feature_planes": (ctypes.c_int, [vp, vp, i64]),
     "pinsage_engine_forward": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_forward_inference": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_frontier": (ctypes.c_int, [vp, vp, vp, i64, vp]),

@@ -560,6 +560,37 @@ int pinsage_wgrad(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const f
   return launch_wgrad_kw(p, (hipStream_t)stream);
 }
 
+int pinsage_wgrad_planes(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const uint16_t* A3, int64_t a3_ps,
+                         int64_t lda, const uint16_t* B3, int64_t b3_ps, int64_t ldb, const int32_t* b_idx,
+                         float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, void* stream) {
+  PS_REQUIRE(M > 0 && N > 0 && M <= INT32_MAX && N <= INT32_MAX && K_max >= 0 && K_max <= INT32_MAX &&
+                 splits >= 0 && scratch && A3 && B3 && a3_ps >= 0 && b3_ps >= 0,
+             kErrArg, "wgrad_planes: bad argument");
+  KwParams p;
+  p.A3 = A3;
+  p.a3_ps = a3_ps;
+  p.lda = lda;
+  p.M = (int)M;
+  p.B3 = B3;
+  p.b3_ps = b3_ps;
+  p.ldb = ldb;
+  p.b_idx = b_idx;
+  p.N = (int)N;
+  p.K_dev = K_dev;
+  p.K_max = (int)K_max;
+  p.dst = dst;
+  p.ld_dst = ld_dst;
+  p.dst_b = dst_b;
+  char* sc = static_cast<char*>(scratch);
+  p.cnt = reinterpret_cast<int*>(sc);
+  sc += align_up(wgrad_kw_tickets((int)M, (int)N) * 4, 256);
+  p.slab = reinterpret_cast<float*>(sc);
+  sc += wgrad_kw_slab_floats((int)M, (int)N) * 4;
+  p.bslab = reinterpret_cast<float*>(sc);
+  p.S = splits;
+  return launch_wgrad_kw(p, (hipStream_t)stream);
+}
+
 int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor, const float* A,
                     int64_t lda, const int32_t* a_idx, const float* B, int64_t ldb,
                     const int32_t* b_idx, float* C, int64_t ldc, const float* bias, int act,

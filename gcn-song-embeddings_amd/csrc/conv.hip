@@ -12,6 +12,7 @@
 //   adam            torch.optim.Adam step (pinsage_training.py:147,191)
 #include "common.h"
 #include "conv.h"
+#include "bf16split.h"
 
 #include <algorithm>
 #include <climits>
@@ -732,6 +733,18 @@ __global__ __launch_bounds__(1024) void csr_sort_rows_kernel(const int2* __restr
 // by a wave on another, and the XCDs' L2s are not coherent; the same hand-off
 // as wgrad.hip's split combine).  `row` must be wave-uniform.
 typedef int dq_v4i __attribute__((ext_vector_type(4)));
+// dpq row elements e .. e + 3 as their hi / mid / lo bf16 planes (plane stride
+// ps elements): the split the long-K weight gradient's fp32 form does in
+// registers (bf16split.h), so its planes form (wgrad_pl_kernel) gets the same
+// products
+__device__ __forceinline__ void dq_store_planes(uint16_t* __restrict__ base, int64_t ps, int64_t e, float4 v) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split_pair(f32x2{v.x, v.y}, h0, m0, l0);
+  split_pair(f32x2{v.z, v.w}, h1, m1, l1);
+  *reinterpret_cast<uint2*>(base + e) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(base + ps + e) = make_uint2(m0, m1);
+  *reinterpret_cast<uint2*>(base + 2 * ps + e) = make_uint2(l0, l1);
+}
 __device__ __forceinline__ void dq_st_wt(float* row, int i, float4 v) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff, 0x00020000);
   const dq_v4i w{__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
@@ -752,12 +765,13 @@ __device__ __forceinline__ float4 dq_ld_wt(const float* row, int i) {
 // parent's children in child order, so every sum has a fixed order whatever
 // the timing (deterministic), and the root applies lrelu'(q) and writes
 // dpq[u].  Tickets reset themselves.  acc: this chunk's raw partial.
-template <int VEC>
+template <int VEC, bool PL3>
 __device__ __forceinline__ void dq_tree_leaf(float4 (&acc)[VEC], const float4 (&qv)[VEC], int u, int64_t ci,
                                              int lane, int h4, int hid, const int* __restrict__ off,
                                              const int* __restrict__ cbase, int* __restrict__ tk,
                                              int64_t tk_stride, float* __restrict__ part,
-                                             float* __restrict__ dpq) {
+                                             float* __restrict__ dpq, uint16_t* __restrict__ dpq3,
+                                             int64_t ps3) {
   const int k = n_chunks(off[u + 1] - off[u]);
   const int64_t cb = cbase[u];
   int64_t g = ci - cb, span = 1, nodes = k;
@@ -803,9 +817,12 @@ __device__ __forceinline__ void dq_tree_leaf(float4 (&acc)[VEC], const float4 (&
       float4* o = reinterpret_cast<float4*>(dpq + (int64_t)u * hid);
 #pragma unroll
       for (int v = 0; v < VEC; ++v)
-        if (v * 64 + lane < h4)
-          o[v * 64 + lane] = make_float4(acc[v].x * lrelu_grad(qv[v].x), acc[v].y * lrelu_grad(qv[v].y),
-                                         acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
+        if (v * 64 + lane < h4) {
+          const float4 r = make_float4(acc[v].x * lrelu_grad(qv[v].x), acc[v].y * lrelu_grad(qv[v].y),
+                                       acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
+          if (PL3) dq_store_planes(dpq3, ps3, (int64_t)u * hid + 4 * (v * 64 + lane), r);
+          else o[v * 64 + lane] = r;
+        }
       return;
     }
     float* node = part + (int64_t)__builtin_amdgcn_readfirstlane((int)(cb + span * g)) * hid;
@@ -815,13 +832,17 @@ __device__ __forceinline__ void dq_tree_leaf(float4 (&acc)[VEC], const float4 (&
   }
 }
 
-template <int VEC, bool CM = false, bool TREE = false>
+// PL3 (with TREE; the bottom layer, where only the Q weight gradient reads
+// dpq): dpq rows are written as hi / mid / lo bf16 planes (dpq3, plane stride
+// ps3) instead of fp32 rows.
+template <int VEC, bool CM = false, bool TREE = false, bool PL3 = false>
 __global__ __launch_bounds__(256) void dq_chunk_kernel(
     const int2* __restrict__ chunks, const int* __restrict__ nchunks, const int2* __restrict__ occ2,
     const float* __restrict__ dagg, int64_t ld_dagg, const float* __restrict__ q, int hid,
     float* __restrict__ dpq, float* __restrict__ part, const int32_t* __restrict__ q_src = nullptr,
     int32_t* __restrict__ csrc = nullptr, const int* __restrict__ off = nullptr,
-    const int* __restrict__ cbase = nullptr, int* __restrict__ tk = nullptr, int64_t tk_stride = 0) {
+    const int* __restrict__ cbase = nullptr, int* __restrict__ tk = nullptr, int64_t tk_stride = 0,
+    uint16_t* __restrict__ dpq3 = nullptr, int64_t ps3 = 0) {
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -839,6 +860,20 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
     // chunk paid a store round trip before its loads could land.
     float4 pend[VEC];
     float4* pend_o = nullptr;
+    int64_t pend_e = -1;  // (PL3) the pending dpq row's first element
+    auto store_pend = [&]() __attribute__((always_inline)) {
+      if (PL3 && pend_e >= 0) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (v * 64 + lane < h4) dq_store_planes(dpq3, ps3, pend_e + 4 * (v * 64 + lane), pend[v]);
+        pend_e = -1;
+      } else if (pend_o) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
+        pend_o = nullptr;
+      }
+    };
     for (int64_t ci = wid; ci < nch; ci += nw) {
       int2 dsc_n = make_int2(0, 0), oc_n = make_int2(0, 0);
       if (ci + nw < nch) {
@@ -866,11 +901,7 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
           }
         }
       }
-      if (pend_o) {  // the previous chunk's result, behind this chunk's loads
-#pragma unroll
-        for (int v = 0; v < VEC; ++v)
-          if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
-      }
+      store_pend();  // the previous chunk's result, behind this chunk's loads
       float4 acc[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -892,13 +923,7 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
         }
       }
       if (TREE && split) {  // this chunk is a leaf of its row's tree (no pending store)
-        if (pend_o) {
-#pragma unroll
-          for (int v = 0; v < VEC; ++v)
-            if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
-          pend_o = nullptr;
-        }
-        dq_tree_leaf<VEC>(acc, qv, u, ci, lane, h4, hid, off, cbase, tk, tk_stride, part, dpq);
+        dq_tree_leaf<VEC, PL3>(acc, qv, u, ci, lane, h4, hid, off, cbase, tk, tk_stride, part, dpq, dpq3, ps3);
         dsc = dsc_n;
         oc = oc_n;
         continue;
@@ -908,15 +933,12 @@ __global__ __launch_bounds__(256) void dq_chunk_kernel(
         pend[v] = split ? acc[v]
                         : make_float4(acc[v].x * lrelu_grad(qv[v].x), acc[v].y * lrelu_grad(qv[v].y),
                                       acc[v].z * lrelu_grad(qv[v].z), acc[v].w * lrelu_grad(qv[v].w));
-      pend_o = reinterpret_cast<float4*>(split ? part + ci * hid : dpq + (int64_t)u * hid);
+      if (PL3 && !split) pend_e = (int64_t)u * hid;
+      else pend_o = reinterpret_cast<float4*>(split ? part + ci * hid : dpq + (int64_t)u * hid);
       dsc = dsc_n;
       oc = oc_n;
     }
-    if (pend_o) {
-#pragma unroll
-      for (int v = 0; v < VEC; ++v)
-        if (v * 64 + lane < h4) pend_o[v * 64 + lane] = pend[v];
-    }
+    store_pend();
     return;
   }
   for (int64_t ci = wid; ci < nch; ci += nw) {
@@ -2012,7 +2034,7 @@ int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks,
                      const int* nsplit, int64_t max_split, const int* off, const int2* occ2,
                      const float* dagg, int64_t ld_dagg, const float* q,
                      int hid, float* dpq, float* part, hipStream_t st, const int32_t* q_src,
-                     int32_t* csrc, const int* cbase, int* tk) {
+                     int32_t* csrc, const int* cbase, int* tk, uint16_t* dpq3, int64_t ps3) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
   // persistent waves (each prefetches its next chunk); 512 to 4096 blocks
   // measured alike at C2 (round 5), 2048 kept
@@ -2032,6 +2054,19 @@ int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks,
   // each XCD gathers its eighth of d_agg from its own L2 -- was bitwise this
   // kernel and slower in the step: C2 0.398-0.406 -> 0.408-0.50 ms, C4
   // 0.426-0.431 -> 0.447-0.452, round 6; removed)
+  if (tk && cbase && hid <= 512 && dpq3) {  // the same, dpq written as bf16 planes
+    if (hid > 256)
+      hipLaunchKernelGGL((dq_chunk_kernel<2, false, true, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks,
+                         occ2, dagg, ld_dagg, q, hid, dpq, part, nullptr, nullptr, off, cbase, tk, max_chunks, dpq3,
+                         ps3);
+    else
+      hipLaunchKernelGGL((dq_chunk_kernel<1, false, true, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks,
+                         occ2, dagg, ld_dagg, q, hid, dpq, part, nullptr, nullptr, off, cbase, tk, max_chunks, dpq3,
+                         ps3);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
+  PS_REQUIRE(!dpq3, kErrArg, "dq: planes output needs the split-row tree and hid <= 512");
   if (tk && cbase && hid <= 512) {  // split rows combined by their own chunks (no combine launch)
     if (hid > 256)
       hipLaunchKernelGGL((dq_chunk_kernel<2, false, true>), dim3(grid), dim3(256), 0, st, chunks, nchunks, occ2,

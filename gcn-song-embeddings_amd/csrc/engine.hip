@@ -58,7 +58,7 @@ int64_t dq_split_capacity(int64_t, int);
 int launch_dq_chunks(const int2*, const int*, int64_t, const int2*, const int*, int64_t, const int*,
                      const int2*, const float*, int64_t, const float*, int, float*, float*, hipStream_t,
                      const int32_t* q_src = nullptr, int32_t* csrc = nullptr, const int* cbase = nullptr,
-                     int* tk = nullptr);
+                     int* tk = nullptr, uint16_t* dpq3 = nullptr, int64_t ps3 = 0);
 int dq_tree_levels(int64_t max_chunks);
 int launch_norm_lrelu_bwd(const float*, const float*, const float*, int, const int*, int64_t,
                           float*, float*, int, const int*, int*, int64_t, hipStream_t);
@@ -109,6 +109,7 @@ struct LayerBuf {
   size_t csrc = 0;  // chunk rows' source indices (bottom layer, Engine::dq_chunk_rows)
   int64_t max_chunks = 0, max_split = 0;
   size_t dqtk = 0;  // split-row tree tickets (dq_tree_levels x max_chunks ints, self-resetting)
+  size_t dpq3 = 0;  // (layer 0, Engine::wgrad_planes) dpq as bf16 planes [3][N.cap][hid]
   int64_t dqtk_len = 0;
   // parameter offsets (floats) into the flat param / grad buffers
   int64_t pQw = 0, pQb = 0, pWw = 0, pWb = 0;
@@ -195,6 +196,18 @@ struct Engine {
   // (three interleaved pairs at C2, ms/step: 0.3949 / 0.3975 / 0.3985 with the
   // combine launch, 0.3872 / 0.3855 / 0.3939 without; C4 even)
   int dq_tree = getenv("PINSAGE_DQ_TREE") ? atoi(getenv("PINSAGE_DQ_TREE")) : 1;
+  // the input feature table as hi / mid / lo bf16 planes [3][n][d_in]
+  // (pinsage_engine_set_feature_planes; null: none): the layer-0 Q weight
+  // gradient then runs on pre-split operands (wgrad_pl_kernel), the
+  // transposed aggregation writing layer 0's dpq as planes too (lb.dpq3)
+  const uint16_t* fplanes = nullptr;
+  int64_t fplanes_ps = 0;
+  // PINSAGE_WGRAD_PLANES=1: carve layer 0's dpq planes buffer so the planes
+  // form can run (default 0: measured no faster -- C2 dQ0 53.4 us fp32 8-wave
+  // form vs 54.0 us on planes, tools/wgrad_bench.py, round 6: the 12-KiB
+  // stages fit only 4 waves x 3 stages in LDS, and the 4-wave fp32 form is
+  // 63.7 us; the split the planes save is ~10 us of it)
+  int wgrad_planes = getenv("PINSAGE_WGRAD_PLANES") ? atoi(getenv("PINSAGE_WGRAD_PLANES")) : 0;
   // a deque: Timed scopes nest and hold pointers to their sites, which must
   // stay valid when an inner scope appends a new site
   std::deque<TimingSite> sites;
@@ -533,6 +546,7 @@ static void layout(Engine& E) {
     lb.nsplit = carve(cur, 16);
     lb.dqtk_len = (int64_t)dq_tree_levels(lb.max_chunks) * lb.max_chunks;
     lb.dqtk = carve(cur, lb.dqtk_len * 4);
+    if (&lb == &E.L[0] && E.wgrad_planes) lb.dpq3 = carve(cur, 3 * FN * c.hid * 2);
   }
   const int64_t top = E.L.back().S.cap;
   E.ids = carve(cur, c.max_pos * 8 + 16);  // + Adam coefficients staged behind the ids
@@ -896,6 +910,11 @@ struct WGrad {
   float* dst = nullptr;
   int64_t ld_dst = 0;
   float* dst_b = nullptr;
+  // pre-split operands (wgrad.hip wgrad_pl_kernel): both set, or neither
+  const uint16_t* A3 = nullptr;
+  int64_t a3_ps = 0;
+  const uint16_t* B3 = nullptr;
+  int64_t b3_ps = 0;
 };
 
 // Adam applied by the gradient reductions (pinsage_engine_backward_adam)
@@ -954,6 +973,10 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
     k.dst = w.dst;
     k.ld_dst = w.ld_dst;
     k.dst_b = w.dst_b;
+    k.A3 = w.A3;
+    k.a3_ps = w.a3_ps;
+    k.B3 = w.B3;
+    k.b3_ps = w.b3_ps;
     if (adam) k.ad = *adam;
     k.slab = slab;
     k.bslab = bslab;
@@ -965,6 +988,7 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
     if (adam && after_use) PS_CHECK_HIP(hipStreamWaitEvent(st, after_use, 0));
     return launch_wgrad_kw(k, st);
   }
+  PS_REQUIRE(!w.A3 && !w.B3, kErrArg, "engine: pre-split operands need the long-K weight-gradient kernel");
   int cfg = 0, S = 1;
   // (a side-stream target of 256 workgroups measured faster at C2 and slower
   // at C4, 128 slower, and a grid cap on side launches even or slower: one
@@ -1226,13 +1250,18 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
       PS_TRY(fork_late(s_w, []() -> int { return kOk; }));
     }
     const bool chunk_rows = l == 0 && E.dq_chunk_rows;
+    // layer 0 on pre-split operands: dpq written as planes, the Q weight
+    // gradient on them and on the feature table's planes (wgrad_pl_kernel)
+    const bool planes = l == 0 && E.fplanes && lb.dpq3 && E.dq_tree && !chunk_rows && hd <= 512 && E.wgrad_kw &&
+                        wgrad_kw_supported(hd, d, -1, false) && (int64_t)(hd / 64) * (d / 64) <= E.kw_cnt_len;
     PS_TRY(launch_dq_chunks(at<int2>(ws, lb.chunks), at<int>(ws, lb.nchunks), lb.max_chunks,
                             at<int2>(ws, lb.split), at<int>(ws, lb.nsplit), lb.max_split,
                             at<int>(ws, lb.off), at<int2>(ws, lb.occ2),
                             at<float>(ws, lb.dagg), hd, at<float>(ws, lb.q), hd, at<float>(ws, lb.dpq),
                             at<float>(ws, lb.dqpart), st, at<int32_t>(ws, lb.q_src),
                             chunk_rows ? at<int32_t>(ws, lb.csrc) : nullptr,
-                            E.dq_tree ? at<int>(ws, lb.cbase) : nullptr, E.dq_tree ? at<int>(ws, lb.dqtk) : nullptr));
+                            E.dq_tree ? at<int>(ws, lb.cbase) : nullptr, E.dq_tree ? at<int>(ws, lb.dqtk) : nullptr,
+                            planes ? at<uint16_t>(ws, lb.dpq3) : nullptr, lb.N.cap * hd));
     PS_TRY(run_pend(E));
     WGrad q_wgrad;
     {
@@ -1252,6 +1281,13 @@ int engine_backward(Engine& E, void* ws, hipStream_t st, const AdamStep* adam, i
       w.dst = gr + lb.pQw;
       w.ld_dst = d;
       w.dst_b = gr + lb.pQb;
+      if (planes) {
+        w.A3 = at<uint16_t>(ws, lb.dpq3);
+        w.a3_ps = lb.N.cap * hd;
+        w.B3 = E.fplanes;
+        w.b3_ps = E.fplanes_ps;
+        w.ldb = d;
+      }
       q_wgrad = w;
     }
     if (l > 0) {
@@ -1477,6 +1513,17 @@ int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, in
     PS_CHECK_HIP(hipMemcpy(&v, at<int>(ws, E->L[l].N.count), 4, hipMemcpyDeviceToHost));
     N[l] = v;
   }
+  return kOk;
+}
+
+int pinsage_engine_set_feature_planes(pinsage_engine* e, const uint16_t* planes, int64_t plane_stride) {
+  if (!e || (planes && plane_stride <= 0)) {
+    set_error("engine_set_feature_planes: bad argument");
+    return kErrArg;
+  }
+  Engine* E = reinterpret_cast<Engine*>(e);
+  E->fplanes = planes;
+  E->fplanes_ps = planes ? plane_stride : 0;
   return kOk;
 }
 

@@ -28,6 +28,14 @@ struct KwParams {
   float* slab = nullptr;
   float* bslab = nullptr;
   int* cnt = nullptr;
+  // pre-split operands (wgrad_pl_kernel): A and B as hi / mid / lo bf16
+  // planes [3][rows][ld] (plane strides a3_ps / b3_ps elements; row strides lda
+  // / ldb elements; B rows gathered by b_idx), the exact split the fp32 form
+  // does in registers, so the products are the same; no B2 segment
+  const uint16_t* A3 = nullptr;
+  int64_t a3_ps = 0;
+  const uint16_t* B3 = nullptr;
+  int64_t b3_ps = 0;
   int S = 0;                  // K splits (0: wgrad_kw_splits)
   int form = 0;               // 0: 8 waves, 128-KiB ring; 1: 4 waves, 64-KiB ring
 };

@@ -52,6 +52,126 @@ __device__ __forceinline__ float4 kw_frag(const float* img, int col, int k4) {
                      img[(k4 + 3) * kKwT + col]);
 }
 
+// The end of a long-K launch (both k-loop forms): the NW wave partials added
+// in wave order, the K splits of the tile combined by the last to arrive (in
+// split order), the bias and the fused Adam step.  smem: the ring (>= NW 64 x
+// 64 floats) followed by >= NW x 64 floats (the bias partials).
+template <int NW>
+__device__ __forceinline__ void kw_finish(const KwParams& p, f32x16 (&acc)[2][2], float bsum, float* smem,
+                                          int ring_floats, int tile, int mb, int s, int m0, int n0,
+                                          bool do_bias) {
+  constexpr int NT = NW * 64;
+  constexpr int E4 = kKwT * kKwT / 4 / NT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int S = p.S;
+  // ---- the NW wave partials, added in wave order
+  float* const part = smem;  // [wave][64 x 64] row-major (the ring is free)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, n = j * 32 + l32;
+        part[wave * kKwT * kKwT + m * kKwT + n] = acc[i][j][r];
+      }
+  float* const bpart = smem + ring_floats;  // [wave][64] (sidx is free)
+  if (do_bias) bpart[wave * kKwT + lane] = bsum;
+  __syncthreads();
+  // this thread's float4s of the tile: e4 = q NT + tid (coalesced rows)
+  float4 v[E4];
+#pragma unroll
+  for (int q = 0; q < E4; ++q) {
+    v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float4 x = *reinterpret_cast<const float4*>(part + w * kKwT * kKwT + 4 * (q * NT + tid));
+      v[q].x += x.x;
+      v[q].y += x.y;
+      v[q].z += x.z;
+      v[q].w += x.w;
+    }
+  }
+  float bv = 0.f;
+  if (do_bias && tid < kKwT)
+#pragma unroll
+    for (int w = 0; w < NW; ++w) bv += bpart[w * kKwT + tid];
+
+  // ---- the splits of this tile, combined by the last to arrive (in split order)
+  if (S > 1) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, 0x7fffffff, 0x00020000);
+    const unsigned so = (unsigned)(((int64_t)tile * S + s) * kKwT * kKwT) * 4u;
+#pragma unroll
+    for (int q = 0; q < E4; ++q) {
+      const v4i w{__float_as_int(v[q].x), __float_as_int(v[q].y), __float_as_int(v[q].z), __float_as_int(v[q].w)};
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, so + (unsigned)(q * NT + tid) * 16u, 0, 16);
+    }
+    if (do_bias && tid < kKwT)
+      __hip_atomic_store(p.bslab + ((int64_t)mb * S + s) * kKwT + tid, bv, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* const flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) flag[0] = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool last = flag[0] == S - 1;
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < E4; ++q) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    bv = 0.f;
+    for (int t = 0; t < S; ++t) {
+      const unsigned o = (unsigned)(((int64_t)tile * S + t) * kKwT * kKwT) * 4u;
+#pragma unroll
+      for (int q = 0; q < E4; ++q) {
+        const v4i y = __builtin_amdgcn_raw_buffer_load_b128(rs, o + (unsigned)(q * NT + tid) * 16u, 0, 16);
+        v[q].x += __int_as_float(y.x);
+        v[q].y += __int_as_float(y.y);
+        v[q].z += __int_as_float(y.z);
+        v[q].w += __int_as_float(y.w);
+      }
+      if (do_bias && tid < kKwT)
+        bv += __hip_atomic_load(p.bslab + ((int64_t)mb * S + t) * kKwT + tid, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // ---- store (and Adam)
+  if (do_bias && tid < kKwT) p.dst_b[m0 + tid] = bv;
+  const bool adam = p.ad.p && p.ad.coef[1] > 0.f;  // (bc2 = 0: a refused step, pinsage_fly_gate_adam)
+  const float ss = adam ? p.ad.coef[0] : 0.f, bc2 = adam ? p.ad.coef[1] : 1.f;
+  const float omb1 = (float)(1.0 - p.ad.beta1), omb2 = (float)(1.0 - p.ad.beta2);
+  const float b2 = (float)p.ad.beta2, eps = p.ad.eps;
+  auto adam1 = [&](float& pp, float g, float& mm, float& vv) {
+    mm = mm + omb1 * (g - mm);
+    vv = vv * b2 + omb2 * g * g;
+    const float denom = sqrtf(vv) / bc2 + eps;
+    pp = pp - ss * (mm / denom);
+  };
+#pragma unroll
+  for (int q = 0; q < E4; ++q) {
+    const int e = 4 * (q * NT + tid);
+    const int64_t o = (int64_t)(m0 + e / kKwT) * p.ld_dst + n0 + (e % kKwT);
+    *reinterpret_cast<float4*>(p.dst + o) = v[q];
+    if (adam) {
+      float4 pp = *reinterpret_cast<const float4*>(p.ad.p + o);
+      float4 mm = *reinterpret_cast<const float4*>(p.ad.m + o);
+      float4 vv = *reinterpret_cast<const float4*>(p.ad.v + o);
+      adam1(pp.x, v[q].x, mm.x, vv.x);
+      adam1(pp.y, v[q].y, mm.y, vv.y);
+      adam1(pp.z, v[q].z, mm.z, vv.z);
+      adam1(pp.w, v[q].w, mm.w, vv.w);
+      *reinterpret_cast<float4*>(p.ad.p + o) = pp;
+      *reinterpret_cast<float4*>(p.ad.m + o) = mm;
+      *reinterpret_cast<float4*>(p.ad.v + o) = vv;
+    }
+  }
+  if (adam && do_bias && tid < kKwT && p.ad.pb) adam1(p.ad.pb[m0 + tid], bv, p.ad.mb[m0 + tid], p.ad.vb[m0 + tid]);
+}
+
 // NW waves, each with an NS-stage private ring (NW * NS * 8 KiB):
 // (8, 2) two waves per SIMD, one stage in flight per wave (128 KiB); (4, 4) one
 // wave per SIMD, three stages in flight (128 KiB); (4, 2) one wave per SIMD, one
@@ -297,111 +417,176 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void wgrad_kw_kernel(KwParams p) {
     __syncthreads();  // (the next pass rewrites sidx; the epilogue reuses the ring)
   }
 
-  // ---- the NW wave partials, added in wave order
-  float* const part = smem;  // [wave][64 x 64] row-major (the ring is free)
+  kw_finish<NW>(p, acc, bsum, smem, kKwRing, tile, mb, s, m0, n0, do_bias);
+}
+
+// ---------------------------------------------------------------- pre-split operands
+// The same long-K weight gradient with both operands already split into hi /
+// mid / lo bf16 planes (the layer-0 Q weight gradient: dpq planes written by
+// the transposed aggregation, the feature table's planes made once): the k
+// loop does no conversions (the split was 16 of the fp32 form's 54 us at C2,
+// tools/wgrad_bench.py PROBE 4).  A stage is 16 k-rows x 64 columns of each of
+// the six planes (12 KiB); 4 waves x 3-stage rings (two stages in flight per
+// wave, as the fp32 form's two waves per SIMD with one each).  The DMA is
+// lane-linear (1 KiB = 8 rows of 128 B per instruction), so a row's 16-B
+// chunks are stored XOR-swizzled (chunk c of row R at c ^ 4 ((R >> 1) & 1)),
+// which makes the ds_read_b64_tr_b16 operand reads bank-conflict free: a
+// 32-lane half reads rows R..R+3, chunks 0..3 -> banks 32 R + 4 c' without
+// repeats.  Each tr read gives a lane 4 k-rows of its column; two give the
+// 8-k half of a 32 x 32 x 16 operand fragment, in the k order the fp32 form
+// splits, so the products -- and with the same wave count the sums -- equal
+// the fp32 form's (4, NS) launch bit for bit.  The bias sums (H + M) + L, the
+// planes' value (within 2^-24 of the fp32 row).
+typedef short kw_s4 __attribute__((ext_vector_type(4)));
+constexpr int kPlImg = kKwBK * kKwT * 2;  // bytes per plane image (2 KiB)
+constexpr int kPlStage = 6 * kPlImg;      // A and B, three planes each (12 KiB)
+constexpr int kPlWin = 2048;              // gathered row numbers staged per pass (8 KiB)
+
+__device__ __forceinline__ bf16x8 kw_tr_frag(unsigned lds_lo, unsigned lds_hi) {
+  const kw_s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) kw_s4*)(size_t)lds_lo);
+  const kw_s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) kw_s4*)(size_t)lds_hi);
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  const s8 v{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int NW, int NS, bool GATHER>
+__global__ __launch_bounds__(NW * 64, 1) void wgrad_pl_kernel(KwParams p) {
+  constexpr int kRing = NW * NS * kPlStage / 4;  // ring floats
+  static_assert(kRing >= NW * kKwT * kKwT, "the wave partials reuse the ring");
+  constexpr int NT = NW * 64;
+  __shared__ __attribute__((aligned(16))) float smem[kRing + kPlWin];
+  int* const sidx = reinterpret_cast<int*>(smem + kRing);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K = p.K_dev ? *p.K_dev : p.K_max;
+  const int tm = p.M / kKwT, tn = p.N / kKwT, S = p.S;
+  const int G = tm * tn * S;
+  const int b = blockIdx.x;  // (the split-major XCD placement of wgrad_kw_kernel)
+  const int L = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+  const int s = L / (tm * tn), t_ = L - s * tm * tn;
+  const int nb = t_ / tm, mb = t_ - nb * tm;
+  const int m0 = mb * kKwT, n0 = nb * kKwT;
+  const int tile = nb * tm + mb;
+  const int kc = ((K + S - 1) / S + kKwBK - 1) / kKwBK * kKwBK;
+  const int kb = min(K, s * kc), ke = min(K, kb + kc);
+  const bool do_bias = p.dst_b && nb == 0;
+  const unsigned smem_lds = (unsigned)(size_t)((__attribute__((address_space(3))) float*)smem);
+  const unsigned ring_w = smem_lds + (unsigned)(wave * NS * kPlStage);
+  char* const ring_g = reinterpret_cast<char*>(smem) + wave * NS * kPlStage;
+  // DMA: lane -> row 8 j + dR of the stage, physical chunk lane & 7 (logical dcol / 8)
+  const int dR = lane >> 3;
+  const int dcol = 8 * ((lane & 7) ^ (4 * ((dR >> 1) & 1)));
+  // tr reads: lane (group g, row q, quad pp) addresses row kq + 4 t + q, columns
+  // 32 i + mq + 4 pp; the byte offsets within a plane image for t, i
+  unsigned toff[2][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int kq = 8 * (g >> 1), mq = 16 * (g & 1) + 4 * pp;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int R = kq + 4 * t + q, col = 32 * i + mq;
+        toff[t][i] = (unsigned)(R * 128 + (((col >> 3) ^ (4 * ((R >> 1) & 1))) << 4) + ((col & 7) << 1));
+      }
+  }
+  f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, n = j * 32 + l32;
-        part[wave * kKwT * kKwT + m * kKwT + n] = acc[i][j][r];
-      }
-  float* const bpart = smem + kKwRing;  // [wave][64] (sidx is free)
-  if (do_bias) bpart[wave * kKwT + lane] = bsum;
-  __syncthreads();
-  // this thread's float4s of the tile: e4 = q NT + tid (coalesced rows)
-  float4 v[E4];
-#pragma unroll
-  for (int q = 0; q < E4; ++q) {
-    v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const float4 x = *reinterpret_cast<const float4*>(part + w * kKwT * kKwT + 4 * (q * NT + tid));
-      v[q].x += x.x;
-      v[q].y += x.y;
-      v[q].z += x.z;
-      v[q].w += x.w;
-    }
-  }
-  float bv = 0.f;
-  if (do_bias && tid < kKwT)
-#pragma unroll
-    for (int w = 0; w < NW; ++w) bv += bpart[w * kKwT + tid];
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float bs2[2] = {0.f, 0.f};  // bias partials of columns 32 i + (lane & 31), k half lane >> 5
 
-  // ---- the splits of this tile, combined by the last to arrive (in split order)
-  if (S > 1) {
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, 0x7fffffff, 0x00020000);
-    const unsigned so = (unsigned)(((int64_t)tile * S + s) * kKwT * kKwT) * 4u;
-#pragma unroll
-    for (int q = 0; q < E4; ++q) {
-      const v4i w{__float_as_int(v[q].x), __float_as_int(v[q].y), __float_as_int(v[q].z), __float_as_int(v[q].w)};
-      __builtin_amdgcn_raw_buffer_store_b128(w, rs, so + (unsigned)(q * NT + tid) * 16u, 0, 16);
+  for (int pb = kb; pb < ke; pb += kPlWin) {
+    const int pe = min(ke, pb + kPlWin);
+    if constexpr (GATHER) {
+      for (int i = tid; i < pe - pb; i += NT) sidx[i] = p.b_idx[pb + i];
+      __syncthreads();
     }
-    if (do_bias && tid < kKwT)
-      __hip_atomic_store(p.bslab + ((int64_t)mb * S + s) * kKwT + tid, bv, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* const flag = reinterpret_cast<int*>(smem);
-    if (tid == 0) flag[0] = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const bool last = flag[0] == S - 1;
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int ns = (pe - pb + kKwBK - 1) / kKwBK;
+    const int nw = ns > wave ? (ns - wave + NW - 1) / NW : 0;
+    int nxt[2];
+    auto fetch_rows = [&](int it) __attribute__((always_inline)) {
+      const int k0 = pb + kKwBK * (wave + NW * it);
 #pragma unroll
-    for (int q = 0; q < E4; ++q) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    bv = 0.f;
-    for (int t = 0; t < S; ++t) {
-      const unsigned o = (unsigned)(((int64_t)tile * S + t) * kKwT * kKwT) * 4u;
-#pragma unroll
-      for (int q = 0; q < E4; ++q) {
-        const v4i y = __builtin_amdgcn_raw_buffer_load_b128(rs, o + (unsigned)(q * NT + tid) * 16u, 0, 16);
-        v[q].x += __int_as_float(y.x);
-        v[q].y += __int_as_float(y.y);
-        v[q].z += __int_as_float(y.z);
-        v[q].w += __int_as_float(y.w);
+      for (int j = 0; j < 2; ++j) {
+        const int k = min(k0 + 8 * j + dR, pe - 1);
+        nxt[j] = GATHER ? sidx[k - pb] : k;
       }
-      if (do_bias && tid < kKwT)
-        bv += __hip_atomic_load(p.bslab + ((int64_t)mb * S + t) * kKwT + tid, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-
-  // ---- store (and Adam)
-  if (do_bias && tid < kKwT) p.dst_b[m0 + tid] = bv;
-  const bool adam = p.ad.p && p.ad.coef[1] > 0.f;  // (bc2 = 0: a refused step, pinsage_fly_gate_adam)
-  const float ss = adam ? p.ad.coef[0] : 0.f, bc2 = adam ? p.ad.coef[1] : 1.f;
-  const float omb1 = (float)(1.0 - p.ad.beta1), omb2 = (float)(1.0 - p.ad.beta2);
-  const float b2 = (float)p.ad.beta2, eps = p.ad.eps;
-  auto adam1 = [&](float& pp, float g, float& mm, float& vv) {
-    mm = mm + omb1 * (g - mm);
-    vv = vv * b2 + omb2 * g * g;
-    const float denom = sqrtf(vv) / bc2 + eps;
-    pp = pp - ss * (mm / denom);
-  };
+    };
+    auto issue = [&](int it) __attribute__((always_inline)) {
+      const int k0 = pb + kKwBK * (wave + NW * it);
+      const unsigned img = ring_w + (unsigned)((it % NS) * kPlStage);
 #pragma unroll
-  for (int q = 0; q < E4; ++q) {
-    const int e = 4 * (q * NT + tid);
-    const int64_t o = (int64_t)(m0 + e / kKwT) * p.ld_dst + n0 + (e % kKwT);
-    *reinterpret_cast<float4*>(p.dst + o) = v[q];
-    if (adam) {
-      float4 pp = *reinterpret_cast<const float4*>(p.ad.p + o);
-      float4 mm = *reinterpret_cast<const float4*>(p.ad.m + o);
-      float4 vv = *reinterpret_cast<const float4*>(p.ad.v + o);
-      adam1(pp.x, v[q].x, mm.x, vv.x);
-      adam1(pp.y, v[q].y, mm.y, vv.y);
-      adam1(pp.z, v[q].z, mm.z, vv.z);
-      adam1(pp.w, v[q].w, mm.w, vv.w);
-      *reinterpret_cast<float4*>(p.ad.p + o) = pp;
-      *reinterpret_cast<float4*>(p.ad.m + o) = mm;
-      *reinterpret_cast<float4*>(p.ad.v + o) = vv;
+      for (int j = 0; j < 2; ++j) {
+        const int k = min(k0 + 8 * j + dR, pe - 1);
+#pragma unroll
+        for (int P = 0; P < 3; ++P)
+          glds16(reinterpret_cast<const float*>(p.A3 + P * p.a3_ps + (int64_t)k * p.lda + m0 + dcol),
+                 img + (unsigned)(P * kPlImg + j * 1024));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int P = 0; P < 3; ++P)
+          glds16(reinterpret_cast<const float*>(p.B3 + P * p.b3_ps + (int64_t)nxt[j] * p.ldb + n0 + dcol),
+                 img + (unsigned)((3 + P) * kPlImg + j * 1024));
+    };
+    for (int st = 0; st < NS - 1 && st < nw; ++st) {
+      fetch_rows(st);
+      issue(st);
     }
+    if (NS - 1 < nw) fetch_rows(NS - 1);
+    for (int it = 0; it < nw; ++it) {
+      wait_stage<12, NS - 2 >= 1 ? NS - 2 : 1>(min(NS - 2, nw - 1 - it));
+      if (it + NS - 1 < nw) {
+        issue(it + NS - 1);
+        if (it + NS < nw) fetch_rows(it + NS);
+      }
+      const unsigned stg = ring_w + (unsigned)((it % NS) * kPlStage);
+      const int k0 = pb + kKwBK * (wave + NW * it);
+      if (k0 + kKwBK > pe) {  // k-tail: A rows past the pass end contribute nothing
+        char* const sg = ring_g + (it % NS) * kPlStage;
+        for (int r = pe - k0; r < kKwBK; ++r)
+#pragma unroll
+          for (int P = 0; P < 3; ++P) reinterpret_cast<uint16_t*>(sg + P * kPlImg + r * 128)[lane] = 0;
+      }
+      bf16x8 aX[3][2], bX[3][2];
+#pragma unroll
+      for (int P = 0; P < 3; ++P)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          aX[P][i] = kw_tr_frag(stg + P * kPlImg + toff[0][i], stg + P * kPlImg + toff[1][i]);
+          bX[P][i] = kw_tr_frag(stg + (3 + P) * kPlImg + toff[0][i], stg + (3 + P) * kPlImg + toff[1][i]);
+        }
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            bs2[i] += ((float)aX[0][i][e] + (float)aX[1][i][e]) + (float)aX[2][i][e];
+      }
+#define PS_PL_ALL(X, Y)                                                                            \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aX[X][i], bX[Y][j], acc[i][j], 0, 0, 0);
+      PS_PL_ALL(2, 0)  // (the fp32 form's order: lo hi, hi lo, mid mid, mid hi, hi mid, hi hi)
+      PS_PL_ALL(0, 2)
+      PS_PL_ALL(1, 1)
+      PS_PL_ALL(1, 0)
+      PS_PL_ALL(0, 1)
+      PS_PL_ALL(0, 0)
+#undef PS_PL_ALL
+#pragma unroll
+      for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(nxt[j]));
+    }
+    __syncthreads();
   }
-  if (adam && do_bias && tid < kKwT && p.ad.pb) adam1(p.ad.pb[m0 + tid], bv, p.ad.mb[m0 + tid], p.ad.vb[m0 + tid]);
+  // bias partials to the fp32 form's layout: lane l holds column l
+  const float v0 = bs2[0] + __shfl_xor(bs2[0], 32, 64), v1 = bs2[1] + __shfl_xor(bs2[1], 32, 64);
+  const float bsum = lane < 32 ? v0 : v1;
+  kw_finish<NW>(p, acc, bsum, smem, kRing, tile, mb, s, m0, n0, do_bias);
 }
 
 // ---------------------------------------------------------------- host side
@@ -426,7 +611,7 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   KwParams p = p_in;
   PS_REQUIRE(wgrad_kw_supported(p.M, p.N, p.N1, p.B2 != nullptr), kErrArg,
              "wgrad: M, N (and N1) must be multiples of 64");
-  PS_REQUIRE(p.A && p.B && p.dst && p.lda % 4 == 0 && p.ldb % 4 == 0 && (!p.B2 || p.ldb2 % 4 == 0) &&
+  PS_REQUIRE((p.A || p.A3) && (p.B || p.B3) && p.dst && p.lda % 4 == 0 && p.ldb % 4 == 0 && (!p.B2 || p.ldb2 % 4 == 0) &&
                  p.ld_dst % 4 == 0 && p.K_max >= 0,
              kErrArg, "wgrad: operands and 16-B aligned row strides");
   PS_REQUIRE(!p.ad.p || (p.ad.m && p.ad.v && p.ad.coef && (!p.dst_b || (p.ad.pb && p.ad.mb && p.ad.vb))),
@@ -439,6 +624,14 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   const int waves = getenv("PINSAGE_KW_WAVES") ? atoi(getenv("PINSAGE_KW_WAVES")) : 8;  // (per call: A/B)
   const int probe = getenv("PINSAGE_KW_PROBE") ? atoi(getenv("PINSAGE_KW_PROBE")) : 0;  // (read per call)
   const bool gather = p.b_idx || p.b2_idx;
+  if (p.A3 || p.B3) {  // pre-split operands
+    PS_REQUIRE(p.A3 && p.B3 && !p.B2 && p.lda % 8 == 0 && p.ldb % 8 == 0, kErrArg,
+               "wgrad: pre-split A and B planes (no B2 segment), row strides multiples of 8");
+    if (p.b_idx) hipLaunchKernelGGL((wgrad_pl_kernel<4, 3, true>), dim3(grid), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((wgrad_pl_kernel<4, 3, false>), dim3(grid), dim3(256), 0, st, p);
+    PS_CHECK_LAUNCH();
+    return kOk;
+  }
   // PINSAGE_KW_FORM (tests / microbenchmarks through the C-ABI): the form of a
   // launch whose caller did not choose one
   if (p.form == 0 && getenv("PINSAGE_KW_FORM")) p.form = atoi(getenv("PINSAGE_KW_FORM"));

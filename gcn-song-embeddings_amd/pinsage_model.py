@@ -964,6 +964,30 @@ class _EngineRunner:
             self._ws = None
         return self.engine
 
+    def feature_planes(self, feats):
+        """The feature table's hi / mid / lo bf16 planes [3, n, d] (pinsage_split_planes)
+        for the layer-0 Q weight gradient on pre-split operands, re-split whenever
+        the tensor changes (torch's version counter counts in-place writes); None
+        unless enabled (PINSAGE_WGRAD_PLANES=1; off by default: measured no faster,
+        DESIGN.md round 6), for shapes the kernel does not take,
+        or when the planes would exceed PINSAGE_FPLANES_MAX_GB (default 32: C5's
+        80M x 256 table stays on the in-register split)."""
+        if os.environ.get("PINSAGE_WGRAD_PLANES", "0") != "1" or feats.dim() != 2:
+            return None
+        n, d = int(feats.shape[0]), int(feats.shape[1])
+        limit = float(os.environ.get("PINSAGE_FPLANES_MAX_GB", "32")) * 2 ** 30
+        if d % 64 or feats.stride(1) != 1 or feats.stride(0) % 4 or 6.0 * n * d > limit:
+            return None
+        key = (feats.data_ptr(), n, d, feats.stride(0), feats._version)
+        if getattr(self, "_fpl_key", None) != key:
+            pl = getattr(self, "_fpl", None)
+            if pl is None or tuple(pl.shape) != (3, n, d) or pl.device != feats.device:
+                pl = self._fpl = torch.empty((3, n, d), dtype=torch.int16, device=feats.device)
+            nat.check(nat.lib().pinsage_split_planes(nat.ptr(feats), n, d, feats.stride(0), nat.ptr(pl),
+                                                     nat.stream_ptr()), "split_planes")
+            self._fpl_key = key
+        return self._fpl
+
     def bind(self, feats, table, grads=None, adam_m=None, adam_v=None, tabs=None):
         e = self.engine
         if table is not None:
@@ -974,6 +998,9 @@ class _EngineRunner:
             e.h, nat.ptr(feats), feats.stride(0), nat.ptr(nb), nat.ptr(wn),
             nb.shape[1], nat.ptr(self.flat), nat.ptr(grads), nat.ptr(adam_m),
             nat.ptr(adam_v)), "engine_set_tensors")
+        pl = self.feature_planes(feats)
+        nat.check(nat.lib().pinsage_engine_set_feature_planes(e.h, nat.ptr(pl), pl[0].numel() if pl is not None else 0),
+                  "engine_set_feature_planes")
 
     def run_forward(self, ws, ids_dev, inference=False):
         e = self.engine

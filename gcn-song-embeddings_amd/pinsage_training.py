@@ -896,6 +896,9 @@ class _FusedStep:
             self._drop_stepper()
         if self.graphs is not None and getattr(self, "stepper", None) is not None:
             self.ws = self.wss[self.parity]
+            # (the planes the graphs read: re-split in place if the features were
+            # written in place since; a moved tensor changed the signature above)
+            r.feature_planes(feats)
             _tick("pre")
             return self._call_native(batch, B)  # (the captured graphs hold every pointer: no bind)
         r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)

@@ -242,6 +242,16 @@ int pinsage_wgrad(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const f
                   float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, float* adam_p,
                   float* adam_m, float* adam_v, float* adam_pb, float* adam_mb, float* adam_vb,
                   const float* coef, double beta1, double beta2, float eps, void* stream);
+/* The same weight gradient with both operands given as their hi / mid / lo
+ * bf16 planes (pinsage_split_planes: A3 [3][K][M], B3 [3][rows][N] with plane
+ * strides a3_ps / b3_ps and row strides lda / ldb elements, B rows gathered
+ * by b_idx): no conversions in the k loop.  Weights are bitwise the fp32
+ * form's 4-wave launch (PINSAGE_KW_WAVES=4) on the planes' source matrices;
+ * dst_b sums the planes' value (H + M) + L.  The layer-0 Q weight gradient
+ * (pinsage_model.py:201's AddmmBackward) in the engine. */
+int pinsage_wgrad_planes(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const uint16_t* A3, int64_t a3_ps,
+                         int64_t lda, const uint16_t* B3, int64_t b3_ps, int64_t ldb, const int32_t* b_idx,
+                         float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, void* stream);
 int pinsage_gemm_ex(int64_t M, int64_t N, int64_t K, int a_kmajor, int b_kmajor, const float* A,
                     int64_t lda, const int32_t* a_idx, const float* B, int64_t ldb,
                     const int32_t* b_idx, float* C, int64_t ldc, const float* bias, int act,
@@ -461,6 +471,16 @@ int pinsage_engine_offsets(const pinsage_engine* e, pinsage_engine_offsets_t* ou
 int pinsage_engine_set_tensors(pinsage_engine* e, const float* feats, int64_t ld_feats,
                                const int32_t* nb_table, const float* w_table, int64_t ld_table,
                                float* params, float* grads, float* adam_m, float* adam_v);
+/* The input feature table's hi / mid / lo bf16 planes [3][n][d_in] (from
+ * pinsage_split_planes(feats, n, d_in, ld_feats, planes); plane stride in
+ * elements), or null: with them the layer-0 Q weight gradient
+ * (pinsage_model.py:201's AddmmBackward) runs on pre-split operands -- the
+ * transposed aggregation writes layer 0's dpq as planes too -- and does no
+ * conversions; the result's weights are those of the fp32 form's 4-wave
+ * launch.  The caller keeps the planes equal to the split of the features the
+ * engine reads (pinsage_model.Runner.bind re-splits when the tensor's version
+ * changes). */
+int pinsage_engine_set_feature_planes(pinsage_engine* e, const uint16_t* planes, int64_t plane_stride);
 /* Zero the workspace regions the step kernels keep zero after use (loss
  * scatter targets, CSR counters).  Call once per new workspace, before its
  * first forward. */

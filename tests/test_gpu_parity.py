@@ -399,7 +399,8 @@ def test_frontier_ahead_matches_serial_step(mode):
 @pytest.mark.parametrize("var,a,b", [("PINSAGE_DEFER_SIDE", "0", "3"), ("PINSAGE_DQ_CHUNK_ROWS", "0", "1"),
                                      ("PINSAGE_FUSED_NEXT_Q", "0", "1"), ("PINSAGE_HEAD_IN_AGGW", "0", "1"),
                                      ("PINSAGE_FORK_PLAN", "0", "7"), ("PINSAGE_FORK_PLAN", "0", "3"),
-                                     ("PINSAGE_KW_SIDE_FORM", "0", "1"), ("PINSAGE_DQ_TREE", "0", "1")])
+                                     ("PINSAGE_KW_SIDE_FORM", "0", "1"), ("PINSAGE_DQ_TREE", "0", "1"),
+                                     ("PINSAGE_WGRAD_PLANES", "0", "1")])
 def test_engine_variants_train_alike(var, a, b, monkeypatch):
     """Engine variants that change only launch order or summation order train
     alike -- same published losses (the monitors' output) and parameters within
@@ -416,7 +417,9 @@ def test_engine_variants_train_alike(var, a, b, monkeypatch):
     so bitwise) and PINSAGE_KW_SIDE_FORM (the side weight gradients as 4-wave
     workgroups: another wave-partial order) and PINSAGE_DQ_TREE (split dq rows
     summed by their chunk waves as a fan-in-8 tree instead of dq_combine's
-    strided wave sums)."""
+    strided wave sums) and PINSAGE_WGRAD_PLANES (the layer-0 Q weight
+    gradient on pre-split bf16 planes of dpq and of the features: the same
+    products, 4-wave partial order)."""
     if var != "PINSAGE_HEAD_IN_AGGW":  # (the head is fused into the 16-row form only)
         monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
     import graph

@@ -378,10 +378,11 @@ def test_step_capture_with_forked_csr_branch(fork, monkeypatch):
     import graph
     import pinsage_training as pt
     import synthetic
-    if os.environ.get("PINSAGE_SEGV_BT") == "1":  # (diagnostics: native backtrace of a host crash)
-        import ctypes
-        ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "dbg",
-                                 "segv_bt.so")).install()
+    def segv_bt():  # (diagnostics: native backtrace of a host crash; installed once HIP is up)
+        if os.environ.get("PINSAGE_SEGV_BT") == "1":
+            import ctypes
+            ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "dbg",
+                                     "segv_bt.so")).install()
     pg = synthetic.make_playlist_graph(3000, 600, 20000, seed=71)
     indptr, indices = pg.csr()
     feats = torch.from_numpy(synthetic.make_features(3000, 128, seed=72))
@@ -411,6 +412,7 @@ def test_step_capture_with_forked_csr_branch(fork, monkeypatch):
                 return losses, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).cpu()
 
             l0, p0 = run(0)
+            segv_bt()
             l1, p1 = run(fork)
             assert l0 == l1, (l0, l1)
             assert torch.equal(p0, p1), (p0 - p1).abs().max().item()

@@ -144,3 +144,55 @@ def test_wgrad_fused_adam_matches_torch():
            adam=dict(p=P2, m=M2, v=V2, pb=Pb.clone(), mb=Mb.clone(), vb=Vb.clone(), coef=coef))
     torch.cuda.synchronize()
     assert torch.equal(P2, P) and torch.equal(M2, Mo) and torch.equal(V2, V)
+
+
+def _planes(X):
+    """hi / mid / lo bf16 planes of a row-major fp32 matrix (pinsage_split_planes)."""
+    import _native as nat
+    R, C = X.shape
+    out = torch.empty((3, R, C), dtype=torch.int16, device="cuda")
+    nat.check(nat.lib().pinsage_split_planes(_vp(X), R, C, X.stride(0), _vp(out),
+                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+              "split_planes")
+    return out
+
+
+@pytest.mark.parametrize("M,N,K,R", [(512, 512, 3001, 5000), (512, 128, 5000, 20000), (512, 256, 40, 100),
+                                     (128, 128, 2345, 0)])
+def test_wgrad_planes_equal_fp32_form_bitwise(M, N, K, R, monkeypatch):
+    """pinsage_wgrad_planes (both operands pre-split, no conversions in the k
+    loop: the engine's layer-0 Q weight gradient) gives the fp32 form's 4-wave
+    launch bit for bit -- the planes hold exactly the in-register split, the
+    products and the per-wave stage order are the same -- over gathered and
+    ungathered B rows, ragged K and a K tail inside a 2048-row pass; the bias
+    (summed from the planes' value) within 2^-22 of it, and both against
+    float64."""
+    import _native as nat
+    lib = nat.lib()
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn((K + 16, M), device="cuda", generator=g)
+    A *= torch.exp2(torch.randint(-10, 10, (K + 16, 1), device="cuda", generator=g).float())
+    B = torch.randn((R if R else K + 16, N), device="cuda", generator=g)
+    b_idx = torch.randint(0, R, (K + 16,), device="cuda", generator=g, dtype=torch.int32) if R else None
+    K_dev = torch.tensor([K], dtype=torch.int32, device="cuda")
+    A3, B3 = _planes(A), _planes(B)
+    Bf = B.double()[b_idx[:K].long()] if R else B.double()[:K]
+    ref = A.double()[:K].t() @ Bf
+    ref_b = A.double()[:K].sum(0)
+    for splits in (0, 1, 3):
+        monkeypatch.setenv("PINSAGE_KW_WAVES", "4")
+        dst = torch.full((M, N), float("nan"), device="cuda")
+        db = torch.full((M,), float("nan"), device="cuda")
+        _wgrad(M, N, K_dev, K + 16, A, B, b_idx, dst, db, splits=splits)
+        monkeypatch.delenv("PINSAGE_KW_WAVES")
+        dp = torch.full((M, N), float("nan"), device="cuda")
+        dbp = torch.full((M,), float("nan"), device="cuda")
+        sc = _Scratch(M, N)
+        nat.check(lib.pinsage_wgrad_planes(M, N, _vp(K_dev), K + 16, _vp(A3), A3[0].numel(), M, _vp(B3),
+                                           B3[0].numel(), N, _vp(b_idx), _vp(dp), N, _vp(dbp), splits, _vp(sc.buf),
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                  "wgrad_planes")
+        torch.cuda.synchronize()
+        assert torch.equal(dp, dst), (splits, (dp - dst).abs().max().item())
+        assert ((dbp - db).abs() <= 2.0 ** -22 * A[:K].abs().sum(0)).all(), splits
+        assert _rel(dp, ref) < 2e-6 and _rel(dbp, ref_b) < 2e-6

@@ -237,7 +237,63 @@ static int run_stale(const std::string& c) {
   return 0;
 }
 
+// The join of a fork AFTER the origin advanced (engine_frontier with
+// PINSAGE_CSR_FORK=2: fork, the CSR builds on the origin, then the empty
+// side joined back -- the join adds an edge from an ancestor of the origin's
+// last node).  nested_advanced_*: the same inside a branch S of A.
+static int run_advanced(const std::string& c) {
+  int* d = nullptr;
+  if (hipMalloc(&d, 64) != hipSuccess) return 90;
+  hipMemset(d, 0, 64);
+  hipStream_t A, S, B;
+  for (hipStream_t* x : {&A, &S, &B}) hipStreamCreateWithFlags(x, hipStreamNonBlocking);
+  hipEvent_t e[6];
+  for (auto& x : e) hipEventCreateWithFlags(&x, hipEventDisableTiming);
+  const bool nested = c.rfind("nested", 0) == 0, empty = c.find("empty") != std::string::npos;
+  hipGraph_t g = nullptr;
+  hipStreamBeginCapture(A, hipStreamCaptureModeGlobal);
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+  hipStream_t O = A;
+  if (nested) {
+    hipEventRecord(e[0], A);
+    hipStreamWaitEvent(S, e[0], 0);
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, S, d + 4);
+    O = S;
+  }
+  hipEventRecord(e[1], O);
+  hipStreamWaitEvent(B, e[1], 0);
+  if (!empty) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, B, d + 8);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, O, d + 4);
+  hipEventRecord(e[2], B);
+  hipError_t r = hipStreamWaitEvent(O, e[2], 0);
+  printf("[%s] join %s\n", c.c_str(), hipGetErrorName(r));
+  if (c.find("tail") == std::string::npos) hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, O, d + 4);
+  if (nested) {
+    hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+    hipEventRecord(e[3], S);
+    hipStreamWaitEvent(A, e[3], 0);
+  }
+  hipLaunchKernelGGL(tick, dim3(1), dim3(64), 0, A, d);
+  fflush(stdout);
+  r = hipStreamEndCapture(A, &g);
+  printf("[%s] end capture %s graph %p\n", c.c_str(), hipGetErrorName(r), (void*)g);
+  fflush(stdout);
+  if (r == hipSuccess && g) {
+    hipGraphExec_t x;
+    r = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    printf("[%s] instantiate %s\n", c.c_str(), hipGetErrorName(r));
+    if (r == hipSuccess) r = hipGraphLaunch(x, A);
+    hipStreamSynchronize(A);
+    int h[16];
+    hipMemcpy(h, d, 64, hipMemcpyDeviceToHost);
+    printf("[%s] replay %s counters %d %d %d\n", c.c_str(), hipGetErrorName(r), h[0], h[4], h[8]);
+  }
+  fflush(stdout);
+  return 0;
+}
+
 static int run_case(const std::string& c) {
+  if (c.find("advanced") != std::string::npos) return run_advanced(c);
   if (c.rfind("stale", 0) == 0) return run_stale(c);
   if (c.rfind("reuse_nested", 0) == 0) return run_reuse_nested(c);
   if (c.rfind("nested", 0) == 0) return run_nested(c);
@@ -305,7 +361,9 @@ int main(int argc, char** argv) {
                          "reuse_after_joined", "reuse_after_unjoined_empty",
                          "nested_separate", "nested_kernel", "nested_empty",
                          "reuse_nested_kernel", "reuse_nested_empty", "reuse_nested_fresh",
-                         "nested_empty_tail", "nested_kernel_tail", "stale_kernel", "stale_empty"};
+                         "nested_empty_tail", "nested_kernel_tail", "stale_kernel", "stale_empty",
+                         "advanced_empty", "advanced_kernel", "nested_advanced_empty", "nested_advanced_kernel",
+                         "nested_advanced_empty_tail", "nested_advanced_kernel_tail"};
   if (argc > 1) return run_case(argv[1]);
   for (const char* c : cases) {
     fflush(stdout);

@@ -84,6 +84,16 @@ def main():
                 (N - n1) if B2 is not None else 0, vp(dst), N, vp(db), 0, vp(sc), None, None, None, None, None,
                 None, None, 0.9, 0.999, 1e-8, st), "wgrad"), a.reps)
             os.environ.pop("PINSAGE_KW_PROBE")
+        if n1 == N:  # both operands pre-split (pinsage_wgrad_planes)
+            A3 = torch.empty((3, A.shape[0], M), dtype=torch.int16, device="cuda")
+            B3 = torch.empty((3, B.shape[0], N), dtype=torch.int16, device="cuda")
+            nat.check(L.pinsage_split_planes(vp(A), A.shape[0], M, M, vp(A3), st), "split")
+            nat.check(L.pinsage_split_planes(vp(B), B.shape[0], N, N, vp(B3), st), "split")
+            for S in (0, 4, 8):
+                res[f"planes S={S or 'auto'}"] = timed(lambda: nat.check(L.pinsage_wgrad_planes(
+                    M, N, vp(K_dev), K, vp(A3), A3[0].numel(), M, vp(B3), B3[0].numel(), N, vp(idx), vp(dst), N,
+                    vp(db), S, vp(sc), st), "wgrad_planes"), a.reps)
+            del A3, B3
         flops = 2.0 * M * N * K
         print(name, {k: f"{v:.1f} us {flops / v / 1e6:.0f} TF/s" for k, v in res.items()}, flush=True)
 
