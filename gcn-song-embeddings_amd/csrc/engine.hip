@@ -180,6 +180,12 @@ struct Engine {
   // which side stream the frontier forks: 2 (default, its own), or 0 (the
   // backward's side[0]: the round-5 shape, kept for tools/dbg reproduction)
   int csr_fork_stream = getenv("PINSAGE_CSR_FORK_STREAM") ? atoi(getenv("PINSAGE_CSR_FORK_STREAM")) : 2;
+  // pinsage_engine_set_frontier_fork(e, 0): the next frontiers do not fork
+  // (a caller running the frontier on a branch of a graph being captured:
+  // forking the engine's stream off a capture branch -- not the capture's
+  // origin -- made hipStreamEndCapture recurse without end, DESIGN.md §5
+  // round 6; and a branch already off the critical path gains nothing from it)
+  int frontier_fork_ok = 1;
   // PINSAGE_WGRAD_KW: weight gradients by the long-K kernel (wgrad.hip: 64 x 64
   // tiles, few splits combined inside the launch, Adam fused) instead of the
   // split-K GEMM + reduce_slabs_2d; 1 (default) every site it supports, 0 none
@@ -710,14 +716,15 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
   // after the index tables the CSR builds read; the join below is recorded on
   // side[0] after its last launch and waited on st before this call returns
   hipStream_t s_fk = st;
-  if (E.csr_fork) {
+  const int csr_fork = E.frontier_fork_ok ? E.csr_fork : 0;
+  if (csr_fork) {
     PS_TRY(ensure_streams(E));
     s_fk = E.side[std::min(std::max(E.csr_fork_stream, 0), 2)];
     PS_TRY(dep(E, st, s_fk));
   }
   for (int l = Lc - 1; l >= 0; --l) {
     LayerBuf& lb = E.L[(size_t)l];
-    hipStream_t sl = (E.csr_fork == 1 && l == 0) ? s_fk : st;
+    hipStream_t sl = (csr_fork == 1 && l == 0) ? s_fk : st;
     Timed tc(E, lname("fwd.csr", l), sl);
     PS_TRY(launch_csr_build(at<int32_t>(ws, lb.loc), at<float>(ws, lb.wloc), cnt(lb.S), lb.S.cap, T, cnt(lb.N),
                             lb.N.cap, at<int>(ws, lb.cnt), at<int>(ws, lb.bsum), at<int>(ws, lb.off),
@@ -726,7 +733,7 @@ int engine_frontier(Engine& E, void* ws, const int64_t* ids_dev, int64_t n_pos, 
                             at<int>(ws, lb.nsplit), at<float>(ws, lb.dpq), (int)c.hid, sl,
                             at<int2>(ws, lb.occ2b)));
   }
-  if (E.csr_fork) PS_TRY(dep(E, s_fk, st));  // join: nothing of this call stays on side[0]
+  if (csr_fork) PS_TRY(dep(E, s_fk, st));  // join: nothing of this call stays on side[0]
   return kOk;
 }
 
@@ -790,7 +797,11 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     if (l == 0 && E.fork.stream) {  // the next batch's frontier beside the rest of the step
       PS_TRY(ensure_streams(E));
       PS_TRY(dep(E, st, E.fork.stream));
-      PS_TRY(engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream));
+      const int ok = E.frontier_fork_ok;
+      E.frontier_fork_ok = 0;  // (no fork off this branch: frontier_fork_ok)
+      const int rc = engine_frontier(E, E.fork.ws, E.fork.ids, E.fork.n, E.fork.stream);
+      E.frontier_fork_ok = ok;
+      PS_TRY(rc);
     }
     if (E.fused_aggw && agg_w_supported(lb.d, c.hid, c.out, T)) {
       // aggregation + [h_self || agg] W^T + bias, lrelu, row L2 norm in one launch
@@ -1513,6 +1524,15 @@ int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, in
     PS_CHECK_HIP(hipMemcpy(&v, at<int>(ws, E->L[l].N.count), 4, hipMemcpyDeviceToHost));
     N[l] = v;
   }
+  return kOk;
+}
+
+int pinsage_engine_set_frontier_fork(pinsage_engine* e, int on) {
+  if (!e) {
+    set_error("engine_set_frontier_fork: null engine");
+    return kErrArg;
+  }
+  reinterpret_cast<Engine*>(e)->frontier_fork_ok = on != 0;
   return kOk;
 }
 

@@ -705,11 +705,20 @@ class _FusedStep:
         adam = not self.dist
         staged = self.dist and self.dp_buckets  # DP: backward stage 1 in its own graph (g2)
         stage = 0 if staged else None
+        # The look-ahead branch's stream is used once here, eagerly: torch's stream
+        # pool creates a slot's HIP stream lazily, at its first use, and a stream
+        # first created inside a capture -- then forking the engine's frontier
+        # stream off it (PINSAGE_CSR_FORK) and joining it back -- sent
+        # hipStreamEndCapture into unbounded recursion through its parallel
+        # capture-stream lists (a stack overflow: the native backtrace is one
+        # libamdhip64 frame repeated; tools/dbg/segv_bt.c).
         side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
         split = self.ahead_mode == "split"
         if split:
             if self.side is None:
                 self.side = torch.cuda.Stream()
+            self.side.wait_stream(torch.cuda.current_stream())
             self.gfr = []
         graphs = []
         for p in (0, 1):
@@ -738,10 +747,21 @@ class _FusedStep:
             with graph(ga):
                 cur = torch.cuda.current_stream()
 
+                def frontier_on_branch(q):
+                    # the engine forks nothing off this branch (engine.hip
+                    # frontier_fork_ok: a fork off a capture branch sent
+                    # hipStreamEndCapture into unbounded recursion)
+                    e = self.runner.engine
+                    nat.check(nat.lib().pinsage_engine_set_frontier_fork(e.h, 0), "set_frontier_fork")
+                    try:
+                        self._frontier(B, q)
+                    finally:
+                        nat.lib().pinsage_engine_set_frontier_fork(e.h, 1)
+
                 def fork_next_frontier():
                     side.wait_stream(cur)
                     with torch.cuda.stream(side):
-                        self._frontier(B, 1 - p)
+                        frontier_on_branch(1 - p)
 
                 # the next step's ids go to workspace 1-p, whose last user
                 # (the previous step) is done: graph launches are stream-ordered
@@ -759,7 +779,7 @@ class _FusedStep:
                     self._main(B, p, with_adam=adam, stage=stage)
                     side.wait_event(fork_ev)
                     with torch.cuda.stream(side):
-                        self._frontier(B, 1 - p)
+                        frontier_on_branch(1 - p)
                 elif self.ahead_mode == "start" or staged:
                     fork_next_frontier()
                     self._main(B, p, with_adam=adam, stage=stage)

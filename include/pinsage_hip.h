@@ -481,6 +481,11 @@ int pinsage_engine_set_tensors(pinsage_engine* e, const float* feats, int64_t ld
  * engine reads (pinsage_model.Runner.bind re-splits when the tensor's version
  * changes). */
 int pinsage_engine_set_feature_planes(pinsage_engine* e, const uint16_t* planes, int64_t plane_stride);
+/* on = 0: the engine's next pinsage_engine_frontier calls do not fork its
+ * side stream (PINSAGE_CSR_FORK), e.g. while the caller captures them on a
+ * branch of a graph (forking off a capture branch, not the capture's origin,
+ * sent hipStreamEndCapture into unbounded recursion); 1 (default) restores. */
+int pinsage_engine_set_frontier_fork(pinsage_engine* e, int on);
 /* Zero the workspace regions the step kernels keep zero after use (loss
  * scatter targets, CSR counters).  Call once per new workspace, before its
  * first forward. */

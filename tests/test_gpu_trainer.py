@@ -358,14 +358,19 @@ def test_engine_on_second_device_after_first_device_engine_destroyed():
             os.chdir(cwd)
 
 
-@pytest.mark.skipif(os.environ.get("PINSAGE_TEST_CSR_FORK") != "1",
-                    reason="diagnostic of the forked-frontier capture crash (DESIGN §5 round 6): "
-                           "PINSAGE_TEST_CSR_FORK=1 runs it")
 @pytest.mark.parametrize("fork", [2, 1])
 def test_step_capture_with_forked_csr_branch(fork, monkeypatch):
     """the step graphs captured with a fork onto the
     engine's side stream inside the frontier (PINSAGE_CSR_FORK: 2 = an empty
     branch, 1 = layer 0's CSR transpose on side[0] beside the upper layers').
+    The crash this reproduced (SIGSEGV in capture_end) was a stack overflow:
+    hipStreamEndCapture recursing without end through its parallel
+    capture-stream lists (tools/dbg/segv_bt.c: one libamdhip64 frame
+    repeated) when the engine forked its stream off the look-ahead BRANCH of
+    the step graph; the frontier graph's fork (off the capture's origin)
+    captured fine.  The trainer now turns the engine's frontier fork off while
+    it captures the frontier on a branch (pinsage_engine_set_frontier_fork),
+    so the frontier graph carries the fork and the look-ahead branch none.
     The fork's wait binds to an event recorded on the frontier's stream, and
     the join is recorded on the side stream and waited on the frontier's
     stream before engine_frontier returns -- so every captured graph (the
