@@ -133,6 +133,7 @@ _SIGS = {
     "pinsage_engine_set_tensors": (ctypes.c_int, [vp, vp, i64, vp, vp, i64, vp, vp, vp, vp]),
     "pinsage_engine_set_feature_planes": (ctypes.c_int, [vp, vp, i64]),
     "pinsage_engine_set_frontier_fork": (ctypes.c_int, [vp, ctypes.c_int]),
+    "pinsage_engine_set_feature_ilv": (ctypes.c_int, [vp, vp, i64]),
     "pinsage_engine_forward": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_forward_inference": (ctypes.c_int, [vp, vp, vp, i64, vp]),
     "pinsage_engine_frontier": (ctypes.c_int, [vp, vp, vp, i64, vp]),

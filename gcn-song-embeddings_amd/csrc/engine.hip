@@ -208,6 +208,13 @@ struct Engine {
   // transposed aggregation writing layer 0's dpq as planes too (lb.dpq3)
   const uint16_t* fplanes = nullptr;
   int64_t fplanes_ps = 0;
+  // the input feature table as its interleaved split-bf16 table [n][ld >= 3
+  // d_in] (pinsage_engine_set_feature_ilv; null: none): the layer-0 Q
+  // projection then reads each gathered row's 16-k stage as one 96-B piece and
+  // converts nothing (gemm.hip a_ilv), with Q0 split per step into the
+  // workspace's table (qw_ilv) beside the W planes (fwd.wsplit)
+  const uint16_t* f_ilv = nullptr;
+  int64_t f_ilv_ld = 0;
   // PINSAGE_WGRAD_PLANES=1: carve layer 0's dpq planes buffer so the planes
   // form can run (default 0: measured no faster -- C2 dQ0 53.4 us fp32 8-wave
   // form vs 54.0 us on planes, tools/wgrad_bench.py, round 6: the 12-KiB
@@ -245,6 +252,7 @@ struct Engine {
   // accumulation of repeated nodes' gradients (conv.hip det_put / rep_sum_kernel)
   size_t rank_off = 0, pos_sorted = 0, Gp = 0;
   size_t slab_main = 0, bslab_main = 0;  // split-K slabs of the main stream's weight gradient
+  size_t qw_ilv = 0;                     // Q0's interleaved split table [hid][3 d_in] (f_ilv)
   int64_t slab_floats = 0;
   // stream-K scratch of the main stream's GEMMs (gemm.h)
   size_t sk_slab = 0, sk_cnt = 0;
@@ -555,6 +563,7 @@ static void layout(Engine& E) {
     if (&lb == &E.L[0] && E.wgrad_planes) lb.dpq3 = carve(cur, 3 * FN * c.hid * 2);
   }
   const int64_t top = E.L.back().S.cap;
+  E.qw_ilv = carve(cur, c.hid * 3 * E.L[0].d * 2);
   E.ids = carve(cur, c.max_pos * 8 + 16);  // + Adam coefficients staged behind the ids
   E.pos_rank = carve(cur, c.max_pos * 4);
   E.H1 = carve(cur, top * c.out * 4);
@@ -762,6 +771,13 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
                                   st));
     }
   }
+  // Q0 on the feature table's interleaved split (f_ilv): Q0 split per step
+  const bool q0_ilv = E.f_ilv && E.L[0].d % 16 == 0;
+  if (q0_ilv) {
+    Timed ts(E, "fwd.wsplit_q", st);
+    PS_TRY(launch_split_ilv(E.params + E.L[0].pQw, E.L[0].d, c.hid, (int)E.L[0].d, at<uint16_t>(ws, E.qw_ilv),
+                            3 * E.L[0].d, st));
+  }
   int q_done = 0;  // this layer's q rows came out of the layer below's kernel (AggNextQ)
   int head_done = 0;  // the head ran inside the top layer's kernel (AggHead)
   for (int l = 0; l < Lc; ++l) {
@@ -785,6 +801,12 @@ int engine_layers(Engine& E, void* ws, hipStream_t st) {
     q.ldc = c.hid;
     q.bias = E.params + lb.pQb;
     q.act = true;
+    if (l == 0 && q0_ilv) {
+      q.a_ilv = E.f_ilv;
+      q.lda_ilv = E.f_ilv_ld;
+      q.b_ilv = at<uint16_t>(ws, E.qw_ilv);
+      q.ldb_ilv = 3 * lb.d;
+    }
     {
       Timed tt(E, lname("fwd.q_gemm", l), st);
       with_sk(E, ws, q);
@@ -1524,6 +1546,17 @@ int pinsage_engine_read_counts(const pinsage_engine* e, void* ws, int64_t* S, in
     PS_CHECK_HIP(hipMemcpy(&v, at<int>(ws, E->L[l].N.count), 4, hipMemcpyDeviceToHost));
     N[l] = v;
   }
+  return kOk;
+}
+
+int pinsage_engine_set_feature_ilv(pinsage_engine* e, const uint16_t* table, int64_t ld) {
+  if (!e || (table && (ld % 8 != 0 || ld < 3 * reinterpret_cast<Engine*>(e)->cfg.d_in))) {
+    set_error("engine_set_feature_ilv: bad argument (ld a multiple of 8, >= 3 d_in)");
+    return kErrArg;
+  }
+  Engine* E = reinterpret_cast<Engine*>(e);
+  E->f_ilv = table;
+  E->f_ilv_ld = table ? ld : 0;
   return kOk;
 }
 

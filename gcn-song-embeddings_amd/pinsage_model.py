@@ -988,6 +988,27 @@ class _EngineRunner:
             self._fpl_key = key
         return self._fpl
 
+    def feature_ilv(self, feats):
+        """The feature table's interleaved split-bf16 table [n, 3 d] (pinsage_split_ilv)
+        for the layer-0 Q projection, re-split whenever the tensor changes (its
+        version counter); None unless PINSAGE_Q0_ILV=1, for shapes the GEMM does not
+        take (d % 16), or above PINSAGE_FPLANES_MAX_GB (default 32)."""
+        if os.environ.get("PINSAGE_Q0_ILV", "0") != "1" or feats.dim() != 2:
+            return None
+        n, d = int(feats.shape[0]), int(feats.shape[1])
+        limit = float(os.environ.get("PINSAGE_FPLANES_MAX_GB", "32")) * 2 ** 30
+        if d % 16 or feats.stride(1) != 1 or feats.stride(0) % 4 or 6.0 * n * d > limit:
+            return None
+        key = (feats.data_ptr(), n, d, feats.stride(0), feats._version)
+        if getattr(self, "_filv_key", None) != key:
+            t = getattr(self, "_filv", None)
+            if t is None or tuple(t.shape) != (n, 3 * d) or t.device != feats.device:
+                t = self._filv = torch.empty((n, 3 * d), dtype=torch.int16, device=feats.device)
+            nat.check(nat.lib().pinsage_split_ilv(nat.ptr(feats), feats.stride(0), n, d, nat.ptr(t), 3 * d,
+                                                  nat.stream_ptr()), "split_ilv")
+            self._filv_key = key
+        return self._filv
+
     def bind(self, feats, table, grads=None, adam_m=None, adam_v=None, tabs=None):
         e = self.engine
         if table is not None:
@@ -1001,6 +1022,9 @@ class _EngineRunner:
         pl = self.feature_planes(feats)
         nat.check(nat.lib().pinsage_engine_set_feature_planes(e.h, nat.ptr(pl), pl[0].numel() if pl is not None else 0),
                   "engine_set_feature_planes")
+        ti = self.feature_ilv(feats)
+        nat.check(nat.lib().pinsage_engine_set_feature_ilv(e.h, nat.ptr(ti), ti.shape[1] if ti is not None else 0),
+                  "engine_set_feature_ilv")
 
     def run_forward(self, ws, ids_dev, inference=False):
         e = self.engine

@@ -919,6 +919,7 @@ class _FusedStep:
             # (the planes the graphs read: re-split in place if the features were
             # written in place since; a moved tensor changed the signature above)
             r.feature_planes(feats)
+            r.feature_ilv(feats)
             _tick("pre")
             return self._call_native(batch, B)  # (the captured graphs hold every pointer: no bind)
         r.bind(feats, table, grads=self.grads, adam_m=self.m, adam_v=self.v)

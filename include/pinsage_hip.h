@@ -486,6 +486,14 @@ int pinsage_engine_set_feature_planes(pinsage_engine* e, const uint16_t* planes,
  * branch of a graph (forking off a capture branch, not the capture's origin,
  * sent hipStreamEndCapture into unbounded recursion); 1 (default) restores. */
 int pinsage_engine_set_frontier_fork(pinsage_engine* e, int on);
+/* The input feature table's interleaved split-bf16 table [n][ld] (from
+ * pinsage_split_ilv(feats, ld_feats, n, d_in, table, ld); ld % 8 == 0, ld >=
+ * 3 d_in), or null: with it the layer-0 Q projection (pinsage_model.py:201)
+ * reads each gathered row's 16-k stage as one 96-B piece and converts nothing
+ * (Q0 is split per step into the workspace); bitwise the in-register split on
+ * the same 128 x 128 tiles.  The caller keeps the table equal to the split of
+ * the features the engine reads. */
+int pinsage_engine_set_feature_ilv(pinsage_engine* e, const uint16_t* table, int64_t ld);
 /* Zero the workspace regions the step kernels keep zero after use (loss
  * scatter targets, CSR counters).  Call once per new workspace, before its
  * first forward. */
