@@ -195,7 +195,6 @@ struct Engine {
   // still takes the chain's workgroups; PINSAGE_KW_SIDE_WG = their grid target
   int kw_side_form = getenv("PINSAGE_KW_SIDE_FORM") ? atoi(getenv("PINSAGE_KW_SIDE_FORM")) : 0;
   int kw_side_wg = getenv("PINSAGE_KW_SIDE_WG") ? atoi(getenv("PINSAGE_KW_SIDE_WG")) : 256;
-  int kw_main_form = getenv("PINSAGE_KW_MAIN_FORM") ? atoi(getenv("PINSAGE_KW_MAIN_FORM")) : 0;
   // PINSAGE_DQ_TREE (default 1): rows of the transposed aggregation split over
   // several chunks are summed by their chunk waves as a fixed fan-in-8 tree
   // (conv.hip dq_tree_leaf) instead of by a dq_combine launch after them
@@ -1014,7 +1013,7 @@ static int weight_grad(Engine& E, void* ws, const WGrad& w, hipStream_t st, cons
     k.slab = slab;
     k.bslab = bslab;
     k.cnt = at<int>(ws, main ? E.kw_cnt_main : E.kw_cnt_side);
-    k.form = main ? E.kw_main_form : E.kw_side_form;
+    k.form = main ? 0 : E.kw_side_form;  // (the main stream's dQ0 in the 64-KiB form: 0.391 -> 0.401 ms at C2)
     k.S = wgrad_kw_splits(w.M, w.N, w.K_hint > 0 ? std::min(w.K_hint, w.K_max) : w.K_max,
                           main ? 256 : E.kw_side_wg);
     PS_REQUIRE((int64_t)k.S * w.M * w.N <= E.slab_floats, kErrWorkspace, "engine: wgrad slab too small");
