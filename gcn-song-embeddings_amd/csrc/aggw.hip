@@ -38,7 +38,10 @@ constexpr int kAwTMax = 64;     // fanout held in LDS per row
 // slot lists.
 __device__ __forceinline__ int aw_lda(int K) { return K + 4; }
 
-__global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
+// HEAD: the model head's forward may be fused (hd.G1w set); without it the
+// kernel fits 128 VGPRs, so two 512-thread blocks share a CU (agg_w_nh_kernel)
+template <bool HEAD>
+__device__ __forceinline__ void agg_w_body(
     const float* __restrict__ h, int64_t ldh, int d, const int32_t* __restrict__ self_src,
     const float* __restrict__ q, int hid, const int32_t* __restrict__ loc,
     const float* __restrict__ wloc, int T, const int* __restrict__ nS, int64_t n_static,
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
     // and G2), fetched under the epilogue
     float4 hw1[8], hw2[8];
     float hb1 = 0.f;
-    if (hd.G1w) {
+    if (HEAD && hd.G1w) {
       const int hc = wave * 16 + l16;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -203,14 +206,14 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
       const float nrm = sqrtf(s2);
       const float4 yv = row < nrows ? make_float4(v[0] / nrm, v[1] / nrm, v[2] / nrm, v[3] / nrm)
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (hd.G1w) *reinterpret_cast<float4*>(sY + row * kAwHd + 4 * c4) = yv;
+      if (HEAD && hd.G1w) *reinterpret_cast<float4*>(sY + row * kAwHd + 4 * c4) = yv;
       if (row < nrows) {
         *reinterpret_cast<float4*>(y + (r0 + row) * kAwOut + 4 * c4) = yv;
         if (c4 == 0 && nrm_out) nrm_out[r0 + row] = nrm;
       }
     }
     __syncthreads();  // LDS is reused by the next tile (or the head below)
-    if (hd.G1w) {
+    if (HEAD && hd.G1w) {
       // ---- head: wave w, columns 16 w .. 16 w + 15 of H1 and Z; lane l
       // supplies row l16 and k = 32 g + s at step s (v_mfma_f32_16x16x4_f32)
       const int hc = wave * 16 + l16;
@@ -250,6 +253,24 @@ __global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(
     }
   }
 }
+
+#define PS_AW_ARGS                                                                                        \
+  const float *__restrict__ h, int64_t ldh, int d, const int32_t *__restrict__ self_src,                  \
+      const float *__restrict__ q, int hid, const int32_t *__restrict__ loc, const float *__restrict__ wloc, \
+      int T, const int *__restrict__ nS, int64_t n_static, const float *__restrict__ W,                    \
+      const float *__restrict__ bias, float *__restrict__ y, float *__restrict__ nrm_out,                  \
+      float *__restrict__ agg, AggHead hd
+__global__ __launch_bounds__(kAwThreads, 2) void agg_w_kernel(PS_AW_ARGS) {
+  agg_w_body<true>(h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm_out, agg, hd);
+}
+// no head: held to 128 VGPRs, so two blocks share a CU (one's gather beside
+// the other's products: PINSAGE_AGGW_NH, the 16-row form's launches without
+// the head)
+__global__ __launch_bounds__(kAwThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void agg_w_nh_kernel(
+    PS_AW_ARGS) {
+  agg_w_body<false>(h, ldh, d, self_src, q, hid, loc, wloc, T, nS, n_static, W, bias, y, nrm_out, agg, hd);
+}
+#undef PS_AW_ARGS
 
 typedef float aw_f32x16 __attribute__((ext_vector_type(16)));
 
@@ -700,8 +721,21 @@ int launch_agg_w(const float* h, int64_t ldh, int d, const int32_t* self_src, co
       hd = *head;
       if (head_done) *head_done = 1;
     }
-    hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
-                       loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, hd);
+    // PINSAGE_AGGW_NH (default 1): a launch without the head runs the
+    // 128-VGPR form (two blocks per CU; the with-head form compiles to more)
+    static const int nh = getenv("PINSAGE_AGGW_NH") ? atoi(getenv("PINSAGE_AGGW_NH")) : 1;
+    static bool prepared_nh = false;
+    if (!prepared_nh) {
+      PS_CHECK_HIP(hipFuncSetAttribute((const void*)agg_w_nh_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024));
+      prepared_nh = true;
+    }
+    if (nh && !hd.G1w)
+      hipLaunchKernelGGL(agg_w_nh_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
+                         loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, hd);
+    else
+      hipLaunchKernelGGL(agg_w_kernel, dim3(grid), dim3(kAwThreads), lds, st, h, ldh, d, self_src, q, hid,
+                         loc, wloc, T, nS, n_static, W, bias, y, nrm, agg, hd);
   }
   PS_CHECK_LAUNCH();
   return kOk;
