@@ -83,6 +83,8 @@ _SIGS = {
     "pinsage_frontier_local_idx": (ctypes.c_int, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "pinsage_linear": (ctypes.c_int, [vp, i64, vp, i64, i64, vp, vp, i64, ctypes.c_int, vp, i64, vp]),
     "pinsage_wgrad_scratch_bytes": (i64, [i64, i64]),
+    "pinsage_wgrad_probe": (ctypes.c_int, [i64, i64, vp, i64, vp, vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int,
+                                           vp]),
     "pinsage_wgrad_planes": (ctypes.c_int, [i64, i64, vp, i64, vp, i64, i64, vp, i64, i64, vp, vp, i64, vp,
                                             ctypes.c_int, vp, vp]),
     "pinsage_wgrad": (ctypes.c_int, [i64, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp,

@@ -560,6 +560,35 @@ int pinsage_wgrad(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const f
   return launch_wgrad_kw(p, (hipStream_t)stream);
 }
 
+int pinsage_wgrad_probe(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const float* A, const float* B,
+                        const int32_t* b_idx, float* dst, float* dst_b, int splits, void* scratch, int probe,
+                        void* stream) {
+  PS_REQUIRE(M > 0 && N > 0 && M <= INT32_MAX && N <= INT32_MAX && K_max >= 0 && K_max <= INT32_MAX &&
+                 splits >= 0 && scratch && probe >= 1 && probe <= 4,
+             kErrArg, "wgrad_probe: bad argument (probe 1-4)");
+  KwParams p;
+  p.A = A;
+  p.lda = M;
+  p.M = (int)M;
+  p.B = B;
+  p.ldb = N;
+  p.b_idx = b_idx;
+  p.N = (int)N;
+  p.K_dev = K_dev;
+  p.K_max = (int)K_max;
+  p.dst = dst;
+  p.ld_dst = N;
+  p.dst_b = dst_b;
+  char* sc = static_cast<char*>(scratch);
+  p.cnt = reinterpret_cast<int*>(sc);
+  sc += align_up(wgrad_kw_tickets((int)M, (int)N) * 4, 256);
+  p.slab = reinterpret_cast<float*>(sc);
+  sc += wgrad_kw_slab_floats((int)M, (int)N) * 4;
+  p.bslab = reinterpret_cast<float*>(sc);
+  p.S = splits;
+  return launch_wgrad_kw_probe(p, probe, (hipStream_t)stream);
+}
+
 int pinsage_wgrad_planes(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const uint16_t* A3, int64_t a3_ps,
                          int64_t lda, const uint16_t* B3, int64_t b3_ps, int64_t ldb, const int32_t* b_idx,
                          float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, void* stream) {

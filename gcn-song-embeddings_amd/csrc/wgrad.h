@@ -46,5 +46,8 @@ int64_t wgrad_kw_slab_floats(int M, int N);
 int64_t wgrad_kw_bslab_floats(int M);
 int64_t wgrad_kw_tickets(int M, int N);
 int launch_wgrad_kw(const KwParams& p, hipStream_t st);
+// timing-only k loops (probe 1-4: DMAs only, products only, without the split;
+// results are wrong) for tools/wgrad_bench.py through pinsage_wgrad_probe
+int launch_wgrad_kw_probe(const KwParams& p, int probe, hipStream_t st);
 
 }  // namespace ps

@@ -607,7 +607,12 @@ int64_t wgrad_kw_slab_floats(int M, int N) { return (int64_t)kKwMaxSplits * M * 
 int64_t wgrad_kw_bslab_floats(int M) { return (int64_t)kKwMaxSplits * M; }
 int64_t wgrad_kw_tickets(int M, int N) { return (int64_t)(M / kKwT) * (N / kKwT); }
 
-int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
+// probe: 0, or a timing-only build of the k loop (1-4, PROBE above: the
+// results are WRONG; only pinsage_wgrad_probe, a measurement entry, passes one)
+int launch_wgrad_kw_probe(const KwParams& p_in, int probe, hipStream_t st);
+int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) { return launch_wgrad_kw_probe(p_in, 0, st); }
+
+int launch_wgrad_kw_probe(const KwParams& p_in, int probe, hipStream_t st) {
   KwParams p = p_in;
   PS_REQUIRE(wgrad_kw_supported(p.M, p.N, p.N1, p.B2 != nullptr), kErrArg,
              "wgrad: M, N (and N1) must be multiples of 64");
@@ -622,7 +627,6 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   const int grid = (p.M / kKwT) * (p.N / kKwT) * p.S;
   // PINSAGE_KW_WAVES: 8 (default: 8 waves x 2-stage rings) or 4 (4 x 4)
   const int waves = getenv("PINSAGE_KW_WAVES") ? atoi(getenv("PINSAGE_KW_WAVES")) : 8;  // (per call: A/B)
-  const int probe = getenv("PINSAGE_KW_PROBE") ? atoi(getenv("PINSAGE_KW_PROBE")) : 0;  // (read per call)
   const bool gather = p.b_idx || p.b2_idx;
   if (p.A3 || p.B3) {  // pre-split operands
     PS_REQUIRE(p.A3 && p.B3 && !p.B2 && p.lda % 8 == 0 && p.ldb % 8 == 0, kErrArg,
@@ -638,7 +642,7 @@ int launch_wgrad_kw(const KwParams& p_in, hipStream_t st) {
   if (waves == 1) {  // PINSAGE_KW_WAVES=1: the register-ring k loop (REG), 8 waves
     if (gather) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 0, true>), dim3(grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, false, 0, true>), dim3(grid), dim3(512), 0, st, p);
-  } else if (probe >= 1 && probe <= 4) {  // timing diagnostics (tools/wgrad_bench.py): wrong results
+  } else if (probe >= 1 && probe <= 4) {  // timing diagnostics (pinsage_wgrad_probe): wrong results
     if (probe == 1) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 1>), dim3(grid), dim3(512), 0, st, p);
     else if (probe == 2) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 2>), dim3(grid), dim3(512), 0, st, p);
     else if (probe == 3) hipLaunchKernelGGL((wgrad_kw_kernel<8, 2, true, 3>), dim3(grid), dim3(512), 0, st, p);

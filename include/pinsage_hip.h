@@ -249,6 +249,13 @@ int pinsage_wgrad(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const f
  * form's 4-wave launch (PINSAGE_KW_WAVES=4) on the planes' source matrices;
  * dst_b sums the planes' value (H + M) + L.  The layer-0 Q weight gradient
  * (pinsage_model.py:201's AddmmBackward) in the engine. */
+/* Measurement only (tools/wgrad_bench.py): the weight-gradient launch with a
+ * timing-only k loop -- probe 1: the DMAs without the products, 2: the products
+ * without the DMAs, 3: 2 without the split, 4: the k loop without the split.
+ * The results are WRONG by construction; nothing in the engine calls it. */
+int pinsage_wgrad_probe(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const float* A, const float* B,
+                        const int32_t* b_idx, float* dst, float* dst_b, int splits, void* scratch, int probe,
+                        void* stream);
 int pinsage_wgrad_planes(int64_t M, int64_t N, const int* K_dev, int64_t K_max, const uint16_t* A3, int64_t a3_ps,
                          int64_t lda, const uint16_t* B3, int64_t b3_ps, int64_t ldb, const int32_t* b_idx,
                          float* dst, int64_t ld_dst, float* dst_b, int splits, void* scratch, void* stream);

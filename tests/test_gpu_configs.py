@@ -260,3 +260,34 @@ def test_autograd_call_above_the_position_csr_limit():
     fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), 2, 10, seed=3, cond=True)
     for a, p in zip(g1, m.parameters()):
         assert ((a - p.grad).norm() / a.norm()).item() <= 1e-6
+
+
+@pytest.mark.parametrize("hid", [256, 384])
+def test_fixed_cotangent_other_hidden_width(hid):
+    """A hidden width other than the reference's 512 (the engine's kernels take
+    any multiple of 64 that their forms support): hid 256 runs the transposed
+    aggregation's one-float4-per-lane form with its split-row tree, hid 384 its
+    two-float4 form with a partial second column pass; the weight gradients'
+    64 x 64 tiles cover M = hid.  Forward rows and every parameter gradient
+    against the oracle under a fixed cotangent, popular tracks and repeated ids
+    included (pinsage_model.py:189-265)."""
+    import graph
+    import pinsage_model as pm
+    import synthetic
+    n = 3000
+    pg = synthetic.make_playlist_graph(n, 600, 40000, seed=17)
+    indptr, indices = pg.csr()
+    g = graph.CSRGraph.from_csr(indptr, indices)
+    feats = torch.from_numpy(synthetic.make_features(n, 128, seed=18))
+    pm.set_rng_mode("philox")
+    try:
+        torch.manual_seed(0)
+        w, nb = pm.precompute_neighborhoods_topt(g, n, 200, 0.85, 100, None)
+    finally:
+        pm.set_rng_mode("mt19937")
+    rng = np.random.default_rng(hid)
+    ids = rng.integers(0, n, 240)
+    ids[10:20] = ids[0]
+    torch.manual_seed(3)
+    m = pm.PinSageModel(g, n, 2, (128, hid, 128), 200, 0.85, 10, (w, nb))
+    fixed_cotangent_check(m, feats, ids, w.numpy(), nb.numpy(), 2, 10, seed=hid)

@@ -77,13 +77,11 @@ def main():
                 (N - n1) if B2 is not None else 0, vp(dst), N, vp(db), S, vp(sc), None, None, None, None, None,
                 None, None, 0.9, 0.999, 1e-8, st), "wgrad"), a.reps)
         os.environ.pop("PINSAGE_KW_WAVES")
-        for probe in ("1", "2", "3", "4"):  # wgrad.hip PROBE (timing, wrong results)
-            os.environ["PINSAGE_KW_PROBE"] = probe
-            res[f"probe{probe} S=auto"] = timed(lambda: nat.check(L.pinsage_wgrad(
-                M, N, vp(K_dev), K, vp(A), M, vp(B), n1, vp(idx), n1 if B2 is not None else -1, vp(B2),
-                (N - n1) if B2 is not None else 0, vp(dst), N, vp(db), 0, vp(sc), None, None, None, None, None,
-                None, None, 0.9, 0.999, 1e-8, st), "wgrad"), a.reps)
-            os.environ.pop("PINSAGE_KW_PROBE")
+        if n1 == N:  # timing-only k loops (pinsage_wgrad_probe: results wrong by construction)
+            for probe in (1, 2, 3, 4):
+                res[f"probe{probe} S=auto"] = timed(lambda: nat.check(L.pinsage_wgrad_probe(
+                    M, N, vp(K_dev), K, vp(A), vp(B), vp(idx), vp(dst), vp(db), 0, vp(sc), probe, st),
+                    "wgrad_probe"), a.reps)
         if n1 == N:  # both operands pre-split (pinsage_wgrad_planes)
             A3 = torch.empty((3, A.shape[0], M), dtype=torch.int16, device="cuda")
             B3 = torch.empty((3, B.shape[0], N), dtype=torch.int16, device="cuda")
