@@ -193,8 +193,10 @@ struct Engine {
   // the side stream's long-K weight gradients run beside the chain's kernels:
   // PINSAGE_KW_SIDE_FORM 1 = the 64-KiB form (wgrad.hip), so a CU holding one
   // still takes the chain's workgroups; PINSAGE_KW_SIDE_WG = their grid target
+  // (128: half the CUs, so the chain's dq / dY W launches beside them keep the
+  // rest; C4 -4 us, C4 B 4096 -23 us, C2 / C3 even against 256)
   int kw_side_form = getenv("PINSAGE_KW_SIDE_FORM") ? atoi(getenv("PINSAGE_KW_SIDE_FORM")) : 0;
-  int kw_side_wg = getenv("PINSAGE_KW_SIDE_WG") ? atoi(getenv("PINSAGE_KW_SIDE_WG")) : 256;
+  int kw_side_wg = getenv("PINSAGE_KW_SIDE_WG") ? atoi(getenv("PINSAGE_KW_SIDE_WG")) : 128;
   // PINSAGE_DQ_TREE (default 1): rows of the transposed aggregation split over
   // several chunks are summed by their chunk waves as a fixed fan-in-8 tree
   // (conv.hip dq_tree_leaf) instead of by a dq_combine launch after them

@@ -400,7 +400,8 @@ def test_frontier_ahead_matches_serial_step(mode):
                                      ("PINSAGE_FUSED_NEXT_Q", "0", "1"), ("PINSAGE_HEAD_IN_AGGW", "0", "1"),
                                      ("PINSAGE_FORK_PLAN", "0", "7"), ("PINSAGE_FORK_PLAN", "0", "3"),
                                      ("PINSAGE_KW_SIDE_FORM", "0", "1"), ("PINSAGE_DQ_TREE", "0", "1"),
-                                     ("PINSAGE_WGRAD_PLANES", "0", "1"), ("PINSAGE_Q0_ILV", "0", "1")])
+                                     ("PINSAGE_WGRAD_PLANES", "0", "1"), ("PINSAGE_Q0_ILV", "0", "1"),
+                                     ("PINSAGE_KW_SIDE_WG", "128", "256")])
 def test_engine_variants_train_alike(var, a, b, monkeypatch):
     """Engine variants that change only launch order or summation order train
     alike -- same published losses (the monitors' output) and parameters within
@@ -421,7 +422,8 @@ def test_engine_variants_train_alike(var, a, b, monkeypatch):
     gradient on pre-split bf16 planes of dpq and of the features: the same
     products, 4-wave partial order) and PINSAGE_Q0_ILV (the layer-0 Q
     projection on the feature table's interleaved split, Q0 split per step:
-    the same products, no stream-K)."""
+    the same products, no stream-K) and PINSAGE_KW_SIDE_WG (the side weight
+    gradients' grid target: other K-split counts, so other summation order)."""
     if var != "PINSAGE_HEAD_IN_AGGW":  # (the head is fused into the 16-row form only)
         monkeypatch.setenv("PINSAGE_AGGW32_MIN_ROWS", "0")
     import graph

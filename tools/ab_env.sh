@@ -1,7 +1,7 @@
 # A/B of one engine env knob on bench.py: tools/ab_env.sh VAR "A B A B" [bench args]
 set -o pipefail
 var=$1; vals=$2; shift 2
-out=gpurun_out/ab_$var
+out=gpurun_out/ab_$var${AB_TAG:+_$AB_TAG}
 mkdir -p $out
 i=0
 for v in $vals; do
