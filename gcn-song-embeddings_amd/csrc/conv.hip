@@ -2037,8 +2037,10 @@ int launch_dq_chunks(const int2* chunks, const int* nchunks, int64_t max_chunks,
                      int32_t* csrc, const int* cbase, int* tk, uint16_t* dpq3, int64_t ps3) {
   PS_REQUIRE(hid % 4 == 0, kErrArg, "dq: hidden dim must be a multiple of 4");
   // persistent waves (each prefetches its next chunk); 512 to 4096 blocks
-  // measured alike at C2 (round 5), 2048 kept
-  const int grid = grid_for(max_chunks * 64, 256, 2048);
+  // measured alike at C2 (round 5), 1024 to 8192 at C2 and C4 (round 6), 2048
+  // kept (PINSAGE_DQ_GRID: the cap, A/B)
+  static const int grid_cap = getenv("PINSAGE_DQ_GRID") ? std::max(1, atoi(getenv("PINSAGE_DQ_GRID"))) : 2048;
+  const int grid = grid_for(max_chunks * 64, 256, grid_cap);
   if (csrc) {  // chunk rows: masked partials in part, no combine
     PS_REQUIRE(q_src, kErrArg, "dq: chunk rows need the rows' source indices");
     if (hid >= 512)
